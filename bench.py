@@ -1,0 +1,219 @@
+"""SdP-Net forward benchmark on MI355X (BASELINE.json metric).
+
+  python bench.py [--gpus N --steps K --warmup W]       (N>1: under torch.distributed.run)
+
+Workload (BASELINE.json configs[1]): SdP-Net-M (12 blocks, d=768, patch 16,
+canonical config SURVEY.md §0) bf16 eval forward, batch 256 synthetic N(0,1)
+224x224 images per GPU, random-init weights (reference init), inputs resident in
+HBM before timing.  A step = one full forward of one batch (logits), replayed
+from a HIP graph captured after warmup.  Multi-GPU: one process per GPU, each
+its own independent batch shard (weak scaling), no data-path collective; barrier
++ max-over-ranks timing only.
+
+Also reported on the same JSON line:
+  roofline     — dominant kernel (gemm_bf16_256x256, ~98 % of FLOPs): algorithmic
+                 FLOPs of its launches / their HIP-event durations (on the launch
+                 stream), vs the dense bf16 MFMA peak.
+  cpu_baseline — the oracle (the reference's math in stock PyTorch CPU ops,
+                 oracle/sdpnet_oracle.py) on this host's cores, bounded sample,
+                 rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "sdp-net_amd"))
+
+METRIC = "images/sec fwd SdP-Net-M 224×224 bs=256 @1 GPU; scaling 1/2/4/8"
+MFMA_BF16_PEAK_TFLOPS = 2516.6   # 256 CU x 2.4 GHz x 4096 FLOP/clk/CU (dense)
+
+M_CFG = dict(embedding_dim=768, num_blocks=12, n_head=8, activation="gelu", embedding_activation="none",
+             conv_kernel_size=7, patch_size=16, ffn_dropout=0.2, attn_dropout=0.2, output_classes=1000,
+             conv_block_num=2, ff_multiplication_factor=4, max_image_size=[16, 16], max_num_registers=5,
+             conv_first=True, head_output_from_register=True, simple_mlp_output=False, output_head_bias=False,
+             normalize_qv=True, stochastic_depth_p=[0.0, 0.0], mixer_deptwise_bias=False, mixer_ffn_bias=False,
+             conv_embedding=False, conv_embedding_kernel_size=5)
+
+
+def flops_per_image(cfg, img=224, num_registers=3):
+    """2*MAC over every conv (incl. depthwise), GEMM and attention QK^T + PV
+    (M = 88.933 GF)."""
+    C, p, k = cfg["embedding_dim"], cfg["patch_size"], cfg["conv_kernel_size"]
+    P = (img // p) ** 2
+    R = min(num_registers + 1, cfg["max_num_registers"])
+    N = R + P
+    mf = cfg["ff_multiplication_factor"]
+    patch = 2 * P * C * 3 * p * p
+    mixer = 2 * P * C * k * k + 2 * P * C * C + 2 * 2 * P * C * 4 * C
+    enc = 2 * N * C * 3 * C + 2 * N * C * C + 2 * 2 * N * C * mf * C + 2 * 2 * N * N * C
+    ncls = cfg["output_classes"]
+    head = 2 * C * ncls + 2 * ncls * ncls
+    return patch + cfg["num_blocks"] * (cfg["conv_block_num"] * mixer + enc) + enc + head
+
+
+def cpu_baseline(model_cpu_sd, cfg, seconds=12.0):
+    import torch
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import sdpnet_oracle as orc
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    bs = 16
+    x = torch.randn(bs, 3, 224, 224)
+    orc.forward(x[:2], model_cpu_sd, cfg)  # warm
+    n, t0 = 0, time.perf_counter()
+    while True:
+        orc.forward(x, model_cpu_sd, cfg)
+        n += bs
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"SdP-Net-M fp32 eval forward, {n} images in batches of {bs}, {dt:.1f} s, "
+                      f"oracle/sdpnet_oracle.py (reference math, stock torch CPU ops)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--prof-steps", type=int, default=2)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import model as sdp
+    import sdpnet_hip as sp
+
+    torch.manual_seed(231424314)  # model_train.py:61
+    m = sdp.MainModel.from_dict(**M_CFG).eval()
+    cpu_sd = {k: v.detach().clone() for k, v in m.state_dict().items()} if rank == 0 else None
+    m = m.to(dev)
+    B = args.batch
+    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
+    x = torch.randn(B, 3, 224, 224, generator=g).to(dev).to(torch.bfloat16)   # resident in HBM
+
+    def step():
+        return m(x)
+
+    for _ in range(max(1, args.warmup)):
+        y = step()
+    torch.cuda.synchronize()
+    graph = None
+    if not args.no_graph:
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step()
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            y = step()
+        graph.replay()
+        torch.cuda.synchronize()
+    run = graph.replay if graph is not None else step
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    assert torch.isfinite(y.float()).all()
+
+    # ---- dominant-kernel roofline: HIP events around every GEMM launch -------------
+    rec = {}
+
+    def timer(name, key, flops, e0, e1):
+        rec.setdefault(key, []).append((flops, e0, e1))
+
+    old = sp.set_launch_timer(timer)
+    try:
+        for _ in range(max(1, args.prof_steps)):
+            step()
+    finally:
+        sp.set_launch_timer(old)
+    torch.cuda.synchronize()
+    fast_fl = fast_ms = 0.0
+    fast_n = 0
+    per_shape = {}
+    for key, lst in rec.items():
+        ms = sum(e0.elapsed_time(e1) for _, e0, e1 in lst)
+        fl = sum(f for f, _, _ in lst)
+        per_shape[f"{key[0]}x{key[1]}x{key[2]}"] = dict(launches=len(lst), avg_us=round(1e3 * ms / len(lst), 2),
+                                                        tflops=round(fl / (ms * 1e-3) / 1e12, 1),
+                                                        kernel="gemm_bf16_256x256" if key[3] == 1 else "gemm_generic")
+        if key[3] == 1:
+            fast_fl += fl
+            fast_ms += ms
+            fast_n += len(lst)
+    achieved = fast_fl / (fast_ms * 1e-3) / 1e12 if fast_ms else 0.0
+
+    gf = flops_per_image(M_CFG) / 1e9
+    total_imgs = B * args.steps * world
+    value = total_imgs / el
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * el / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic N(0,1) 224x224 images resident in HBM; random-init weights (reference init)",
+        "config": {"workload": "SdP-Net-M eval forward (12 blocks, d=768, patch 16, 200 tokens), "
+                               "bf16 storage / fp32 accumulate, HIP-graph replay",
+                   "global_batch": B * world, "per_gpu_batch": B, "image": 224, "tokens": 200,
+                   "parallelism": f"dp{world} independent batch shards (no collective)"},
+        "model_flops_per_image_gf": round(gf, 3),
+        "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
+        "roofline": {"bound": "mfma", "kernel": "gemm_bf16_256x256",
+                     "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "launches_per_step": fast_n // max(1, args.prof_steps),
+                     "avg_launch_us": round(1e3 * fast_ms / max(1, fast_n), 2),
+                     "algorithmic_gflop_per_launch": round(fast_fl / max(1, fast_n) / 1e9, 3),
+                     "per_shape": per_shape},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cpu_sd, M_CFG)
+        cb = out["cpu_baseline"]["value"]
+        out["gpu_over_cpu"] = round(value / cb, 1) if cb else None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,141 @@
+/*
+ * sdpnet_hip.h — C ABI of libsdpnet_hip.so, the MI355X (gfx950) kernels of the
+ * SdP-Net forward hot path (y-akbal/SdP-Net @ 2025-06-14).
+ *
+ * The reference is pure Python on stock ATen ops; it has no FFI of its own.
+ * Each entry point below replaces the ATen call(s) a reference forward makes at
+ * the cited file:line; the Python host side (sdp-net_amd/sdpnet_hip.py, bound with
+ * ctypes) mirrors the reference's nn.Module surface on top of these.
+ *
+ * Conventions (all entry points):
+ *   - dtype codes: 0 = fp32, 1 = bf16 (uint16 bit pattern).  Arithmetic is fp32.
+ *   - Every buffer is caller-owned device memory; kernels never allocate.
+ *   - `stream` is a hipStream_t; launches are asynchronous on it, no host sync.
+ *     Everything is graph-capturable.
+ *   - Return value: 0 on success, else a hipError_t code (1 = invalid argument).
+ *   - Row maps.  Row-addressed operands take (grp, gstride, off): logical row m
+ *     lives at physical row (m / grp) * gstride + off + (m % grp), times the row
+ *     stride `ld` (in elements).  grp <= 0 means "dense" (physical = logical).
+ *     This addresses the image rows of the persistent [B, R+P, C] token buffer
+ *     (grp = P, gstride = R+P, off = R) without gather/scatter copies.
+ *   - Activation codes: 0 none, 1 gelu (exact erf), 2 relu, 3 tanh, 4 sigmoid,
+ *     5 leaky_relu (0.01), 6 selu, 7 kelu (model.py:13-24,
+ *     training_utilities.py:91-92).
+ */
+#ifndef SDPNET_HIP_H
+#define SDPNET_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Version string of the library build. */
+const char* sdp_version(void);
+
+/*
+ * Y[m, n] = epi( sum_k X[m, k] * W[n, k] ),  W stored [N][K] (torch Linear /
+ * 1x1-conv layout).  epi: v = acc + bias[n]; if (resid_pre) v += R[m, n];
+ * v = act(v); if (!resid_pre) v += R[m, n].  bias fp32 or NULL, R or NULL.
+ * Replaces: nn.Conv2d 1x1 of ConvMixer (layers.py:79-91), q/k/v/o_proj and
+ * ff_linear1/2 (layers.py:242-249, :282-284, :301, :308), the patch conv as a
+ * GEMM on im2col rows (layers.py:34-42) with the positional add of
+ * EmbeddingLayer fused (layers.py:162-163), the head Linears (layers.py:445-459).
+ * bf16 with K % 64 == 0 runs the 256x256x64 MFMA kernel; everything else the
+ * masked generic kernel (fp32 uses exact v_mfma_f32_16x16x4_f32).
+ */
+int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+             const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+             int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
+             int64_t y_gstride, int y_off, int M, int N, int K, int act, int resid_pre,
+             void* stream);
+/* Which kernel sdp_gemm picks for a shape: 1 = 256x256 MFMA, 0 = generic. */
+int sdp_gemm_variant(int dtype, int M, int N, int K);
+/* Test hook: force the generic kernel (returns the previous setting). */
+int sdp_gemm_force_generic(int on);
+
+/*
+ * Row LayerNorm over C contiguous channels, fp32 statistics, biased variance.
+ * Replaces: channel LayerNorm of ConvMixer (layers.py:12-24, eps 1e-6) on the
+ * token layout; nn.LayerNorm norm1/norm2 (layers.py:252-253, eps 1e-5); the
+ * head LayerNorm (layers.py:445, :449).
+ */
+int sdp_layernorm(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                  const float* gamma, const float* beta, float eps, void* Y, int64_t ldy,
+                  int y_grp, int64_t y_gstride, int y_off, int M, int C, void* stream);
+
+/*
+ * In-place LayerNorm over each head_dim segment of the q and k thirds of the
+ * fused QKV rows [rows, ld >= 3C]: q_norm / k_norm (layers.py:236-237, :286).
+ */
+int sdp_qk_headnorm(int dtype, void* QKV, int64_t ld, int64_t rows, int n_head, int head_dim,
+                    const float* q_gamma, const float* q_beta, const float* k_gamma,
+                    const float* k_beta, float eps, void* stream);
+
+/*
+ * Depthwise k x k conv, zero "same" padding, NHWC token rows (pixel (b,h,w) is
+ * logical row b*H*W + h*W + w).  weight fp32 [C][k][k], bias fp32 [C] or NULL.
+ * Replaces: nn.Conv2d(C, C, k, groups=C, padding="same") (layers.py:73-78).
+ * k in {1,3,5,7,9}.
+ */
+int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+               const float* weight, const float* bias, void* Y, int64_t ldy, int y_grp,
+               int64_t y_gstride, int y_off, int B, int H, int W, int C, int k, void* stream);
+
+/*
+ * softmax(Q K^T / sqrt(hd) + mask) V per (batch, head) from fused QKV rows
+ * [B*N, ld_qkv] (q | k | v thirds), output rows [B*N, ld_o] (heads concatenated).
+ * mask: optional fp32 additive [.., N, N] with batch / head strides (0 =
+ * broadcast).  Replaces F.scaled_dot_product_attention (layers.py:289-291) and
+ * the manual softmax path (layers.py:292-298).
+ */
+int sdp_attention(int dtype, const void* QKV, int64_t ld_qkv, void* O, int64_t ld_o, int B, int N,
+                  int n_head, int head_dim, const float* mask, int64_t mask_sb, int64_t mask_sh,
+                  void* stream);
+/* 1 if sdp_attention takes the LDS-resident MFMA kernel for this shape. */
+int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask);
+
+/*
+ * im2col of the patch conv: image [B,3,Hi,Wi] -> rows [B*(Hi/p)*(Wi/p), Kpad],
+ * column c*p*p + i*p + j, zero padded to Kpad.  (ConvPatcher, layers.py:34-42.)
+ */
+int sdp_patchify(int dtype_in, const void* img, int dtype_out, void* out, int B, int Hi, int Wi,
+                 int p, int Kpad, void* stream);
+
+/* T[h*W + w][c] = Eh[h][c] + Ew[w][c]   (EmbeddingLayer, layers.py:157-163). */
+int sdp_pos_table(const float* eh, const float* ew, float* out, int H, int W, int C, void* stream);
+
+/* T[h*W + w][c] = mean_{k x k} bone[c][h+i][w+j]  (ConvEmbedding, layers.py:205). */
+int sdp_avgpool_table(const float* bone, int BH, int BW, float* out, int H, int W, int C, int k,
+                      void* stream);
+
+/* dst[b*gstride + r*ldd + c] = src[b*sgstride + r*lds + c]; sgstride = 0 expands
+ * the register table over the batch (layers.py:166, :208), otherwise it copies
+ * the register rows in/out of the token buffer (layers.py:275, :311). */
+int sdp_copy_rows(int dtype_src, const void* src, int64_t lds, int64_t sgstride, int dtype_dst,
+                  void* dst, int64_t ldd, int64_t gstride, int B, int R, int C, void* stream);
+
+/* In place x[b][c][hw] += table[hw][c] on NCHW (standalone EmbeddingLayer.forward,
+ * layers.py:162-163), and y = act(x) elementwise (its activation, :168). */
+int sdp_nchw_add_table(int dtype, void* X, const float* table, int B, int C, int HW, void* stream);
+int sdp_act(int dtype, const void* X, void* Y, int64_t n, int act, void* stream);
+
+/* out[g][c] = mean over `rows` consecutive logical rows of X: registers.mean(-2)
+ * (layers.py:464) and AdaptiveAvgPool2d((1,1)) + Flatten (layers.py:457-458). */
+int sdp_group_mean(int dtype_in, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                   int dtype_out, void* out, int64_t ldo, int G, int rows, int C, void* stream);
+
+/* NCHW [B,C,HW] <-> token rows (layers.py:271, :314). */
+int sdp_nchw_to_rows(int dtype_in, const void* X, int dtype_out, void* Y, int64_t ldy, int y_grp,
+                     int64_t y_gstride, int y_off, int B, int C, int HW, void* stream);
+int sdp_rows_to_nchw(int dtype_in, const void* X, int64_t ldx, int x_grp, int64_t x_gstride,
+                     int x_off, int dtype_out, void* Y, int B, int C, int HW, void* stream);
+
+/* Element cast fp32 <-> bf16 (weight cache preparation, output conversion). */
+int sdp_cast(int dtype_in, const void* X, int dtype_out, void* Y, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDPNET_HIP_H */

@@ -1,0 +1,80 @@
+// Shared device helpers for the SdP-Net gfx950 kernels.
+// Storage types: float (fp32 path) and bf16 (uint16 bit pattern, bf16 path).
+// All arithmetic is fp32; bf16 is storage only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+#include "sdpnet_hip.h"
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) short bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+#define SDP_DEV __device__ __forceinline__
+
+SDP_DEV float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+SDP_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+template <typename T> SDP_DEV float to_f(T v);
+template <> SDP_DEV float to_f<float>(float v) { return v; }
+template <> SDP_DEV float to_f<bf16_t>(bf16_t v) { return bf2f(v); }
+
+template <typename T> SDP_DEV T from_f(float v);
+template <> SDP_DEV float from_f<float>(float v) { return v; }
+template <> SDP_DEV bf16_t from_f<bf16_t>(float v) { return f2bf(v); }
+
+// ---- activations: model.py:13-24 registry, training_utilities.py:91-92 (KeLu)
+enum SdpAct {
+  ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_SIGMOID = 4,
+  ACT_LEAKY_RELU = 5, ACT_SELU = 6, ACT_KELU = 7
+};
+
+SDP_DEV float apply_act(int act, float x) {
+  switch (act) {
+    case ACT_GELU: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));  // exact erf GELU
+    case ACT_RELU: return fmaxf(x, 0.0f);
+    case ACT_TANH: return tanhf(x);
+    case ACT_SIGMOID: return 1.0f / (1.0f + expf(-x));
+    case ACT_LEAKY_RELU: return x >= 0.0f ? x : 0.01f * x;
+    case ACT_SELU: {
+      const float alpha = 1.6732632423543772848f, scale = 1.0507009873554804934f;
+      return scale * (x > 0.0f ? x : alpha * (expf(x) - 1.0f));
+    }
+    case ACT_KELU: {
+      const float a = 3.5f;
+      if (x < -a) return 0.0f;
+      if (x > a) return x;
+      return 0.5f * x * (1.0f + x / a + 0.31830988618379067f * sinf(x * 3.14159265358979323846f / a));
+    }
+    default: return x;
+  }
+}
+
+// Grouped row map: logical row m -> physical row (m / grp) * gstride + off + (m % grp).
+// Lets one kernel address the image rows of a [B, R+P, C] token buffer (grp=P,
+// gstride=R+P, off=R), a plain dense matrix (grp=huge, gstride=0, off=0), or a
+// table broadcast over the batch (grp=P, gstride=0, off=0).
+struct RowMap {
+  int grp;
+  int off;
+  int64_t gstride;
+  SDP_DEV int64_t operator()(int64_t m) const {
+    return (m / grp) * gstride + off + (m % grp);
+  }
+};
+
+SDP_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+SDP_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+#define SDP_CHECK_LAUNCH() (int)hipGetLastError()

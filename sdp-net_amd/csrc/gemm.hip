@@ -1,0 +1,341 @@
+// Dense contractions of the SdP-Net forward on gfx950 MFMA.
+//
+// Every GEMM on the hot path has the nn.Linear / 1x1-conv form
+//     Y[m, n] = epilogue( sum_k X[m, k] * W[n, k] )
+// with W stored [N][K] (K contiguous) exactly as torch keeps Linear weights and
+// 1x1-conv weights ([out, in, 1, 1]).  Call sites: layers.py:79-91 (1x1 convs of
+// ConvMixer), layers.py:242-249 / :282-284 / :301 / :308 (q/k/v/o projections and
+// FFN of EncoderLayer), layers.py:34-42 (patch conv as a GEMM over im2col rows),
+// layers.py:449-454 (classification head).
+//
+// Epilogue (fused, fp32):  v = acc + bias[n];  if (resid_pre) v += R[m,n];
+//                          v = act(v);         if (!resid_pre) v += R[m,n];
+// covers  act(conv)+x  (ConvMixer), x + FFN (+bias) (Encoder), pos-emb add +
+// embedding activation (EmbeddingLayer), Tanh (head).
+//
+// Two kernels:
+//  * gemm_bf16_256x256 — the hot kernel: 256x256x64 tiles, 8 waves (2 along M x
+//    4 along N, 128x64 per wave), v_mfma_f32_16x16x32_bf16, both operands staged
+//    HBM->LDS by global_load_lds_dwordx4 into an XOR-swizzled [row][64] image
+//    (conflict-free ds_read_b128), two LDS stages, XCD-aware tile order.
+//    Requires K % 64 == 0; any M, N (clamped loads, masked stores).
+//  * gemm_generic<T> — correctness path for fp32 (exact f32 MFMA
+//    v_mfma_f32_16x16x4_f32) and for odd bf16 shapes; fully masked.
+//
+// The MFMA is issued "swapped" (A-operand = W rows, B-operand = X rows) so the
+// accumulator holds D[n][m] with 4 consecutive n per lane: every epilogue
+// access (bias, residual, output) is an 8/16-byte vector per lane.
+#include "common.h"
+
+#define AS1 __attribute__((address_space(1)))
+#define AS3 __attribute__((address_space(3)))
+
+template <typename T>
+struct Epi {
+  const float* bias;   // [N] or null
+  const T* resid;      // or null
+  int64_t ldr;
+  RowMap rmap;
+  T* out;
+  int64_t ldc;
+  RowMap cmap;
+  int act;
+  int resid_pre;
+};
+
+// Apply the epilogue to 4 consecutive columns n..n+3 of logical row m.
+template <typename T>
+SDP_DEV void epi_store4(const Epi<T>& e, int64_t m, int n, int N, f32x4 acc) {
+  float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+  const bool full = (n + 3 < N);
+  if (e.bias) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += (full || n + r < N) ? e.bias[n + r] : 0.f;
+  }
+  float rv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (e.resid) {
+    const T* rp = e.resid + e.rmap(m) * e.ldr + n;
+    if constexpr (sizeof(T) == 2) {
+      if (full && ((((uintptr_t)rp) & 7) == 0)) {
+        bf16x4 rr = *(const bf16x4*)rp;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rv[r] = bf2f((bf16_t)rr[r]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) if (n + r < N) rv[r] = to_f<T>(rp[r]);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) if (n + r < N) rv[r] = to_f<T>(rp[r]);
+    }
+  }
+  if (e.resid && e.resid_pre) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += rv[r];
+  }
+  if (e.act != ACT_NONE) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = apply_act(e.act, v[r]);
+  }
+  if (e.resid && !e.resid_pre) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += rv[r];
+  }
+  T* op = e.out + e.cmap(m) * e.ldc + n;
+  if constexpr (sizeof(T) == 2) {
+    if (full && ((((uintptr_t)op) & 7) == 0)) {
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
+      *(bf16x4*)op = o;
+      return;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) if (n + r < N) op[r] = from_f<T>(v[r]);
+}
+
+// ---------------------------------------------------------------------------
+// Hot kernel: bf16, 256x256x64, glds double buffer.
+// ---------------------------------------------------------------------------
+namespace fast {
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int TILE_BYTES = BM * BK * 2;       // 32 KiB per operand per stage
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;   // A + W
+constexpr int NTHREADS = 512;
+
+// LDS image of one operand tile: [256 rows][64 bf16] = 128 B per row, 16-B chunk
+// c of row r stored at chunk position c ^ ((r >> 1) & 7): a 16-lane ds_read_b128
+// group reading one logical chunk of 16 consecutive rows hits 16 distinct 4-bank
+// slots (conflict-free).
+SDP_DEV int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// Issue the 4 global_load_lds_dwordx4 pieces of one 256x64 tile for this wave.
+// A piece = 8 rows x 128 B = one wave-instruction (lane-linear LDS destination),
+// so the swizzle is applied to the per-lane SOURCE chunk (involution).
+SDP_DEV void stage_tile(const bf16_t* __restrict__ base, int64_t ld, RowMap map, int row0,
+                        int nrows, int k0, char* lds_tile, int wave, int lane) {
+  const int rr = lane >> 3;          // row inside the piece
+  const int pc = lane & 7;           // physical chunk this lane fills
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i;  // 0..31
+    const int r = piece * 8 + rr;
+    const int c = swz(r, pc);        // logical chunk to fetch
+    int grow = row0 + r;
+    grow = grow < nrows ? grow : nrows - 1;  // clamp (tail rows are never stored)
+    const bf16_t* src = base + map(grow) * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const AS1 void*)src, (AS3 void*)(lds_tile + piece * 1024), 16, 0, 0);
+  }
+}
+
+SDP_DEV bf16x8 lds_frag(const char* lds_tile, int r, int c) {
+  return *(const bf16x8*)(lds_tile + r * 128 + swz(r, c) * 16);
+}
+
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_256x256(
+    const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap, const bf16_t* __restrict__ W,
+    int64_t ldw, Epi<bf16_t> epi, int M, int N, int K, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+
+  // XCD-aware, bijective block -> tile remap: blocks b and b+8 share an XCD,
+  // give each XCD a contiguous range of tiles (row-panel major, N fastest) so
+  // concurrently resident blocks on one L2 share X row panels and W panels.
+  const int nwg = tiles_m * tiles_n;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2;  // 0..1  -> 128 rows of X each
+  const int wn = wave & 3;   // 0..3  -> 64 rows of W each
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const RowMap wmap{0x7fffffff, 0, 0};
+  const int nk = K / BK;
+  stage_tile(X, ldx, xmap, m0, M, 0, smem, wave, lane);
+  stage_tile(W, ldw, wmap, n0, N, 0, smem + TILE_BYTES, wave, lane);
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE_BYTES;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
+      stage_tile(X, ldx, xmap, m0, M, (kt + 1) * BK, nxt, wave, lane);
+      stage_tile(W, ldw, wmap, n0, N, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+    }
+    const char* xt = cur;
+    const char* wt = cur + TILE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + fq;
+      bf16x8 bx[8], aw[4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bx[j] = lds_frag(xt, wm * 128 + j * 16 + fr, c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) aw[i] = lds_frag(wt, wn * 64 + i * 16 + fr, c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[i], bx[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // D[n][m]: lane holds n = base + 4*fq + r, m = base + fr.
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int m = m0 + wm * 128 + j * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + wn * 64 + i * 16 + fq * 4;
+      if (n < N) epi_store4<bf16_t>(epi, m, n, N, acc[i][j]);
+    }
+  }
+}
+}  // namespace fast
+
+// ---------------------------------------------------------------------------
+// Generic masked kernel (fp32 exact-MFMA path and odd bf16 shapes).
+// 64x64 tile, BK=32, 4 waves (2x2, 32x32 each), register-staged LDS.
+// ---------------------------------------------------------------------------
+namespace gen {
+constexpr int BM = 64, BN = 64, BK = 32, PAD = 8, LDK = BK + PAD;
+
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_generic(const T* __restrict__ X, int64_t ldx, RowMap xmap,
+                                                    const T* __restrict__ W, int64_t ldw, Epi<T> epi,
+                                                    int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) T xs[BM * LDK];
+  __shared__ __attribute__((aligned(16))) T ws[BN * LDK];
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < K; k0 += BK) {
+#pragma unroll
+    for (int it = 0; it < (BM * BK) / 256; ++it) {
+      const int idx = tid + it * 256;
+      const int r = idx / BK, c = idx % BK;
+      const int gm = m0 + r, gn = n0 + r, gk = k0 + c;
+      T xv = from_f<T>(0.f), wv = from_f<T>(0.f);
+      if (gm < M && gk < K) xv = X[xmap(gm) * ldx + gk];
+      if (gn < N && gk < K) wv = W[(int64_t)gn * ldw + gk];
+      xs[r * LDK + c] = xv;
+      ws[r * LDK + c] = wv;
+    }
+    __syncthreads();
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 bx[2], aw[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bx[j] = *(const bf16x8*)&xs[(wm * 32 + j * 16 + fr) * LDK + fq * 8];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) aw[i] = *(const bf16x8*)&ws[(wn * 32 + i * 16 + fr) * LDK + fq * 8];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[i], bx[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 4) {
+        float bx[2], aw[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bx[j] = xs[(wm * 32 + j * 16 + fr) * LDK + kk + fq];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) aw[i] = ws[(wn * 32 + i * 16 + fr) * LDK + kk + fq];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(aw[i], bx[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int m = m0 + wm * 32 + j * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = n0 + wn * 32 + i * 16 + fq * 4;
+      if (n < N) epi_store4<T>(epi, m, n, N, acc[i][j]);
+    }
+  }
+}
+}  // namespace gen
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+static RowMap mk_map(int grp, int64_t gstride, int off) {
+  RowMap r;
+  r.grp = grp > 0 ? grp : 0x7fffffff;
+  r.gstride = grp > 0 ? gstride : 0;
+  r.off = grp > 0 ? off : 0;
+  return r;
+}
+
+// Returns the kernel variant chosen for the shape (for tests / profiling).
+extern "C" int sdp_gemm_variant(int dtype, int M, int N, int K) {
+  if (dtype == 1 && K % fast::BK == 0 && K >= fast::BK && M >= 128 && N >= 128) return 1;
+  return 0;
+}
+
+static int g_force_generic = 0;
+extern "C" int sdp_gemm_force_generic(int on) {
+  int old = g_force_generic;
+  g_force_generic = on;
+  return old;
+}
+
+extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                        const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+                        int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
+                        int64_t y_gstride, int y_off, int M, int N, int K, int act, int resid_pre,
+                        void* stream) {
+  if (M < 0 || N <= 0 || K <= 0 || !X || !W || !Y) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const RowMap xm = mk_map(x_grp, x_gstride, x_off);
+  const RowMap rm = mk_map(r_grp, r_gstride, r_off);
+  const RowMap ym = mk_map(y_grp, y_gstride, y_off);
+  if (dtype == 1) {
+    Epi<bf16_t> e{bias, (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, act, resid_pre};
+    if (!g_force_generic && sdp_gemm_variant(dtype, M, N, K) == 1) {
+      const int tm = (M + fast::BM - 1) / fast::BM, tn = (N + fast::BN - 1) / fast::BN;
+      hipLaunchKernelGGL(fast::gemm_bf16_256x256, dim3(tm * tn), dim3(fast::NTHREADS), 0, s,
+                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn);
+    } else {
+      dim3 grid((M + gen::BM - 1) / gen::BM, (N + gen::BN - 1) / gen::BN);
+      hipLaunchKernelGGL(gen::gemm_generic<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)X, ldx, xm,
+                         (const bf16_t*)W, ldw, e, M, N, K);
+    }
+  } else if (dtype == 0) {
+    Epi<float> e{bias, (const float*)R, ldr, rm, (float*)Y, ldy, ym, act, resid_pre};
+    dim3 grid((M + gen::BM - 1) / gen::BM, (N + gen::BN - 1) / gen::BN);
+    hipLaunchKernelGGL(gen::gemm_generic<float>, grid, dim3(256), 0, s, (const float*)X, ldx, xm,
+                       (const float*)W, ldw, e, M, N, K);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  return SDP_CHECK_LAUNCH();
+}

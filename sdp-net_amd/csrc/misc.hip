@@ -1,0 +1,307 @@
+// Layout / embedding kernels around the SdP-Net hot path.
+//
+//  * sdp_patchify   — im2col for the stride = kernel = p patch conv
+//                     (ConvPatcher, layers.py:34-42): image [B,3,Hi,Wi] ->
+//                     rows [B*Hp*Wp, Kpad], column c*p*p + i*p + j (the flattened
+//                     conv weight order), zero pad to Kpad (multiple of 64).
+//  * sdp_pos_table  — EmbeddingLayer positional table (layers.py:157-163):
+//                     T[h*W + w] = Eh[h] + Ew[w]  ('horizontal' table by row h,
+//                     'vertical' by column w).
+//  * sdp_avgpool_table — ConvEmbedding (layers.py:205): T[h*W+w][c] =
+//                     mean_{k x k} bone[c][h+i][w+j].
+//  * sdp_copy_rows  — strided row copy; with a zero source batch stride it is the
+//                     register expansion over the batch (layers.py:166, :208)
+//                     into token rows 0..R-1, else the register split (:311).
+//  * sdp_nchw_add_table / sdp_act — standalone EmbeddingLayer.forward
+//                     (in-place positional add on NCHW, layers.py:162-163, then
+//                     the embedding activation) outside the fused model path.
+//  * sdp_group_mean — mean over groups of rows: registers.mean(-2) of the head
+//                     (layers.py:464) and the AdaptiveAvgPool2d((1,1)) head (:457).
+//  * sdp_nchw_to_rows / sdp_rows_to_nchw — NCHW <-> token rows (the
+//                     flatten/transpose of layers.py:271, :314), LDS-tiled.
+//  * sdp_cast       — fp32 <-> bf16 element cast.
+#include "common.h"
+
+static RowMap mk_map3(int grp, int64_t gstride, int off) {
+  RowMap r;
+  r.grp = grp > 0 ? grp : 0x7fffffff;
+  r.gstride = grp > 0 ? gstride : 0;
+  r.off = grp > 0 ? off : 0;
+  return r;
+}
+
+template <typename TI, typename TO>
+__global__ void patchify_k(const TI* __restrict__ img, TO* __restrict__ out, int B, int Hi, int Wi, int p, int Hp,
+                           int Wp, int Kpad) {
+  const int64_t total = (int64_t)B * Hp * Wp * Kpad;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int col = (int)(idx % Kpad);
+    const int64_t row = idx / Kpad;
+    float v = 0.f;
+    if (col < 3 * p * p) {
+      const int c = col / (p * p), ij = col % (p * p), i = ij / p, j = ij % p;
+      const int pw = (int)(row % Wp);
+      const int64_t t = row / Wp;
+      const int ph = (int)(t % Hp);
+      const int b = (int)(t / Hp);
+      v = to_f<TI>(img[(((int64_t)b * 3 + c) * Hi + ph * p + i) * Wi + pw * p + j]);
+    }
+    out[idx] = from_f<TO>(v);
+  }
+}
+
+extern "C" int sdp_patchify(int dtype_in, const void* img, int dtype_out, void* out, int B, int Hi, int Wi, int p,
+                            int Kpad, void* stream) {
+  if (!img || !out || p <= 0 || Kpad < 3 * p * p) return (int)hipErrorInvalidValue;
+  const int Hp = Hi / p, Wp = Wi / p;
+  const int64_t total = (int64_t)B * Hp * Wp * Kpad;
+  if (total == 0) return 0;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_in == 0 && dtype_out == 1)
+    hipLaunchKernelGGL((patchify_k<float, bf16_t>), dim3(blocks), dim3(256), 0, s, (const float*)img, (bf16_t*)out, B, Hi, Wi, p, Hp, Wp, Kpad);
+  else if (dtype_in == 0 && dtype_out == 0)
+    hipLaunchKernelGGL((patchify_k<float, float>), dim3(blocks), dim3(256), 0, s, (const float*)img, (float*)out, B, Hi, Wi, p, Hp, Wp, Kpad);
+  else if (dtype_in == 1 && dtype_out == 1)
+    hipLaunchKernelGGL((patchify_k<bf16_t, bf16_t>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)img, (bf16_t*)out, B, Hi, Wi, p, Hp, Wp, Kpad);
+  else if (dtype_in == 1 && dtype_out == 0)
+    hipLaunchKernelGGL((patchify_k<bf16_t, float>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)img, (float*)out, B, Hi, Wi, p, Hp, Wp, Kpad);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+__global__ void pos_table_k(const float* __restrict__ eh, const float* __restrict__ ew, float* __restrict__ out, int H,
+                            int W, int C) {
+  const int64_t total = (int64_t)H * W * C;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(idx % C);
+    const int64_t hw = idx / C;
+    const int h = (int)(hw / W), w = (int)(hw % W);
+    out[idx] = eh[(int64_t)h * C + c] + ew[(int64_t)w * C + c];
+  }
+}
+
+extern "C" int sdp_pos_table(const float* eh, const float* ew, float* out, int H, int W, int C, void* stream) {
+  if (!eh || !ew || !out || H <= 0 || W <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)H * W * C;
+  hipLaunchKernelGGL(pos_table_k, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, eh, ew, out, H, W, C);
+  return SDP_CHECK_LAUNCH();
+}
+
+__global__ void avgpool_table_k(const float* __restrict__ bone, int BH, int BW, float* __restrict__ out, int H, int W,
+                                int C, int k) {
+  const int64_t total = (int64_t)H * W * C;
+  const float inv = 1.0f / (float)(k * k);
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(idx % C);
+    const int64_t hw = idx / C;
+    const int h = (int)(hw / W), w = (int)(hw % W);
+    float s = 0.f;
+    for (int i = 0; i < k; ++i)
+      for (int j = 0; j < k; ++j) s += bone[((int64_t)c * BH + h + i) * BW + w + j];
+    out[idx] = s * inv;
+  }
+}
+
+extern "C" int sdp_avgpool_table(const float* bone, int BH, int BW, float* out, int H, int W, int C, int k,
+                                 void* stream) {
+  if (!bone || !out || H + k - 1 > BH || W + k - 1 > BW) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)H * W * C;
+  hipLaunchKernelGGL(avgpool_table_k, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, bone, BH, BW, out, H, W, C, k);
+  return SDP_CHECK_LAUNCH();
+}
+
+template <typename TI, typename TO>
+__global__ void broadcast_rows_k(const TI* __restrict__ src, int64_t lds, int64_t sgstride, TO* __restrict__ dst,
+                                 int64_t ldd, int64_t gstride, int B, int R, int C) {
+  const int64_t total = (int64_t)B * R * C;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(idx % C);
+    const int64_t br = idx / C;
+    const int r = (int)(br % R), b = (int)(br / R);
+    dst[b * gstride + (int64_t)r * ldd + c] = from_f<TO>(to_f<TI>(src[b * sgstride + (int64_t)r * lds + c]));
+  }
+}
+
+// dst[b*gstride + r*ldd + c] = src[b*sgstride + r*lds + c]  (sgstride 0 = broadcast)
+extern "C" int sdp_copy_rows(int dtype_src, const void* src, int64_t lds, int64_t sgstride, int dtype_dst, void* dst,
+                             int64_t ldd, int64_t gstride, int B, int R, int C, void* stream) {
+  if (!src || !dst || B < 0 || R < 0 || C <= 0) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)B * R * C;
+  if (total == 0) return 0;
+  dim3 grid((unsigned)std::min<int64_t>((total + 255) / 256, 4096));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_src == 0 && dtype_dst == 1)
+    hipLaunchKernelGGL((broadcast_rows_k<float, bf16_t>), grid, dim3(256), 0, s, (const float*)src, lds, sgstride, (bf16_t*)dst, ldd, gstride, B, R, C);
+  else if (dtype_src == 0 && dtype_dst == 0)
+    hipLaunchKernelGGL((broadcast_rows_k<float, float>), grid, dim3(256), 0, s, (const float*)src, lds, sgstride, (float*)dst, ldd, gstride, B, R, C);
+  else if (dtype_src == 1 && dtype_dst == 1)
+    hipLaunchKernelGGL((broadcast_rows_k<bf16_t, bf16_t>), grid, dim3(256), 0, s, (const bf16_t*)src, lds, sgstride, (bf16_t*)dst, ldd, gstride, B, R, C);
+  else if (dtype_src == 1 && dtype_dst == 0)
+    hipLaunchKernelGGL((broadcast_rows_k<bf16_t, float>), grid, dim3(256), 0, s, (const bf16_t*)src, lds, sgstride, (float*)dst, ldd, gstride, B, R, C);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// out[g][c] = mean_{i < rows} X[xm(g*rows + i)][c]
+template <typename TI, typename TO>
+__global__ void group_mean_k(const TI* __restrict__ X, int64_t ldx, RowMap xm, TO* __restrict__ out, int64_t ldo,
+                             int G, int rows, int C) {
+  const int g = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C || g >= G) return;
+  float s = 0.f;
+  for (int i = 0; i < rows; ++i) s += to_f<TI>(X[xm((int64_t)g * rows + i) * ldx + c]);
+  out[(int64_t)g * ldo + c] = from_f<TO>(s / (float)rows);
+}
+
+extern "C" int sdp_group_mean(int dtype_in, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                              int dtype_out, void* out, int64_t ldo, int G, int rows, int C, void* stream) {
+  if (!X || !out || G < 0 || rows <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+  if (G == 0) return 0;
+  const RowMap xm = mk_map3(x_grp, x_gstride, x_off);
+  dim3 grid((C + 255) / 256, G);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_in == 1 && dtype_out == 1)
+    hipLaunchKernelGGL((group_mean_k<bf16_t, bf16_t>), grid, dim3(256), 0, s, (const bf16_t*)X, ldx, xm, (bf16_t*)out, ldo, G, rows, C);
+  else if (dtype_in == 1 && dtype_out == 0)
+    hipLaunchKernelGGL((group_mean_k<bf16_t, float>), grid, dim3(256), 0, s, (const bf16_t*)X, ldx, xm, (float*)out, ldo, G, rows, C);
+  else if (dtype_in == 0 && dtype_out == 0)
+    hipLaunchKernelGGL((group_mean_k<float, float>), grid, dim3(256), 0, s, (const float*)X, ldx, xm, (float*)out, ldo, G, rows, C);
+  else if (dtype_in == 0 && dtype_out == 1)
+    hipLaunchKernelGGL((group_mean_k<float, bf16_t>), grid, dim3(256), 0, s, (const float*)X, ldx, xm, (bf16_t*)out, ldo, G, rows, C);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// NCHW [B, C, HW] <-> rows: row (b, hw) -> ym(b*HW + hw), element c.  64x64 LDS tile.
+template <typename TI, typename TO, bool TO_ROWS>
+__global__ __launch_bounds__(256) void transpose_k(const TI* __restrict__ src, TO* __restrict__ dst, int64_t ld,
+                                                   RowMap rm, int C, int HW) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.z;
+  const int c0 = blockIdx.y * 64, p0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  if (TO_ROWS) {
+    // read NCHW: consecutive threads -> consecutive hw
+    for (int i = ty; i < 64; i += 4) {
+      const int c = c0 + i, p = p0 + tx;
+      tile[i][tx] = (c < C && p < HW) ? to_f<TI>(src[((int64_t)b * C + c) * HW + p]) : 0.f;
+    }
+    __syncthreads();
+    for (int i = ty; i < 64; i += 4) {
+      const int p = p0 + i, c = c0 + tx;
+      if (c < C && p < HW) dst[rm((int64_t)b * HW + p) * ld + c] = from_f<TO>(tile[tx][i]);
+    }
+  } else {
+    for (int i = ty; i < 64; i += 4) {
+      const int p = p0 + i, c = c0 + tx;
+      tile[tx][i] = (c < C && p < HW) ? to_f<TI>(src[rm((int64_t)b * HW + p) * ld + c]) : 0.f;
+    }
+    __syncthreads();
+    for (int i = ty; i < 64; i += 4) {
+      const int c = c0 + i, p = p0 + tx;
+      if (c < C && p < HW) dst[((int64_t)b * C + c) * HW + p] = from_f<TO>(tile[i][tx]);
+    }
+  }
+}
+
+template <bool TO_ROWS>
+static int launch_transpose(int dti, const void* src, int dto, void* dst, int64_t ld, RowMap rm, int B, int C,
+                            int HW, hipStream_t s) {
+  dim3 grid((HW + 63) / 64, (C + 63) / 64, B);
+#define SDP_T(TI, TO) hipLaunchKernelGGL((transpose_k<TI, TO, TO_ROWS>), grid, dim3(256), 0, s, (const TI*)src, (TO*)dst, ld, rm, C, HW)
+  if (dti == 0 && dto == 0) SDP_T(float, float);
+  else if (dti == 0 && dto == 1) SDP_T(float, bf16_t);
+  else if (dti == 1 && dto == 0) SDP_T(bf16_t, float);
+  else if (dti == 1 && dto == 1) SDP_T(bf16_t, bf16_t);
+  else return (int)hipErrorInvalidValue;
+#undef SDP_T
+  return SDP_CHECK_LAUNCH();
+}
+
+extern "C" int sdp_nchw_to_rows(int dtype_in, const void* X, int dtype_out, void* Y, int64_t ldy, int y_grp,
+                                int64_t y_gstride, int y_off, int B, int C, int HW, void* stream) {
+  if (!X || !Y || B < 0 || C <= 0 || HW <= 0) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  return launch_transpose<true>(dtype_in, X, dtype_out, Y, ldy, mk_map3(y_grp, y_gstride, y_off), B, C, HW,
+                                (hipStream_t)stream);
+}
+
+extern "C" int sdp_rows_to_nchw(int dtype_in, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                                int dtype_out, void* Y, int B, int C, int HW, void* stream) {
+  if (!X || !Y || B < 0 || C <= 0 || HW <= 0) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  return launch_transpose<false>(dtype_in, X, dtype_out, Y, ldx, mk_map3(x_grp, x_gstride, x_off), B, C, HW,
+                                 (hipStream_t)stream);
+}
+
+template <typename TI, typename TO>
+__global__ void cast_k(const TI* __restrict__ x, TO* __restrict__ y, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = from_f<TO>(to_f<TI>(x[i]));
+}
+
+extern "C" int sdp_cast(int dtype_in, const void* X, int dtype_out, void* Y, int64_t n, void* stream) {
+  if (!X || !Y || n < 0) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  dim3 grid((unsigned)std::min<int64_t>((n + 255) / 256, 8192));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_in == 0 && dtype_out == 1) hipLaunchKernelGGL((cast_k<float, bf16_t>), grid, dim3(256), 0, s, (const float*)X, (bf16_t*)Y, n);
+  else if (dtype_in == 1 && dtype_out == 0) hipLaunchKernelGGL((cast_k<bf16_t, float>), grid, dim3(256), 0, s, (const bf16_t*)X, (float*)Y, n);
+  else if (dtype_in == 0 && dtype_out == 0) hipLaunchKernelGGL((cast_k<float, float>), grid, dim3(256), 0, s, (const float*)X, (float*)Y, n);
+  else if (dtype_in == 1 && dtype_out == 1) hipLaunchKernelGGL((cast_k<bf16_t, bf16_t>), grid, dim3(256), 0, s, (const bf16_t*)X, (bf16_t*)Y, n);
+  else return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// x[b][c][hw] += table[hw][c]  (in place, NCHW)
+template <typename T>
+__global__ void nchw_add_table_k(T* __restrict__ x, const float* __restrict__ table, int B, int C, int HW) {
+  const int64_t total = (int64_t)B * C * HW;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int hw = (int)(i % HW);
+    const int c = (int)((i / HW) % C);
+    x[i] = from_f<T>(to_f<T>(x[i]) + table[(int64_t)hw * C + c]);
+  }
+}
+
+extern "C" int sdp_nchw_add_table(int dtype, void* X, const float* table, int B, int C, int HW, void* stream) {
+  if (!X || !table || B < 0 || C <= 0 || HW <= 0) return (int)hipErrorInvalidValue;
+  const int64_t n = (int64_t)B * C * HW;
+  if (n == 0) return 0;
+  dim3 grid((unsigned)std::min<int64_t>((n + 255) / 256, 8192));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 1) hipLaunchKernelGGL(nchw_add_table_k<bf16_t>, grid, dim3(256), 0, s, (bf16_t*)X, table, B, C, HW);
+  else if (dtype == 0) hipLaunchKernelGGL(nchw_add_table_k<float>, grid, dim3(256), 0, s, (float*)X, table, B, C, HW);
+  else return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+template <typename T>
+__global__ void act_k(const T* __restrict__ x, T* __restrict__ y, int64_t n, int act) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = from_f<T>(apply_act(act, to_f<T>(x[i])));
+}
+
+extern "C" int sdp_act(int dtype, const void* X, void* Y, int64_t n, int act, void* stream) {
+  if (!X || !Y || n < 0) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  dim3 grid((unsigned)std::min<int64_t>((n + 255) / 256, 8192));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 1) hipLaunchKernelGGL(act_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)X, (bf16_t*)Y, n, act);
+  else if (dtype == 0) hipLaunchKernelGGL(act_k<float>, grid, dim3(256), 0, s, (const float*)X, (float*)Y, n, act);
+  else return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+extern "C" const char* sdp_version(void) { return "sdpnet-hip gfx950 r1"; }

@@ -1,0 +1,283 @@
+"""ctypes binding of libsdpnet_hip.so (include/sdpnet_hip.h) + thin tensor wrappers.
+
+This is the only place Python touches the C ABI.  Every wrapper:
+  * checks device / dtype / contiguity / shape on the host,
+  * passes raw device pointers and sizes (no torch types cross the boundary),
+  * launches on the caller's current HIP stream (torch.cuda.current_stream()),
+  * raises RuntimeError naming the op if the library returns a non-zero code.
+
+There is no fallback: if the shared library is missing or cannot be loaded,
+``lib()`` raises, and every op that needs it raises with it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SDPNET_HIP_LIB", os.path.join(_HERE, "lib", "libsdpnet_hip.so"))
+
+F32, BF16 = 0, 1
+ACT_CODES = {"none": 0, "gelu": 1, "relu": 2, "tanh": 3, "sigmoid": 4, "leaky_relu": 5, "selu": 6, "kelu": 7}
+
+_i32, _i64, _f32, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+_ROWMAP = [_i32, _i64, _i32]
+
+# Signatures, in the order of include/sdpnet_hip.h.
+_SIGS = {
+    "sdp_version": ([], ctypes.c_char_p),
+    "sdp_gemm": ([_i32, _vp, _i64, *_ROWMAP, _vp, _i64, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP,
+                  _i32, _i32, _i32, _i32, _i32, _vp], _i32),
+    "sdp_gemm_variant": ([_i32, _i32, _i32, _i32], _i32),
+    "sdp_gemm_force_generic": ([_i32], _i32),
+    "sdp_layernorm": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _f32, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
+    "sdp_qk_headnorm": ([_i32, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp], _i32),
+    "sdp_dwconv": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _i32, _i32, _i32, _vp],
+                   _i32),
+    "sdp_attention": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _vp], _i32),
+    "sdp_attention_variant": ([_i32, _i32, _i32, _i32, _i32], _i32),
+    "sdp_patchify": ([_i32, _vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp], _i32),
+    "sdp_pos_table": ([_vp, _vp, _vp, _i32, _i32, _i32, _vp], _i32),
+    "sdp_avgpool_table": ([_vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp], _i32),
+    "sdp_copy_rows": ([_i32, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _i32, _i32, _i32, _vp], _i32),
+    "sdp_nchw_add_table": ([_i32, _vp, _vp, _i32, _i32, _i32, _vp], _i32),
+    "sdp_act": ([_i32, _vp, _vp, _i64, _i32, _vp], _i32),
+    "sdp_group_mean": ([_i32, _vp, _i64, *_ROWMAP, _i32, _vp, _i64, _i32, _i32, _i32, _vp], _i32),
+    "sdp_nchw_to_rows": ([_i32, _vp, _i32, _vp, _i64, *_ROWMAP, _i32, _i32, _i32, _vp], _i32),
+    "sdp_rows_to_nchw": ([_i32, _vp, _i64, *_ROWMAP, _i32, _vp, _i32, _i32, _i32, _vp], _i32),
+    "sdp_cast": ([_i32, _vp, _i32, _vp, _i64, _vp], _i32),
+}
+
+_lib = None
+
+# Optional launch timer (bench.py roofline): callable(name, shape_key, flops, start_evt, end_evt)
+_TIMER = None
+
+
+def set_launch_timer(fn):
+    global _TIMER
+    old = _TIMER
+    _TIMER = fn
+    return old
+
+
+def lib():
+    """Load libsdpnet_hip.so (after torch, so it binds torch's HIP runtime)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"sdpnet: HIP extension not built: {LIB_PATH} is missing "
+                               "(run `python -c 'import __graft_entry__ as g; g.build()'` or `make -C sdp-net_amd/csrc`)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS.keys())
+
+
+def _check(rc: int, name: str):
+    if rc != 0:
+        raise RuntimeError(f"sdpnet HIP op {name} failed with hip error code {rc}")
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def dcode(dtype: torch.dtype) -> int:
+    if dtype == torch.float32:
+        return F32
+    if dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"sdpnet HIP path supports float32 and bfloat16, got {dtype}")
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("sdpnet HIP op called with a CPU tensor; the HIP path has no CPU fallback")
+
+
+@dataclass
+class Rows:
+    """A row-addressed operand: logical row m -> physical row
+    (m // grp) * gstride + off + m % grp of ``t`` (row stride ``ld`` elements).
+    grp <= 0: dense."""
+    t: torch.Tensor
+    ld: int
+    grp: int = 0
+    gstride: int = 0
+    off: int = 0
+
+    def args(self):
+        return [self.t.data_ptr(), self.ld, self.grp, self.gstride, self.off]
+
+    def map(self):
+        return [self.grp, self.gstride, self.off]
+
+
+def dense(t: torch.Tensor) -> Rows:
+    assert t.is_contiguous()
+    return Rows(t, t.shape[-1])
+
+
+# ---------------------------------------------------------------------------
+def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Optional[torch.Tensor] = None,
+         resid: Optional[Rows] = None, act: int = 0, resid_pre: bool = False):
+    _need_cuda(x.t, w, y.t, bias)
+    dt = dcode(x.t.dtype)
+    assert w.dtype == x.t.dtype == y.t.dtype and w.is_contiguous() and w.shape[0] >= N
+    assert bias is None or (bias.dtype == torch.float32 and bias.is_contiguous())
+    if resid is not None:
+        assert resid.t.dtype == x.t.dtype
+        r = [resid.t.data_ptr(), resid.ld, *resid.map()]
+    else:
+        r = [None, 0, 0, 0, 0]
+    timer = _TIMER
+    if timer is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    rc = lib().sdp_gemm(dt, *x.args(), w.data_ptr(), w.stride(0), _ptr(bias), *r, *y.args(), M, N, K, act,
+                        int(bool(resid_pre)), _stream(y.t))
+    _check(rc, "gemm")
+    if timer is not None:
+        e1.record()
+        timer("gemm", (M, N, K, lib().sdp_gemm_variant(dt, M, N, K)), 2.0 * M * N * K, e0, e1)
+
+
+def layernorm(x: Rows, gamma: torch.Tensor, beta: torch.Tensor, eps: float, y: Rows, M: int, C: int):
+    _need_cuda(x.t, y.t, gamma, beta)
+    dt = dcode(x.t.dtype)
+    assert y.t.dtype == x.t.dtype and gamma.dtype == beta.dtype == torch.float32
+    rc = lib().sdp_layernorm(dt, *x.args(), gamma.data_ptr(), beta.data_ptr(), float(eps), *y.args(), M, C,
+                             _stream(y.t))
+    _check(rc, "layernorm")
+
+
+def qk_headnorm(qkv: torch.Tensor, rows: int, n_head: int, head_dim: int, gq, bq, gk, bk, eps: float = 1e-5):
+    _need_cuda(qkv, gq, bq, gk, bk)
+    rc = lib().sdp_qk_headnorm(dcode(qkv.dtype), qkv.data_ptr(), qkv.stride(0), rows, n_head, head_dim,
+                               gq.data_ptr(), bq.data_ptr(), gk.data_ptr(), bk.data_ptr(), float(eps), _stream(qkv))
+    _check(rc, "qk_headnorm")
+
+
+def dwconv(x: Rows, weight: torch.Tensor, bias: Optional[torch.Tensor], y: Rows, B: int, H: int, W: int, C: int,
+           k: int):
+    _need_cuda(x.t, y.t, weight, bias)
+    assert weight.dtype == torch.float32 and weight.is_contiguous()
+    rc = lib().sdp_dwconv(dcode(x.t.dtype), *x.args(), weight.data_ptr(), _ptr(bias), *y.args(), B, H, W, C, k,
+                          _stream(y.t))
+    _check(rc, "dwconv")
+
+
+def attention(qkv: torch.Tensor, out: torch.Tensor, B: int, N: int, n_head: int, head_dim: int,
+              mask: Optional[torch.Tensor] = None, mask_sb: int = 0, mask_sh: int = 0):
+    _need_cuda(qkv, out, mask)
+    assert qkv.dtype == out.dtype
+    rc = lib().sdp_attention(dcode(qkv.dtype), qkv.data_ptr(), qkv.stride(0), out.data_ptr(), out.stride(0), B, N,
+                             n_head, head_dim, _ptr(mask), mask_sb, mask_sh, _stream(out))
+    _check(rc, "attention")
+
+
+def patchify(img: torch.Tensor, out: torch.Tensor, p: int, kpad: int):
+    _need_cuda(img, out)
+    assert img.is_contiguous() and img.dim() == 4 and img.shape[1] == 3
+    B, _, Hi, Wi = img.shape
+    rc = lib().sdp_patchify(dcode(img.dtype), img.data_ptr(), dcode(out.dtype), out.data_ptr(), B, Hi, Wi, p, kpad,
+                            _stream(out))
+    _check(rc, "patchify")
+
+
+def pos_table(eh: torch.Tensor, ew: torch.Tensor, out: torch.Tensor, H: int, W: int, C: int):
+    _need_cuda(eh, ew, out)
+    rc = lib().sdp_pos_table(eh.data_ptr(), ew.data_ptr(), out.data_ptr(), H, W, C, _stream(out))
+    _check(rc, "pos_table")
+
+
+def avgpool_table(bone: torch.Tensor, out: torch.Tensor, H: int, W: int, C: int, k: int):
+    _need_cuda(bone, out)
+    assert bone.is_contiguous() and bone.dtype == torch.float32
+    rc = lib().sdp_avgpool_table(bone.data_ptr(), bone.shape[-2], bone.shape[-1], out.data_ptr(), H, W, C, k,
+                                 _stream(out))
+    _check(rc, "avgpool_table")
+
+
+def copy_rows(src: torch.Tensor, lds: int, sgstride: int, dst: torch.Tensor, ldd: int, gstride: int, B: int,
+              R: int, C: int, src_offset_rows: int = 0, dst_offset_rows: int = 0):
+    _need_cuda(src, dst)
+    sp = src.data_ptr() + src_offset_rows * lds * src.element_size()
+    dp = dst.data_ptr() + dst_offset_rows * ldd * dst.element_size()
+    rc = lib().sdp_copy_rows(dcode(src.dtype), sp, lds, sgstride, dcode(dst.dtype), dp, ldd, gstride, B, R, C,
+                             _stream(dst))
+    _check(rc, "copy_rows")
+
+
+def nchw_add_table(x: torch.Tensor, table: torch.Tensor):
+    _need_cuda(x, table)
+    assert x.is_contiguous() and table.dtype == torch.float32
+    B, C, H, W = x.shape
+    rc = lib().sdp_nchw_add_table(dcode(x.dtype), x.data_ptr(), table.data_ptr(), B, C, H * W, _stream(x))
+    _check(rc, "nchw_add_table")
+
+
+def act(x: torch.Tensor, y: torch.Tensor, code: int):
+    _need_cuda(x, y)
+    assert x.is_contiguous() and y.is_contiguous() and x.dtype == y.dtype
+    rc = lib().sdp_act(dcode(x.dtype), x.data_ptr(), y.data_ptr(), x.numel(), code, _stream(y))
+    _check(rc, "act")
+
+
+def group_mean(x: Rows, out: torch.Tensor, G: int, rows: int, C: int):
+    _need_cuda(x.t, out)
+    rc = lib().sdp_group_mean(dcode(x.t.dtype), *x.args(), dcode(out.dtype), out.data_ptr(), out.stride(0), G, rows,
+                              C, _stream(out))
+    _check(rc, "group_mean")
+
+
+def nchw_to_rows(x: torch.Tensor, y: Rows):
+    _need_cuda(x, y.t)
+    assert x.is_contiguous()
+    B, C, H, W = x.shape
+    rc = lib().sdp_nchw_to_rows(dcode(x.dtype), x.data_ptr(), dcode(y.t.dtype), *y.args(), B, C, H * W,
+                                _stream(y.t))
+    _check(rc, "nchw_to_rows")
+
+
+def rows_to_nchw(x: Rows, y: torch.Tensor):
+    _need_cuda(x.t, y)
+    assert y.is_contiguous()
+    B, C, H, W = y.shape
+    rc = lib().sdp_rows_to_nchw(dcode(x.t.dtype), *x.args(), dcode(y.dtype), y.data_ptr(), B, C, H * W,
+                                _stream(y))
+    _check(rc, "rows_to_nchw")
+
+
+def cast(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    _need_cuda(x)
+    x = x.contiguous()
+    y = torch.empty(x.shape, dtype=dtype, device=x.device)
+    rc = lib().sdp_cast(dcode(x.dtype), x.data_ptr(), dcode(dtype), y.data_ptr(), x.numel(), _stream(y))
+    _check(rc, "cast")
+    return y
+
+
+def gemm_variant(dtype: torch.dtype, M: int, N: int, K: int) -> int:
+    return lib().sdp_gemm_variant(dcode(dtype), M, N, K)
+
+
+def attention_variant(dtype: torch.dtype, N: int, n_head: int, head_dim: int, has_mask: bool = False) -> int:
+    return lib().sdp_attention_variant(dcode(dtype), N, n_head, head_dim, int(has_mask))

@@ -1,0 +1,299 @@
+"""GPU: each HIP kernel (through the C ABI) against a plain PyTorch fp32
+reference of the same op, on seeded inputs, including ragged sizes, row maps and
+epilogue variants.  Tolerances are stated per dtype: fp32 kernels compute in
+exact fp32 (f32 MFMA / fp32 VALU) -> ~1e-5 relative; bf16 kernels round their
+inputs/outputs to bf16 (8 significant bits) -> ~1e-2 relative."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import sdpnet_hip as sp
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def rnd(*shape, dtype=torch.float32, seed=0, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype).to(DEV)
+
+
+def close(got, ref, dtype, rel=None, what=""):
+    got, ref = got.float(), ref.float()
+    assert torch.isfinite(got).all(), what
+    scale = ref.abs().max().item() + 1e-6
+    err = (got - ref).abs().max().item()
+    tol = rel if rel is not None else (2e-5 if dtype == torch.float32 else 1.2e-2)
+    assert err <= tol * scale + 1e-6, f"{what}: max err {err:.3e} vs scale {scale:.3e} (tol {tol})"
+
+
+ACTS = {0: lambda x: x, 1: F.gelu, 2: F.relu, 3: torch.tanh, 4: torch.sigmoid,
+        5: lambda x: F.leaky_relu(x, 0.01), 6: F.selu,
+        7: lambda x: torch.where(x < -3.5, torch.zeros_like(x), torch.where(
+            x > 3.5, x, 0.5 * x * (1 + x / 3.5 + torch.sin(x * math.pi / 3.5) / math.pi)))}
+
+
+# --------------------------------------------------------------------------- GEMM
+GEMM_SHAPES = [(1, 8, 16), (37, 50, 96), (256, 256, 64), (300, 384, 128), (1000, 768, 768),
+               (513, 1000, 1000), (2000, 2304, 768), (392, 3072, 768), (392, 768, 3072), (130, 130, 640)]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+def test_gemm_plain(dtype, M, N, K):
+    x = rnd(M, K, dtype=dtype, seed=1)
+    w = rnd(N, K, dtype=dtype, seed=2, scale=0.05)
+    y = torch.empty(M, N, dtype=dtype, device=DEV)
+    sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K)
+    close(y, x.float() @ w.float().t(), dtype, what=f"gemm {M}x{N}x{K}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("act", list(ACTS))
+def test_gemm_epilogue(dtype, act):
+    M, N, K = 700, 512, 256
+    x = rnd(M, K, dtype=dtype, seed=3)
+    w = rnd(N, K, dtype=dtype, seed=4, scale=0.1)
+    b = rnd(N, seed=5)
+    r = rnd(M, N, dtype=dtype, seed=6)
+    for pre in (False, True):
+        y = torch.empty(M, N, dtype=dtype, device=DEV)
+        sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, bias=b, resid=sp.dense(r), act=act, resid_pre=pre)
+        z = x.float() @ w.float().t() + b
+        ref = ACTS[act](z + r.float()) if pre else ACTS[act](z) + r.float()
+        close(y, ref, dtype, what=f"act {act} pre {pre}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+def test_gemm_row_maps_and_inplace_residual(dtype):
+    # token buffer [B, R+P, C]; GEMM over the image rows, residual = the same rows (in place)
+    B, R, P, C, K = 3, 4, 196, 256, 128
+    N = R + P
+    tok = rnd(B * N, C, dtype=dtype, seed=7)
+    ref_tok = tok.float().clone()
+    x = rnd(B * P, K, dtype=dtype, seed=8)
+    w = rnd(C, K, dtype=dtype, seed=9, scale=0.1)
+    img = sp.Rows(tok, C, P, N, R)
+    sp.gemm(sp.dense(x), w, img, B * P, C, K, resid=img, act=1)
+    v = ref_tok.view(B, N, C)
+    v[:, R:, :] = F.gelu((x.float() @ w.float().t()).view(B, P, C)) + v[:, R:, :]
+    close(tok, ref_tok, dtype, what="row-mapped in-place")
+    # table residual broadcast over batch (grp=P, gstride=0) as the pos-emb add
+    table = rnd(P, C, dtype=dtype, seed=10)
+    y = torch.zeros(B * N, C, dtype=dtype, device=DEV)
+    sp.gemm(sp.dense(x), w, sp.Rows(y, C, P, N, R), B * P, C, K, resid=sp.Rows(table, C, P, 0, 0), resid_pre=True)
+    ref = torch.zeros(B, N, C, device=DEV)
+    ref[:, R:, :] = (x.float() @ w.float().t()).view(B, P, C) + table.float()
+    close(y, ref.view(B * N, C), dtype, what="table residual")
+    # mapped X operand (read image rows of the buffer)
+    y2 = torch.empty(B * P, C, dtype=dtype, device=DEV)
+    w2 = rnd(C, C, dtype=dtype, seed=11, scale=0.05)
+    sp.gemm(img, w2, sp.dense(y2), B * P, C, C)
+    close(y2, tok.float().view(B, N, C)[:, R:, :].reshape(B * P, C) @ w2.float().t(), dtype, what="mapped X")
+
+
+def test_gemm_fast_vs_generic_bf16():
+    M, N, K = 1536, 768, 3072
+    x = rnd(M, K, dtype=BF, seed=12)
+    w = rnd(N, K, dtype=BF, seed=13, scale=0.02)
+    b = rnd(N, seed=14)
+    assert sp.gemm_variant(BF, M, N, K) == 1
+    y1 = torch.empty(M, N, dtype=BF, device=DEV)
+    sp.gemm(sp.dense(x), w, sp.dense(y1), M, N, K, bias=b, act=1)
+    old = sp.lib().sdp_gemm_force_generic(1)
+    try:
+        y2 = torch.empty(M, N, dtype=BF, device=DEV)
+        sp.gemm(sp.dense(x), w, sp.dense(y2), M, N, K, bias=b, act=1)
+    finally:
+        sp.lib().sdp_gemm_force_generic(old)
+    close(y1, y2, BF, rel=1e-2, what="fast vs generic")
+
+
+def test_gemm_identity_asymmetric():
+    # A = I catches a transposed C write (symmetric B would hide it)
+    n = 256
+    x = torch.eye(n, dtype=BF, device=DEV)
+    w = (torch.arange(n * n, device=DEV).float().view(n, n) % 97 - 48).to(BF)
+    y = torch.empty(n, n, dtype=BF, device=DEV)
+    sp.gemm(sp.dense(x), w, sp.dense(y), n, n, n)
+    assert torch.equal(y, w.t().contiguous())
+
+
+# ---------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("M,C,eps", [(1, 64, 1e-5), (333, 768, 1e-6), (50, 128, 1e-5), (7, 3072, 1e-5),
+                                     (9, 96, 1e-5), (5, 6000, 1e-5), (4, 10, 1e-5)])
+def test_layernorm(dtype, M, C, eps):
+    x = rnd(M, C, dtype=dtype, seed=20, scale=3.0) + 1.5
+    g = rnd(C, seed=21) * 0.1 + 1
+    b = rnd(C, seed=22) * 0.1
+    y = torch.empty_like(x)
+    sp.layernorm(sp.dense(x), g, b, eps, sp.dense(y), M, C)
+    close(y, F.layer_norm(x.float(), (C,), g, b, eps), dtype, what="layernorm")
+
+
+def test_layernorm_row_maps():
+    B, R, P, C = 2, 4, 49, 768
+    N = R + P
+    tok = rnd(B * N, C, dtype=BF, seed=23)
+    g, b = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+    y = torch.empty(B * P, C, dtype=BF, device=DEV)
+    sp.layernorm(sp.Rows(tok, C, P, N, R), g, b, 1e-6, sp.dense(y), B * P, C)
+    ref = F.layer_norm(tok.float().view(B, N, C)[:, R:], (C,), eps=1e-6).reshape(B * P, C)
+    close(y, ref, BF)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("H,hd", [(8, 96), (8, 16), (4, 16), (2, 128), (8, 12)])
+def test_qk_headnorm(dtype, H, hd):
+    T = 77
+    C = H * hd
+    qkv = rnd(T, 3 * C, dtype=dtype, seed=24, scale=2.0)
+    gq, bq, gk, bk = (rnd(hd, seed=s) * 0.1 + (1 if s % 2 == 0 else 0) for s in (25, 26, 27, 28))
+    ref = qkv.float().clone()
+    sp.qk_headnorm(qkv, T, H, hd, gq, bq, gk, bk, 1e-5)
+    ref[:, :C] = F.layer_norm(ref[:, :C].view(T, H, hd), (hd,), gq, bq).view(T, C)
+    ref[:, C:2 * C] = F.layer_norm(ref[:, C:2 * C].view(T, H, hd), (hd,), gk, bk).view(T, C)
+    close(qkv, ref, dtype, what="qk headnorm")
+
+
+# ------------------------------------------------------------------------ DW conv
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("B,H,W,C,k", [(2, 14, 14, 768, 7), (1, 16, 16, 128, 7), (3, 7, 7, 64, 3),
+                                       (2, 8, 8, 96, 5), (1, 28, 28, 64, 7), (2, 5, 9, 40, 3), (1, 56, 56, 64, 7)])
+@pytest.mark.parametrize("bias", [False, True])
+def test_dwconv(dtype, B, H, W, C, k, bias):
+    x = rnd(B, C, H, W, dtype=dtype, seed=30)
+    w = rnd(C, 1, k, k, seed=31, scale=0.2)
+    b = rnd(C, seed=32) if bias else None
+    rows = x.permute(0, 2, 3, 1).contiguous().view(B * H * W, C)
+    y = torch.empty_like(rows)
+    sp.dwconv(sp.dense(rows), w.view(C, k * k).contiguous(), b, sp.dense(y), B, H, W, C, k)
+    ref = F.conv2d(x.float(), w, b, padding="same", groups=C).permute(0, 2, 3, 1).reshape(B * H * W, C)
+    close(y, ref, dtype, what="dwconv")
+
+
+# ---------------------------------------------------------------------- attention
+def attn_ref(qkv, B, N, H, hd, add=None):
+    C = H * hd
+    q, k, v = qkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    s = q @ k.transpose(-1, -2) / math.sqrt(hd)
+    if add is not None:
+        s = s + add
+    return (torch.softmax(s, -1) @ v).permute(0, 2, 1, 3).reshape(B * N, C)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("B,N,H,hd", [(2, 200, 8, 96), (1, 260, 8, 96), (3, 200, 8, 16), (2, 53, 4, 16),
+                                      (1, 5, 2, 32), (2, 1, 8, 64), (1, 300, 2, 128), (2, 53, 8, 12),
+                                      (1, 384, 8, 96), (1, 500, 4, 32)])
+def test_attention(dtype, B, N, H, hd):
+    C = H * hd
+    qkv = rnd(B * N, 3 * C, dtype=dtype, seed=40)
+    o = torch.empty(B * N, C, dtype=dtype, device=DEV)
+    sp.attention(qkv, o, B, N, H, hd)
+    close(o, attn_ref(qkv, B, N, H, hd), dtype, what=f"attn variant {sp.attention_variant(dtype, N, H, hd)}")
+
+
+def test_attention_mfma_path_is_taken_for_canonical_shapes():
+    assert sp.attention_variant(BF, 200, 8, 96) == 1
+    assert sp.attention_variant(BF, 260, 8, 96) == 1
+    assert sp.attention_variant(BF, 200, 8, 16) == 1
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+def test_attention_mask(dtype):
+    B, N, H, hd = 2, 40, 4, 16
+    C = H * hd
+    qkv = rnd(B * N, 3 * C, dtype=dtype, seed=41)
+    add = torch.zeros(B, 1, N, N, device=DEV)
+    add[0, 0, :, 30:] = float("-inf")
+    add[1] = rnd(1, N, N, seed=42)
+    o = torch.empty(B * N, C, dtype=dtype, device=DEV)
+    sp.attention(qkv, o, B, N, H, hd, add, add.stride(0), 0)
+    close(o, attn_ref(qkv, B, N, H, hd, add), dtype, what="masked attn")
+
+
+def test_attention_spiky_scores():
+    # large logits: softmax max-subtraction must hold (no inf/nan), one dominant key
+    B, N, H, hd = 1, 200, 8, 96
+    C = H * hd
+    qkv = rnd(B * N, 3 * C, dtype=BF, seed=43)
+    qkv[:, :C] *= 6
+    qkv[7, C:2 * C] *= 8
+    o = torch.empty(B * N, C, dtype=BF, device=DEV)
+    sp.attention(qkv, o, B, N, H, hd)
+    close(o, attn_ref(qkv, B, N, H, hd), BF, rel=2e-2, what="spiky")
+
+
+# ------------------------------------------------------------------ misc kernels
+@pytest.mark.parametrize("p,img", [(16, 224), (14, 224), (8, 64), (16, 112)])
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+def test_patchify(p, img, dtype):
+    B = 2
+    x = rnd(B, 3, img, img, seed=50)
+    kp = (3 * p * p + 63) // 64 * 64
+    out = torch.empty(B * (img // p) ** 2, kp, dtype=dtype, device=DEV)
+    sp.patchify(x, out, p, kp)
+    ref = F.unfold(x, p, stride=p).transpose(1, 2).reshape(-1, 3 * p * p)
+    close(out[:, : 3 * p * p], ref, dtype, rel=4e-3 if dtype == BF else 0)
+    assert (out[:, 3 * p * p:] == 0).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+def test_transposes_and_row_copies(dtype):
+    B, C, H, W, R = 3, 130, 7, 9, 4
+    N = R + H * W
+    x = rnd(B, C, H, W, dtype=dtype, seed=51)
+    tok = torch.zeros(B * N, C, dtype=dtype, device=DEV)
+    sp.nchw_to_rows(x, sp.Rows(tok, C, H * W, N, R))
+    assert torch.equal(tok.view(B, N, C)[:, R:], x.permute(0, 2, 3, 1).reshape(B, H * W, C))
+    back = torch.empty_like(x)
+    sp.rows_to_nchw(sp.Rows(tok, C, H * W, N, R), back)
+    assert torch.equal(back, x)
+    regs = rnd(B, R, C, dtype=dtype, seed=52)
+    sp.copy_rows(regs, C, R * C, tok, C, N * C, B, R, C)
+    assert torch.equal(tok.view(B, N, C)[:, :R], regs)
+    table = rnd(R, C, seed=53)
+    sp.copy_rows(table, C, 0, tok, C, N * C, B, R, C)
+    assert torch.equal(tok.view(B, N, C)[:, :R].float(), table.to(dtype).float().expand(B, R, C))
+    m = torch.empty(B, C, dtype=dtype, device=DEV)
+    sp.group_mean(sp.Rows(tok, C, H * W, N, R), m, B, H * W, C)
+    close(m, tok.float().view(B, N, C)[:, R:].mean(1), dtype, rel=1e-5 if dtype == torch.float32 else 8e-3)
+
+
+def test_pos_tables():
+    H, W, C = 14, 15, 96
+    eh, ew = rnd(16, C, seed=54), rnd(16, C, seed=55)
+    t = torch.empty(H * W, C, device=DEV)
+    sp.pos_table(eh, ew, t, H, W, C)
+    assert torch.allclose(t, (eh[:H, None, :] + ew[None, :W, :]).reshape(H * W, C), atol=1e-6)
+    k = 5
+    bone = rnd(1, C, 16 + k, 16 + k, seed=56) * 0.02
+    t2 = torch.empty(H * W, C, device=DEV)
+    sp.avgpool_table(bone, t2, H, W, C, k)
+    ref = F.avg_pool2d(bone[:, :, : H + k - 1, : W + k - 1], k, stride=1)[0].permute(1, 2, 0).reshape(H * W, C)
+    assert torch.allclose(t2, ref, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("code", list(ACTS))
+def test_act_and_cast(dtype, code):
+    x = (torch.linspace(-6, 6, 4097, device=DEV)).to(dtype)
+    y = torch.empty_like(x)
+    sp.act(x, y, code)
+    close(y, ACTS[code](x.float()), dtype, rel=2e-6 if dtype == torch.float32 else 8e-3)
+    c = sp.cast(x, BF if dtype == torch.float32 else torch.float32)
+    assert torch.equal(c.float(), x.float().to(BF).float()) or dtype == BF
+
+
+def test_nchw_add_table():
+    B, C, H, W = 2, 40, 6, 7
+    x = rnd(B, C, H, W, seed=57)
+    t = rnd(H * W, C, seed=58)
+    ref = x + t.t().reshape(1, C, H, W)
+    sp.nchw_add_table(x, t)
+    assert torch.allclose(x, ref, atol=1e-6)
