@@ -54,6 +54,11 @@ int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride
 int sdp_gemm_variant(int dtype, int M, int N, int K);
 /* Test hook: force the generic kernel (returns the previous setting). */
 int sdp_gemm_force_generic(int on);
+/* Select the bf16 fast kernel: 1 = 2-stage LDS ring + 8-byte stores, 3 = 2-stage
+ * ring + permlane-paired 16-byte stores, 5 = deep X ring (3 slots) + 16-byte
+ * stores (default), 4 = no-store timing probe (benchmarks only: wrong results).
+ * Returns the previous selection. */
+int sdp_gemm_set_fast_kernel(int k);
 
 /*
  * Row LayerNorm over C contiguous channels, fp32 statistics, biased variance.
@@ -74,12 +79,23 @@ int sdp_qk_headnorm(int dtype, void* QKV, int64_t ld, int64_t rows, int n_head, 
                     const float* k_beta, float eps, void* stream);
 
 /*
+ * Per-row LayerNorm statistics: stats[2m] = mean, stats[2m+1] = 1/sqrt(var+eps)
+ * (biased variance) of logical row m; C % 4 == 0, C <= 2048.  Feeds the LN that
+ * sdp_dwconv applies on load (ConvMixer layer_norm_1, layers.py:12-24, :102).
+ */
+int sdp_rowstats(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                 float eps, float* stats, int M, int C, void* stream);
+
+/*
  * Depthwise k x k conv, zero "same" padding, NHWC token rows (pixel (b,h,w) is
  * logical row b*H*W + h*W + w).  weight fp32 [C][k][k], bias fp32 [C] or NULL.
- * Replaces: nn.Conv2d(C, C, k, groups=C, padding="same") (layers.py:73-78).
- * k in {1,3,5,7,9}.
+ * If stats != NULL the conv input is the LayerNorm (x - mean) * rstd * ln_gamma +
+ * ln_beta computed while staging (fused layer_norm_1 of ConvMixer).
+ * Replaces: layer_norm_1 + nn.Conv2d(C, C, k, groups=C, padding="same")
+ * (layers.py:73-78, :102).  k in {1,3,5,7,9}.
  */
 int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+               const float* stats, const float* ln_gamma, const float* ln_beta,
                const float* weight, const float* bias, void* Y, int64_t ldy, int y_grp,
                int64_t y_gstride, int y_off, int B, int H, int W, int C, int k, void* stream);
 

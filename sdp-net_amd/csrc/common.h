@@ -32,6 +32,22 @@ enum SdpAct {
   ACT_LEAKY_RELU = 5, ACT_SELU = 6, ACT_KELU = 7
 };
 
+// GELU(x) = x * Phi(x), Phi via erf from Abramowitz-Stegun 7.1.26 (|err| <= 1.5e-7):
+// ~16 VALU incl. one v_rcp_f32 and one v_exp_f32, branch-free.  Used by the
+// hot GEMM epilogue; the generic path keeps libm erff.
+SDP_DEV float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);
+  const float q = 0.5f * p * e;           // = 0.5 * (1 - erf(|x|/sqrt2))
+  return x * (x >= 0.0f ? 1.0f - q : q);
+}
+
 SDP_DEV float apply_act(int act, float x) {
   switch (act) {
     case ACT_GELU: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));  // exact erf GELU

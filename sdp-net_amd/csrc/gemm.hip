@@ -133,6 +133,129 @@ SDP_DEV bf16x8 lds_frag(const char* lds_tile, int r, int c) {
   return *(const bf16x8*)(lds_tile + r * 128 + swz(r, c) * 16);
 }
 
+// Epilogue activation is a template parameter: ACT_NONE, ACT_GELU (fast erf) or -1
+// (runtime code through apply_act).
+template <int ACT>
+SDP_DEV float epi_act(int code, float v) {
+  if constexpr (ACT == ACT_NONE) return v;
+  else if constexpr (ACT == ACT_GELU) return gelu_fast(v);
+  else return apply_act(code, v);
+}
+
+// Epilogue of one 256x256 tile held as acc[4 n-tiles][8 m-tiles] per wave.
+template <int ACT>
+SDP_DEV void tile_epilogue(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int M, int N, int wm, int wn,
+                           int fr, int fq) {
+  // D[n][m]: lane holds n = base + 4*fq + r, m = base + fr.
+  const bool full_n = (n0 + BN <= N);
+  if (!full_n) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + wm * 128 + j * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + wn * 64 + i * 16 + fq * 4;
+        if (n < N) epi_store4<bf16_t>(epi, m, n, N, acc[i][j]);
+      }
+    }
+    return;
+  }
+  f32x4 bv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + wn * 64 + i * 16 + fq * 4;
+    bv[i] = epi.bias ? *(const f32x4*)(epi.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int m = m0 + wm * 128 + j * 16 + fr;
+    if (m >= M) continue;
+    const int nb = n0 + wn * 64 + fq * 4;
+    bf16x4 rr[4];
+    if (epi.resid) {
+      const bf16_t* rp = epi.resid + epi.rmap(m) * epi.ldr + nb;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rr[i] = *(const bf16x4*)(rp + i * 16);
+    }
+    bf16_t* op = epi.out + epi.cmap(m) * epi.ldc + nb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[i][j][r] + bv[i][r];
+        if (epi.resid && epi.resid_pre) v += bf2f((bf16_t)rr[i][r]);
+        v = epi_act<ACT>(epi.act, v);
+        if (epi.resid && !epi.resid_pre) v += bf2f((bf16_t)rr[i][r]);
+        o[r] = (short)f2bf(v);
+      }
+      *(bf16x4*)(op + i * 16) = o;
+    }
+  }
+}
+
+// Same epilogue with 16-byte stores: v_permlane16_swap pairs the 4-column chunks of
+// n-tiles (2p, 2p+1) held by lanes l and l+16, so each lane ends up with 8
+// contiguous columns (col0 = 32p + {0,16,8,24}[fq]); residual loads / output
+// stores become one 16-B access per lane per pair (half the store instructions).
+SDP_DEV int pair_col0(int fq) { return 8 * (((fq & 1) << 1) | (fq >> 1)); }
+
+template <int ACT>
+SDP_DEV void tile_epilogue16(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int M, int N, int wm,
+                             int wn, int fr, int fq) {
+  if (n0 + BN > N) {  // ragged N: generic per-4 path
+    tile_epilogue<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
+    return;
+  }
+  const int cbase = n0 + wn * 64 + pair_col0(fq);
+  f32x4 bv[2][2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    if (epi.bias) {
+      bv[p][0] = *(const f32x4*)(epi.bias + cbase + 32 * p);
+      bv[p][1] = *(const f32x4*)(epi.bias + cbase + 32 * p + 4);
+    } else {
+      bv[p][0] = bv[p][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int m = m0 + wm * 128 + j * 16 + fr;
+    if (m >= M) continue;
+    bf16x8 rr[2];
+    if (epi.resid) {
+      const bf16_t* rp = epi.resid + epi.rmap(m) * epi.ldr + cbase;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) rr[p] = *(const bf16x8*)(rp + 32 * p);
+    }
+    bf16_t* op = epi.out + epi.cmap(m) * epi.ldc + cbase;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                   __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[4 + r] = __uint_as_float(sw[1]);
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = v[e] + bv[p][e >> 2][e & 3];
+        if (epi.resid && epi.resid_pre) x += bf2f((bf16_t)rr[p][e]);
+        x = epi_act<ACT>(epi.act, x);
+        if (epi.resid && !epi.resid_pre) x += bf2f((bf16_t)rr[p][e]);
+        o[e] = (short)f2bf(x);
+      }
+      *(bf16x8*)(op + 32 * p) = o;
+    }
+  }
+}
+
+// EPI: 0 = 8-B stores, 1 = permlane-paired 16-B stores, 2 = no stores (timing probe only)
+template <int ACT, int EPI>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_256x256(
     const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap, const bf16_t* __restrict__ W,
     int64_t ldw, Epi<bf16_t> epi, int M, int N, int K, int tiles_m, int tiles_n) {
@@ -191,17 +314,84 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_256x256(
     __syncthreads();
   }
 
-  // D[n][m]: lane holds n = base + 4*fq + r, m = base + fr.
+  tile_epilogue<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
+}
+
+
+
+// Deep-X variant: the streamed activation operand X gets a 3-slot LDS ring, the
+// weight operand W (L2/MALL resident) a 2-slot ring: 5 x 32 KiB = all 160 KiB.
+// Iteration kt issues W(kt+1) then X(kt+2) and ends with a COUNTED
+// s_waitcnt vmcnt(4) (X(kt+2)'s four wave-instructions stay in flight across the
+// barrier; they are the youngest) + lgkmcnt(0) + raw s_barrier, so an HBM miss
+// on X has two K-steps (~4 us) to land instead of one.
+template <int ACT>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_deepx(
+    const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap, const bf16_t* __restrict__ W,
+    int64_t ldw, Epi<bf16_t> epi, int M, int N, int K, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[5 * TILE_BYTES];
+  char* xring = smem;                   // 3 slots
+  char* wring = smem + 3 * TILE_BYTES;  // 2 slots
+  const int nwg = tiles_m * tiles_n;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[4][8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int m = m0 + wm * 128 + j * 16 + fr;
-    if (m >= M) continue;
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = n0 + wn * 64 + i * 16 + fq * 4;
-      if (n < N) epi_store4<bf16_t>(epi, m, n, N, acc[i][j]);
-    }
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const RowMap wmap{0x7fffffff, 0, 0};
+  const int nk = K / BK;
+  // prologue: W(0), X(0), X(1)
+  stage_tile(W, ldw, wmap, n0, N, 0, wring, wave, lane);
+  stage_tile(X, ldx, xmap, m0, M, 0, xring, wave, lane);
+  if (nk > 1) {
+    stage_tile(X, ldx, xmap, m0, M, BK, xring + TILE_BYTES, wave, lane);
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   }
+  __builtin_amdgcn_s_barrier();
+
+  int xs = 0, ws = 0;  // current ring slots
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more1 = kt + 1 < nk, more2 = kt + 2 < nk;
+    if (more1) stage_tile(W, ldw, wmap, n0, N, (kt + 1) * BK, wring + (ws ^ 1) * TILE_BYTES, wave, lane);
+    if (more2) {
+      const int xs2 = xs >= 1 ? xs - 1 : 2;  // (xs + 2) % 3
+      stage_tile(X, ldx, xmap, m0, M, (kt + 2) * BK, xring + xs2 * TILE_BYTES, wave, lane);
+    }
+    const char* xt = xring + xs * TILE_BYTES;
+    const char* wt = wring + ws * TILE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + fq;
+      bf16x8 bx[8], aw[4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bx[j] = lds_frag(xt, wm * 128 + j * 16 + fr, c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) aw[i] = lds_frag(wt, wn * 64 + i * 16 + fr, c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[i], bx[j], acc[i][j], 0, 0, 0);
+    }
+    if (more2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    xs = xs == 2 ? 0 : xs + 1;
+    ws ^= 1;
+  }
+  tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
 }
 }  // namespace fast
 
@@ -307,6 +497,26 @@ extern "C" int sdp_gemm_force_generic(int on) {
   return old;
 }
 
+// bf16 fast-kernel selection: 1 = 2-stage ring + 8-B stores, 3 = 2-stage ring + paired
+// 16-B stores, 5 = deep-X ring (3 X slots, 2 W slots, counted vmcnt) + 16-B stores
+// (default), 4 = no-store timing probe (wrong results; benchmarks only).
+static int g_fast_kernel = 5;
+extern "C" int sdp_gemm_set_fast_kernel(int k) {
+  int old = g_fast_kernel;
+  if (k == 1 || k == 3 || k == 4 || k == 5) g_fast_kernel = k;
+  return old;
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
 extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
                         const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
                         int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
@@ -320,10 +530,29 @@ extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_
   const RowMap ym = mk_map(y_grp, y_gstride, y_off);
   if (dtype == 1) {
     Epi<bf16_t> e{bias, (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, act, resid_pre};
-    if (!g_force_generic && sdp_gemm_variant(dtype, M, N, K) == 1) {
+    const bool aligned = (ldy % 4 == 0) && ((uintptr_t)Y % 8 == 0) && (!R || ((ldr % 4 == 0) && ((uintptr_t)R % 8 == 0))) &&
+                         (!bias || ((uintptr_t)bias % 16 == 0)) && (ldx % 8 == 0) && ((uintptr_t)X % 16 == 0) &&
+                         (ldw % 8 == 0) && ((uintptr_t)W % 16 == 0);
+    if (!g_force_generic && aligned && sdp_gemm_variant(dtype, M, N, K) == 1) {
       const int tm = (M + fast::BM - 1) / fast::BM, tn = (N + fast::BN - 1) / fast::BN;
-      hipLaunchKernelGGL(fast::gemm_bf16_256x256, dim3(tm * tn), dim3(fast::NTHREADS), 0, s,
-                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn);
+#define SDP_FAST(A, E) hipLaunchKernelGGL((fast::gemm_bf16_256x256<A, E>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
+                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
+      if (g_fast_kernel == 5) {
+#define SDP_DEEP(A) hipLaunchKernelGGL((fast::gemm_bf16_deepx<A>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
+                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
+        if (act == ACT_NONE) SDP_DEEP(ACT_NONE); else if (act == ACT_GELU) SDP_DEEP(ACT_GELU); else SDP_DEEP(-1);
+#undef SDP_DEEP
+        return SDP_CHECK_LAUNCH();
+      }
+      const int em = g_fast_kernel == 1 ? 0 : (g_fast_kernel == 4 ? 2 : 1);
+      if (em == 0) {
+        if (act == ACT_NONE) SDP_FAST(ACT_NONE, 0); else if (act == ACT_GELU) SDP_FAST(ACT_GELU, 0); else SDP_FAST(-1, 0);
+      } else if (em == 1) {
+        if (act == ACT_NONE) SDP_FAST(ACT_NONE, 1); else if (act == ACT_GELU) SDP_FAST(ACT_GELU, 1); else SDP_FAST(-1, 1);
+      } else {
+        SDP_FAST(ACT_NONE, 2);
+      }
+#undef SDP_FAST
     } else {
       dim3 grid((M + gen::BM - 1) / gen::BM, (N + gen::BN - 1) / gen::BN);
       hipLaunchKernelGGL(gen::gemm_generic<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)X, ldx, xm,

@@ -9,11 +9,10 @@
 //    variance (fp32), 8-16 B vector loads.
 //  * sdp_qk_headnorm — q_norm / k_norm (layers.py:236-237, :286): LayerNorm over
 //    each head_dim segment of the q and k thirds of the fused QKV rows, in place.
+//  * sdp_rowstats — per-row (mean, rstd) for a LayerNorm applied by its consumer.
 //  * sdp_dwconv — depthwise conv (layers.py:73-78: groups=C, padding="same",
-//    zeros, optional bias) on image rows of a token-major buffer.  One block =
-//    one image x row band x 128 B of channels; the band + halo is staged in LDS
-//    (zero-filled border), each thread owns one channel and slides a k-wide
-//    window along 16-pixel output strips with its k*k taps in registers.
+//    zeros, optional bias) on image rows of a token-major buffer, optionally on
+//    LN(x) computed while staging (ConvMixer layer_norm_1, layers.py:102).
 #include "common.h"
 
 // ---------------------------------------------------------------------------
@@ -218,131 +217,261 @@ extern "C" int sdp_qk_headnorm(int dtype, void* QKV, int64_t ld, int64_t rows, i
 }
 
 // ---------------------------------------------------------------------------
-// Depthwise conv, NHWC token rows.
-// X: image pixel (b, h, w) at physical row xm(b*H*W + h*W + w) (stride ldx)
-// Y: same with ym.  Weight fp32 [C][k][k], bias fp32 [C] or null.
+// Row statistics (mean, rstd) for a LayerNorm applied by the consumer kernel.
+// stats[2m] = mean, stats[2m+1] = 1/sqrt(var + eps) of logical row m.
 // ---------------------------------------------------------------------------
-constexpr int DW_STRIP = 16;   // output pixels per sliding window
+template <typename T>
+__global__ __launch_bounds__(256) void rowstats_k(const T* __restrict__ X, int64_t ldx, RowMap xm, float eps,
+                                                  float* __restrict__ stats, int M, int C) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const T* xp = X + xm(row) * ldx;
+  constexpr int VPL = 8;  // C <= 64 * 4 * 8 = 2048 in registers
+  float v[VPL][4];
+  float s = 0.f;
+  const int nv = C >> 2;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c4 = lane + i * 64;
+    if (c4 < nv) {
+      if constexpr (sizeof(T) == 2) {
+        bf16x4 t = *(const bf16x4*)(xp + c4 * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[i][r] = bf2f((bf16_t)t[r]);
+      } else {
+        f32x4 t = *(const f32x4*)(xp + c4 * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[i][r] = t[r];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[i][r] = 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s += v[i][r];
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    if (lane + i * 64 < nv) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = v[i][r] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)C + eps);
+  if (lane == 0) {
+    stats[2 * row] = mean;
+    stats[2 * row + 1] = rstd;
+  }
+}
+
+extern "C" int sdp_rowstats(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, float eps,
+                            float* stats, int M, int C, void* stream) {
+  if (!X || !stats || M < 0 || C <= 0 || C % 4 || C > 2048 || ldx % 4) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  const RowMap xm = mk_rmap(x_grp, x_gstride, x_off);
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((M + 3) / 4), blk(256);
+  if (dtype == 1) hipLaunchKernelGGL(rowstats_k<bf16_t>, grid, blk, 0, s, (const bf16_t*)X, ldx, xm, eps, stats, M, C);
+  else if (dtype == 0) hipLaunchKernelGGL(rowstats_k<float>, grid, blk, 0, s, (const float*)X, ldx, xm, eps, stats, M, C);
+  else return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// Depthwise conv, NHWC token rows, with the channel LayerNorm applied on load.
+// X: pixel (b, h, w) at physical row xm(b*H*W + h*W + w).  Y: same with ym.
+// If stats != null the conv input is LN(x) = (x - mean) * rstd * g + be (the
+// ConvMixer's layer_norm_1, layers.py:102 + :20-24); the zero "same" padding is
+// applied to that normalised input, as in the reference.
+// Block = 32 channels x a band of output rows (+ halo) of one image, 128 threads.
+// The band is staged in LDS (storage type T, rows padded to an odd pixel pitch
+// -> conflict-free 8/16-B reads); thread = 4 channels x a 16-pixel output strip,
+// sliding the k-wide window along the row with the k*k taps read from LDS.
+// ---------------------------------------------------------------------------
+constexpr int DW_CB = 32;
+constexpr int DW_STRIP = 16;
+constexpr int DW_THREADS = 128;
 constexpr int DW_LDS_BYTES = 64 * 1024;
 
 template <typename T, int KS>
-__global__ __launch_bounds__(256) void dwconv_nhwc(const T* __restrict__ X, int64_t ldx, RowMap xm,
-                                                   const float* __restrict__ Wt, const float* __restrict__ bias,
-                                                   T* __restrict__ Y, int64_t ldy, RowMap ym, int H, int W, int C,
-                                                   int band) {
-  constexpr int CB = 128 / sizeof(T);  // channels per block (128 B per pixel)
-  constexpr int PADK = KS / 2;
+__global__ __launch_bounds__(DW_THREADS) void dwconv_ln_nhwc(
+    const T* __restrict__ X, int64_t ldx, RowMap xm, const float* __restrict__ stats, const float* __restrict__ lg,
+    const float* __restrict__ lb, const float* __restrict__ Wt, const float* __restrict__ bias, T* __restrict__ Y,
+    int64_t ldy, RowMap ym, int H, int W, int C, int band, int pitch, int vec_in) {
+  constexpr int PAD = KS / 2;
   extern __shared__ __attribute__((aligned(16))) char dsm[];
-  T* tile = (T*)dsm;  // [(band+KS-1)][(W+KS-1)][CB]
-
+  T* tile = (T*)dsm;                                                         // [TH][pitch][32]
   const int b = blockIdx.z;
   const int h0 = blockIdx.y * band;
-  const int c0 = blockIdx.x * CB;
+  const int c0 = blockIdx.x * DW_CB;
   const int hb = min(band, H - h0);
   const int TH = hb + KS - 1, TW = W + KS - 1;
+  float* wts = (float*)(dsm + (((size_t)band + KS - 1) * pitch * DW_CB * sizeof(T) + 15) / 16 * 16);  // [KS*KS][32]
   const int64_t img0 = (int64_t)b * H * W;
+  const int tid = threadIdx.x;
 
-  // stage band + halo: 8 lanes x 16 B per pixel
-  constexpr int LPP = 8;                // lanes per pixel
-  constexpr int EPL = 16 / sizeof(T);   // elements per lane
-  const int npix = TH * TW;
-  for (int idx = threadIdx.x; idx < npix * LPP; idx += 256) {
+  for (int i = tid; i < KS * KS * DW_CB; i += DW_THREADS) {
+    const int tap = i / DW_CB, cc = i % DW_CB;
+    wts[i] = (c0 + cc < C) ? Wt[(int64_t)(c0 + cc) * KS * KS + tap] : 0.f;
+  }
+  // ---- stage LN(x) for the band + halo ----
+  constexpr int EPL = 16 / sizeof(T);   // elements per 16-B lane load
+  constexpr int LPP = DW_CB / EPL;      // lanes per pixel
+  for (int idx = tid; idx < TH * TW * LPP; idx += DW_THREADS) {
     const int pix = idx / LPP, part = idx % LPP;
     const int th = pix / TW, tw = pix % TW;
-    const int h = h0 + th - PADK, w = tw - PADK;
+    const int h = h0 + th - PAD, w = tw - PAD;
     const int c = c0 + part * EPL;
-    T* dst = tile + (int64_t)pix * CB + part * EPL;
-    if (h >= 0 && h < H && w >= 0 && w < W && c + EPL <= C) {
-      const T* src = X + xm(img0 + (int64_t)h * W + w) * ldx + c;
-      *(f32x4*)dst = *(const f32x4*)src;
-    } else {
+    float v[EPL];
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) {
-        const bool ok = (h >= 0 && h < H && w >= 0 && w < W && c + e < C);
-        dst[e] = ok ? X[xm(img0 + (int64_t)h * W + w) * ldx + c + e] : from_f<T>(0.f);
+    for (int e = 0; e < EPL; ++e) v[e] = 0.f;
+    if (h >= 0 && h < H && w >= 0 && w < W) {
+      const int64_t m = img0 + (int64_t)h * W + w;
+      const T* src = X + xm(m) * ldx + c;
+      if (vec_in && c + EPL <= C) {
+        const f32x4 raw = *(const f32x4*)src;
+        const T* rv = (const T*)&raw;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) v[e] = to_f<T>(rv[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) if (c + e < C) v[e] = to_f<T>(src[e]);
       }
+      if (stats) {
+        const float mean = stats[2 * m], rstd = stats[2 * m + 1];
+#pragma unroll
+        for (int e = 0; e < EPL; ++e)
+          if (c + e < C) v[e] = (v[e] - mean) * rstd * lg[c + e] + lb[c + e];
+      }
+    }
+    T* dst = tile + ((size_t)th * pitch + tw) * DW_CB + part * EPL;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(v[e]);
+      *(bf16x8*)dst = o;
+    } else {
+      *(f32x4*)dst = f32x4{v[0], v[1], v[2], v[3]};
     }
   }
   __syncthreads();
 
-  const int cl = threadIdx.x % CB;
-  const int grp = threadIdx.x / CB;
-  constexpr int NGRP = 256 / CB;
-  const int c = c0 + cl;
-  if (c >= C) return;
-  float wk[KS * KS];
-#pragma unroll
-  for (int i = 0; i < KS * KS; ++i) wk[i] = Wt[(int64_t)c * KS * KS + i];
-  const float bv = bias ? bias[c] : 0.f;
-
+  const int cq = tid & 7;          // channels 4cq .. 4cq+3 of the block
+  const int grp = tid >> 3;        // 16 strip workers
+  const int cg = c0 + cq * 4;
+  const f32x4 bv = (bias && cg + 3 < C) ? *(const f32x4*)(bias + cg) : f32x4{0.f, 0.f, 0.f, 0.f};
   const int nstrip = (W + DW_STRIP - 1) / DW_STRIP;
-  for (int job = grp; job < hb * nstrip; job += NGRP) {
+  for (int job = grp; job < hb * nstrip; job += DW_THREADS / 8) {
     const int oh = job / nstrip;
     const int w0 = (job % nstrip) * DW_STRIP;
-    float acc[DW_STRIP];
+    f32x4 acc[DW_STRIP];
 #pragma unroll
-    for (int i = 0; i < DW_STRIP; ++i) acc[i] = bv;
-#pragma unroll
+    for (int o = 0; o < DW_STRIP; ++o) acc[o] = bv;
     for (int ky = 0; ky < KS; ++ky) {
-      const T* trow = tile + ((int64_t)(oh + ky) * TW + w0) * CB + cl;
-      float win[DW_STRIP + KS - 1];
+      f32x4 wk[KS];
 #pragma unroll
-      for (int i = 0; i < DW_STRIP + KS - 1; ++i)
-        win[i] = (w0 + i < TW) ? to_f<T>(trow[i * CB]) : 0.f;
+      for (int kx = 0; kx < KS; ++kx) wk[kx] = *(const f32x4*)&wts[(ky * KS + kx) * DW_CB + cq * 4];
+      const T* trow = tile + ((size_t)(oh + ky) * pitch + w0) * DW_CB + cq * 4;
 #pragma unroll
-      for (int kx = 0; kx < KS; ++kx) {
-        const float wv = wk[ky * KS + kx];
+      for (int ix = 0; ix < DW_STRIP + KS - 1; ++ix) {
+        f32x4 v;
+        if (w0 + ix < TW) {
+          if constexpr (sizeof(T) == 2) {
+            const bf16x4 t = *(const bf16x4*)(trow + ix * DW_CB);
+            v = f32x4{bf2f((bf16_t)t[0]), bf2f((bf16_t)t[1]), bf2f((bf16_t)t[2]), bf2f((bf16_t)t[3])};
+          } else {
+            v = *(const f32x4*)(trow + ix * DW_CB);
+          }
+        } else {
+          v = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
 #pragma unroll
-        for (int i = 0; i < DW_STRIP; ++i) acc[i] = fmaf(win[i + kx], wv, acc[i]);
+        for (int kx = 0; kx < KS; ++kx) {
+          const int o = ix - kx;
+          if (o >= 0 && o < DW_STRIP) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[o][r] = fmaf(v[r], wk[kx][r], acc[o][r]);
+          }
+        }
       }
     }
     const int gh = h0 + oh;
 #pragma unroll
-    for (int i = 0; i < DW_STRIP; ++i) {
-      const int w = w0 + i;
-      if (w < W) Y[ym(img0 + (int64_t)gh * W + w) * ldy + c] = from_f<T>(acc[i]);
+    for (int o = 0; o < DW_STRIP; ++o) {
+      const int w = w0 + o;
+      if (w < W) {
+        T* dst = Y + ym(img0 + (int64_t)gh * W + w) * ldy + cg;
+        if (cg + 3 < C) {
+          if constexpr (sizeof(T) == 2) {
+            bf16x4 t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t[r] = (short)f2bf(acc[o][r]);
+            *(bf16x4*)dst = t;
+          } else {
+            *(f32x4*)dst = acc[o];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) if (cg + r < C) dst[r] = from_f<T>(acc[o][r]);
+        }
+      }
     }
   }
 }
 
 template <typename T, int KS>
-static int launch_dw(const void* X, int64_t ldx, RowMap xm, const float* Wt, const float* bias, void* Y,
-                     int64_t ldy, RowMap ym, int B, int H, int W, int C, hipStream_t s) {
-  constexpr int CB = 128 / sizeof(T);
+static int launch_dw(const void* X, int64_t ldx, RowMap xm, const float* stats, const float* lg, const float* lb,
+                     const float* Wt, const float* bias, void* Y, int64_t ldy, RowMap ym, int B, int H, int W, int C,
+                     hipStream_t s) {
   const int TW = W + KS - 1;
-  int band = DW_LDS_BYTES / (TW * 128) - (KS - 1);
+  const int pitch = TW | 1;  // odd pixel pitch: rows land on different LDS banks
+  const size_t row_bytes = (size_t)pitch * DW_CB * sizeof(T);
+  const size_t wbytes = (size_t)KS * KS * DW_CB * 4 + 16;
+  int band = (int)((DW_LDS_BYTES - wbytes) / row_bytes) - (KS - 1);
   if (band < 1) return (int)hipErrorInvalidValue;  // image too wide for the LDS band
   band = band > H ? H : band;
   const int nb = (H + band - 1) / band;
-  const size_t lds = (size_t)(band + KS - 1) * TW * 128;
-  dim3 grid((C + CB - 1) / CB, nb, B);
-  hipLaunchKernelGGL((dwconv_nhwc<T, KS>), grid, dim3(256), lds, s, (const T*)X, ldx, xm, Wt, bias, (T*)Y, ldy,
-                     ym, H, W, C, band);
+  const size_t lds = ((size_t)(band + KS - 1) * row_bytes + 15) / 16 * 16 + (size_t)KS * KS * DW_CB * 4;
+  dim3 grid((C + DW_CB - 1) / DW_CB, nb, B);
+  const int vec_in = ((ldx * (int64_t)sizeof(T)) % 16 == 0) && ((uintptr_t)X % 16 == 0);
+  hipLaunchKernelGGL((dwconv_ln_nhwc<T, KS>), grid, dim3(DW_THREADS), lds, s, (const T*)X, ldx, xm, stats, lg, lb,
+                     Wt, bias, (T*)Y, ldy, ym, H, W, C, band, pitch, vec_in);
   return SDP_CHECK_LAUNCH();
 }
 
 template <typename T>
-static int dw_dispatch(int k, const void* X, int64_t ldx, RowMap xm, const float* Wt, const float* bias, void* Y,
-                       int64_t ldy, RowMap ym, int B, int H, int W, int C, hipStream_t s) {
+static int dw_dispatch(int k, const void* X, int64_t ldx, RowMap xm, const float* stats, const float* lg,
+                       const float* lb, const float* Wt, const float* bias, void* Y, int64_t ldy, RowMap ym, int B,
+                       int H, int W, int C, hipStream_t s) {
   switch (k) {
-    case 1: return launch_dw<T, 1>(X, ldx, xm, Wt, bias, Y, ldy, ym, B, H, W, C, s);
-    case 3: return launch_dw<T, 3>(X, ldx, xm, Wt, bias, Y, ldy, ym, B, H, W, C, s);
-    case 5: return launch_dw<T, 5>(X, ldx, xm, Wt, bias, Y, ldy, ym, B, H, W, C, s);
-    case 7: return launch_dw<T, 7>(X, ldx, xm, Wt, bias, Y, ldy, ym, B, H, W, C, s);
-    case 9: return launch_dw<T, 9>(X, ldx, xm, Wt, bias, Y, ldy, ym, B, H, W, C, s);
+    case 1: return launch_dw<T, 1>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
+    case 3: return launch_dw<T, 3>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
+    case 5: return launch_dw<T, 5>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
+    case 7: return launch_dw<T, 7>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
+    case 9: return launch_dw<T, 9>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
     default: return (int)hipErrorInvalidValue;
   }
 }
 
 extern "C" int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
-                          const float* weight, const float* bias, void* Y, int64_t ldy, int y_grp,
-                          int64_t y_gstride, int y_off, int B, int H, int W, int C, int k, void* stream) {
+                          const float* stats, const float* ln_gamma, const float* ln_beta, const float* weight,
+                          const float* bias, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int B,
+                          int H, int W, int C, int k, void* stream) {
   if (!X || !Y || !weight || B < 0 || H <= 0 || W <= 0 || C <= 0) return (int)hipErrorInvalidValue;
-  if ((ldx * (dtype == 1 ? 2 : 4)) % 16 || ((uintptr_t)X % 16)) return (int)hipErrorInvalidValue;
+  if (stats && (!ln_gamma || !ln_beta)) return (int)hipErrorInvalidValue;
+  const int esz = dtype == 1 ? 2 : 4;
+  if ((ldy * esz) % 8 || ((uintptr_t)Y % 8) || ((uintptr_t)X % esz)) return (int)hipErrorInvalidValue;
+  if (bias && ((uintptr_t)bias % 16)) return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
   const RowMap xm = mk_rmap(x_grp, x_gstride, x_off), ym = mk_rmap(y_grp, y_gstride, y_off);
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == 1) return dw_dispatch<bf16_t>(k, X, ldx, xm, weight, bias, Y, ldy, ym, B, H, W, C, s);
-  if (dtype == 0) return dw_dispatch<float>(k, X, ldx, xm, weight, bias, Y, ldy, ym, B, H, W, C, s);
+  if (dtype == 1) return dw_dispatch<bf16_t>(k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s);
+  if (dtype == 0) return dw_dispatch<float>(k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s);
   return (int)hipErrorInvalidValue;
 }

@@ -159,10 +159,13 @@ class ConvMixer(nn.Module):
         w = self._prep(dt)
         a = act_code(self.activation)
         dev = img.t.device
-        ln = torch.empty(M, C, dtype=dt, device=dev)
-        self.layer_norm_1._run_rows(img, _dense(ln), M)
+        # LN1 fused into the depthwise conv: row stats, then normalise-on-load (layers.py:102)
+        stats = torch.empty(M, 2, dtype=torch.float32, device=dev)
+        sp.rowstats(img, self.layer_norm_1.eps, stats, M, C)
+        g1, b1 = self.layer_norm_1._params()
         dwo = torch.empty(M, C, dtype=dt, device=dev)
-        sp.dwconv(_dense(ln), w["dw_w"], w["dw_b"], _dense(dwo), B, H, W, C, w["k"])
+        sp.dwconv(img, w["dw_w"], w["dw_b"], _dense(dwo), B, H, W, C, w["k"], stats=stats, ln_gamma=g1, ln_beta=b1)
+        ln = torch.empty(M, C, dtype=dt, device=dev)
         # x_ = act(PW(DW(LN1 x)) + b) + x      (layers.py:102)
         sp.gemm(_dense(dwo), w["cc_w"], img, M, C, C, bias=w["cc_b"], resid=img, act=a)
         self.layer_norm_2._run_rows(img, _dense(ln), M)

@@ -34,10 +34,12 @@ _SIGS = {
                   _i32, _i32, _i32, _i32, _i32, _vp], _i32),
     "sdp_gemm_variant": ([_i32, _i32, _i32, _i32], _i32),
     "sdp_gemm_force_generic": ([_i32], _i32),
+    "sdp_gemm_set_fast_kernel": ([_i32], _i32),
     "sdp_layernorm": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _f32, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_qk_headnorm": ([_i32, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp], _i32),
-    "sdp_dwconv": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _i32, _i32, _i32, _vp],
-                   _i32),
+    "sdp_rowstats": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _i32, _i32, _vp], _i32),
+    "sdp_dwconv": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _i32,
+                    _i32, _i32, _vp], _i32),
     "sdp_attention": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _vp], _i32),
     "sdp_attention_variant": ([_i32, _i32, _i32, _i32, _i32], _i32),
     "sdp_patchify": ([_i32, _vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp], _i32),
@@ -175,12 +177,20 @@ def qk_headnorm(qkv: torch.Tensor, rows: int, n_head: int, head_dim: int, gq, bq
     _check(rc, "qk_headnorm")
 
 
+def rowstats(x: Rows, eps: float, stats: torch.Tensor, M: int, C: int):
+    _need_cuda(x.t, stats)
+    assert stats.dtype == torch.float32 and stats.numel() >= 2 * M
+    rc = lib().sdp_rowstats(dcode(x.t.dtype), *x.args(), float(eps), stats.data_ptr(), M, C, _stream(stats))
+    _check(rc, "rowstats")
+
+
 def dwconv(x: Rows, weight: torch.Tensor, bias: Optional[torch.Tensor], y: Rows, B: int, H: int, W: int, C: int,
-           k: int):
-    _need_cuda(x.t, y.t, weight, bias)
+           k: int, stats: Optional[torch.Tensor] = None, ln_gamma: Optional[torch.Tensor] = None,
+           ln_beta: Optional[torch.Tensor] = None):
+    _need_cuda(x.t, y.t, weight, bias, stats)
     assert weight.dtype == torch.float32 and weight.is_contiguous()
-    rc = lib().sdp_dwconv(dcode(x.t.dtype), *x.args(), weight.data_ptr(), _ptr(bias), *y.args(), B, H, W, C, k,
-                          _stream(y.t))
+    rc = lib().sdp_dwconv(dcode(x.t.dtype), *x.args(), _ptr(stats), _ptr(ln_gamma), _ptr(ln_beta), weight.data_ptr(),
+                          _ptr(bias), *y.args(), B, H, W, C, k, _stream(y.t))
     _check(rc, "dwconv")
 
 

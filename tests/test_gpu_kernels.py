@@ -163,16 +163,28 @@ def test_qk_headnorm(dtype, H, hd):
 # ------------------------------------------------------------------------ DW conv
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
 @pytest.mark.parametrize("B,H,W,C,k", [(2, 14, 14, 768, 7), (1, 16, 16, 128, 7), (3, 7, 7, 64, 3),
-                                       (2, 8, 8, 96, 5), (1, 28, 28, 64, 7), (2, 5, 9, 40, 3), (1, 56, 56, 64, 7)])
+                                       (2, 8, 8, 96, 5), (1, 28, 28, 64, 7), (2, 5, 9, 40, 3), (1, 56, 56, 64, 7),
+                                       (1, 20, 37, 36, 9), (2, 3, 3, 8, 1)])
 @pytest.mark.parametrize("bias", [False, True])
-def test_dwconv(dtype, B, H, W, C, k, bias):
-    x = rnd(B, C, H, W, dtype=dtype, seed=30)
+@pytest.mark.parametrize("ln", [False, True])
+def test_dwconv(dtype, B, H, W, C, k, bias, ln):
+    x = rnd(B, C, H, W, dtype=dtype, seed=30, scale=2.0) + 0.5
     w = rnd(C, 1, k, k, seed=31, scale=0.2)
     b = rnd(C, seed=32) if bias else None
     rows = x.permute(0, 2, 3, 1).contiguous().view(B * H * W, C)
     y = torch.empty_like(rows)
-    sp.dwconv(sp.dense(rows), w.view(C, k * k).contiguous(), b, sp.dense(y), B, H, W, C, k)
-    ref = F.conv2d(x.float(), w, b, padding="same", groups=C).permute(0, 2, 3, 1).reshape(B * H * W, C)
+    xin = x.float()
+    kw = {}
+    if ln and C % 4 == 0:
+        g, be = rnd(C, seed=33) * 0.1 + 1, rnd(C, seed=34) * 0.1
+        stats = torch.empty(B * H * W, 2, device=DEV)
+        sp.rowstats(sp.dense(rows), 1e-6, stats, B * H * W, C)
+        ref_stats = torch.stack([rows.float().mean(1), 1 / torch.sqrt(rows.float().var(1, unbiased=False) + 1e-6)], 1)
+        close(stats, ref_stats, torch.float32, rel=1e-5, what="rowstats")
+        kw = dict(stats=stats, ln_gamma=g, ln_beta=be)
+        xin = F.layer_norm(rows.float(), (C,), g, be, 1e-6).view(B, H, W, C).permute(0, 3, 1, 2)
+    sp.dwconv(sp.dense(rows), w.view(C, k * k).contiguous(), b, sp.dense(y), B, H, W, C, k, **kw)
+    ref = F.conv2d(xin, w, b, padding="same", groups=C).permute(0, 2, 3, 1).reshape(B * H * W, C)
     close(y, ref, dtype, what="dwconv")
 
 
@@ -297,3 +309,22 @@ def test_nchw_add_table():
     ref = x + t.t().reshape(1, C, H, W)
     sp.nchw_add_table(x, t)
     assert torch.allclose(x, ref, atol=1e-6)
+
+
+@pytest.mark.parametrize("kern", [1, 3, 5])
+@pytest.mark.parametrize("M,N,K,act,res", [(1000, 768, 768, 1, True), (300, 384, 128, 0, False),
+                                           (777, 3072, 768, 1, False), (520, 768, 3072, 0, True),
+                                           (256, 256, 64, 3, True), (600, 2304, 192, 0, False)])
+def test_gemm_fast_kernel_variants(kern, M, N, K, act, res):
+    x = rnd(M, K, dtype=BF, seed=60)
+    w = rnd(N, K, dtype=BF, seed=61, scale=0.05)
+    b = rnd(N, seed=62)
+    r = rnd(M, N, dtype=BF, seed=63) if res else None
+    old = sp.lib().sdp_gemm_set_fast_kernel(kern)
+    try:
+        y = torch.empty(M, N, dtype=BF, device=DEV)
+        sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, bias=b, resid=None if r is None else sp.dense(r), act=act)
+    finally:
+        sp.lib().sdp_gemm_set_fast_kernel(old)
+    ref = ACTS[act](x.float() @ w.float().t() + b) + (r.float() if res else 0)
+    close(y, ref, BF, what=f"kernel {kern}")

@@ -214,7 +214,7 @@ def test_weight_cache_invalidates_on_load_state_dict():
     y0 = m(x.to(DEV))
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     with torch.no_grad():
-        m.blocks[0].t_block.q_proj.weight.mul_(1.5)
+        m.blocks[0].t_block.ff_linear2.weight.mul_(1.5)  # (q_proj would be undone by q_norm)
     y1 = m(x.to(DEV))
     assert (y1 - y0).abs().max() > 1e-6
     m.load_state_dict(sd)

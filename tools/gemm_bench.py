@@ -1,0 +1,93 @@
+"""Microbenchmark of sdp_gemm at the SdP-Net-M shapes (bs=256), random data.
+
+  python tools/gemm_bench.py [--reps 20] [--streams 1,2]
+
+Per shape: the production epilogue (bias / act / residual as the model uses it),
+average µs per launch from HIP events, TFLOP/s.  With --streams 2 the same total
+work is split into two half-M launches on two streams (tail filling).
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "sdp-net_amd"))
+
+import torch  # noqa: E402
+import sdpnet_hip as sp  # noqa: E402
+
+# name: (M, N, K, bias, act, resid)
+SHAPES = {
+    "mixer_cc": (50176, 768, 768, False, 1, True),
+    "mixer_up": (50176, 3072, 768, False, 1, False),
+    "mixer_down": (50176, 768, 3072, False, 0, True),
+    "enc_qkv": (51200, 2304, 768, False, 0, False),
+    "enc_o": (51200, 768, 768, False, 0, True),
+    "enc_ff1": (51200, 3072, 768, True, 1, False),
+    "enc_ff2": (51200, 768, 3072, True, 0, True),
+    "sq8192": (8192, 8192, 8192, False, 0, False),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--streams", default="1")
+    ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--kernels", default="3", help="bf16 fast kernel ids to A/B (1 tile/block, 2 persistent)")
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    bf = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(0)
+    total_us = {}
+    for name in args.shapes.split(","):
+        M, N, K, has_b, act, has_r = SHAPES[name]
+        x = (torch.rand(M, K, generator=g) * 2 - 1).to(bf).to(dev)
+        w = ((torch.rand(N, K, generator=g) * 2 - 1) * 0.05).to(bf).to(dev)
+        b = torch.randn(N, generator=g).to(dev) if has_b else None
+        r = torch.randn(M, N, generator=g).to(bf).to(dev) if has_r else None
+        y = torch.empty(M, N, dtype=bf, device=dev)
+        for kern, ns in [(kk, int(s)) for kk in args.kernels.split(",") for s in args.streams.split(",")]:
+            sp.lib().sdp_gemm_set_fast_kernel(int(kern))
+            streams = [torch.cuda.Stream() for _ in range(ns)]
+            parts = []
+            step = (M + ns - 1) // ns
+            for i in range(ns):
+                lo, hi = i * step, min(M, (i + 1) * step)
+                parts.append((lo, hi))
+
+            def run():
+                cur = torch.cuda.current_stream()
+                for s in streams:
+                    s.wait_stream(cur)
+                for s, (lo, hi) in zip(streams, parts):
+                    with torch.cuda.stream(s):
+                        sp.gemm(sp.dense(x[lo:hi]), w, sp.dense(y[lo:hi]), hi - lo, N, K, bias=b,
+                                resid=None if r is None else sp.dense(r[lo:hi]), act=act)
+                for s in streams:
+                    cur.wait_stream(s)
+
+            for _ in range(3):
+                run()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            us = 1e3 * e0.elapsed_time(e1) / args.reps
+            tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
+            total_us[(name, kern, ns)] = us
+            print(f"{name:11s} M={M:6d} N={N:5d} K={K:5d} kern={kern} streams={ns} variant={sp.gemm_variant(bf, M, N, K)} "
+                  f"{us:9.1f} us  {tf:7.1f} TF/s  ({100 * tf / 2516.6:4.1f}% of bf16 peak)", flush=True)
+    # per-forward estimate for M (launch counts per forward)
+    counts = dict(mixer_cc=24, mixer_up=24, mixer_down=24, enc_qkv=13, enc_o=13, enc_ff1=13, enc_ff2=13)
+    for kern, ns in [(kk, int(s)) for kk in args.kernels.split(",") for s in args.streams.split(",")]:
+        if all((n, kern, ns) in total_us for n in counts):
+            t = sum(total_us[(n, kern, ns)] * c for n, c in counts.items())
+            print(f"GEMM time per M forward (kernel={kern}, streams={ns}): {t / 1e3:.2f} ms")
+
+
+if __name__ == "__main__":
+    main()
