@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prof-steps", type=int, default=2)
+    ap.add_argument("--streams", type=int, default=0, help="sub-batch streams per GPU (0 = model default)")
     args = ap.parse_args()
 
     import torch
@@ -103,6 +104,8 @@ def main():
 
     torch.manual_seed(231424314)  # model_train.py:61
     m = sdp.MainModel.from_dict(**M_CFG).eval()
+    if args.streams > 0:
+        m.num_streams = args.streams
     cpu_sd = {k: v.detach().clone() for k, v in m.state_dict().items()} if rank == 0 else None
     m = m.to(dev)
     B = args.batch
@@ -191,6 +194,7 @@ def main():
         "data": "synthetic N(0,1) 224x224 images resident in HBM; random-init weights (reference init)",
         "config": {"workload": "SdP-Net-M eval forward (12 blocks, d=768, patch 16, 200 tokens), "
                                "bf16 storage / fp32 accumulate, HIP-graph replay",
+                   "streams_per_gpu": m._num_streams(B),
                    "global_batch": B * world, "per_gpu_batch": B, "image": 224, "tokens": 200,
                    "parallelism": f"dp{world} independent batch shards (no collective)"},
         "model_flops_per_image_gf": round(gf, 3),

@@ -54,10 +54,10 @@ int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride
 int sdp_gemm_variant(int dtype, int M, int N, int K);
 /* Test hook: force the generic kernel (returns the previous setting). */
 int sdp_gemm_force_generic(int on);
-/* Select the bf16 fast kernel: 1 = 2-stage LDS ring + 8-byte stores, 3 = 2-stage
- * ring + permlane-paired 16-byte stores, 5 = deep X ring (3 slots) + 16-byte
- * stores (default), 4 = no-store timing probe (benchmarks only: wrong results).
- * Returns the previous selection. */
+/* Select the bf16 fast kernel: 1 = 256x256 tiles, 2-stage LDS ring, 8-byte stores;
+ * 3 = same with permlane-paired 16-byte stores; 5 = 256x256, deep X ring (3 slots);
+ * 7 = 256x128 tiles, 3-slot ring, two blocks per CU (default); 4 = no-store timing
+ * probe (benchmarks only: wrong results).  Returns the previous selection. */
 int sdp_gemm_set_fast_kernel(int k);
 
 /*
@@ -100,16 +100,20 @@ int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstri
                int64_t y_gstride, int y_off, int B, int H, int W, int C, int k, void* stream);
 
 /*
- * softmax(Q K^T / sqrt(hd) + mask) V per (batch, head) from fused QKV rows
- * [B*N, ld_qkv] (q | k | v thirds), output rows [B*N, ld_o] (heads concatenated).
- * mask: optional fp32 additive [.., N, N] with batch / head strides (0 =
- * broadcast).  Replaces F.scaled_dot_product_attention (layers.py:289-291) and
- * the manual softmax path (layers.py:292-298).
+ * softmax(LN_q(Q) LN_k(K)^T / sqrt(hd) + mask) V per (batch, head) from fused QKV
+ * rows [B*N, ld_qkv] (q | k | v thirds), output rows [B*N, ld_o] (heads
+ * concatenated).  q/k LayerNorm (q_norm / k_norm, shared across heads, eps) is
+ * applied when q_gamma != NULL (then all four must be given); the generic path
+ * applies it in place on the QKV rows.  mask: optional fp32 additive [.., N, N]
+ * with batch / head strides (0 = broadcast).  Replaces q_norm/k_norm and
+ * F.scaled_dot_product_attention (layers.py:286-291) and the manual softmax path
+ * (layers.py:292-298).
  */
 int sdp_attention(int dtype, const void* QKV, int64_t ld_qkv, void* O, int64_t ld_o, int B, int N,
-                  int n_head, int head_dim, const float* mask, int64_t mask_sb, int64_t mask_sh,
-                  void* stream);
-/* 1 if sdp_attention takes the LDS-resident MFMA kernel for this shape. */
+                  int n_head, int head_dim, const float* q_gamma, const float* q_beta,
+                  const float* k_gamma, const float* k_beta, float eps, const float* mask,
+                  int64_t mask_sb, int64_t mask_sh, void* stream);
+/* 2 if sdp_attention takes the flash-style MFMA kernel for this shape, else 0. */
 int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask);
 
 /*

@@ -2,18 +2,14 @@
 //     O = softmax(Q K^T / sqrt(hd) + bias) V      per (batch, head), no dropout (eval)
 // Q, K, V are read straight out of the fused QKV projection rows
 // [B*N, 3C] (q | k | v, head h at columns h*hd..h*hd+hd-1 of each third), already
-// q/k-normalised (sdp_qk_headnorm).  O is written as [B*N, C] rows (heads
+// q/k-normalised here.  O is written as [B*N, C] rows (heads
 // concatenated), i.e. the layout o_proj consumes (layers.py:300-301).
 //
-//  * attn_mfma_bf16 — one workgroup per (b, h), 4 waves.  The whole K (row-major)
-//    and V^T of the head are staged in LDS (N <= ~320 fits), each wave walks
-//    16-query tiles: S = Q K^T with v_mfma_f32_16x16x32_bf16 (Q fragments loaded
-//    straight from HBM), row softmax with in-lane + 16-lane shuffle reductions,
-//    P (bf16) through a per-wave LDS tile, O = P V with the same MFMA, O staged
-//    through LDS and stored as 16-B row chunks.  Row strides are padded by 16 B so
-//    every 16-row ds_read_b128 fragment read is bank-conflict free.
+//  * attn_fa_bf16 — bf16 hot path: flash-style, swapped-operand 32x32x16 MFMA with
+//    P kept in registers, q/k LayerNorm fused into the loads (see below).
 //  * attn_generic<T> — fp32 path / any shape / optional additive mask: 4 lanes per
-//    query, online softmax over keys (fp32 throughout).
+//    query, online softmax over keys (fp32 throughout); q/k norms are applied
+//    first, in place on the QKV rows, by sdp_qk_headnorm.
 #include "common.h"
 
 // ---------------------------------------------------------------------------
@@ -79,235 +75,291 @@ __global__ __launch_bounds__(256) void attn_generic(const T* __restrict__ QKV, i
 }
 
 // ---------------------------------------------------------------------------
-// MFMA bf16
+// Flash-style MFMA attention, one workgroup per (b, h), one wave per 32-query
+// tile, v_mfma_f32_32x32x16_bf16 in the "swapped" form:
+//   S^T[key][q] = K Q^T       (A = K rows from LDS, B = Q fragment in registers)
+//   O^T[d][q]  += V^T P^T     (A = V^T read transposed from the row-major V tile
+//                             with ds_read_b64_tr_b16, B = the S^T accumulator)
+// The S^T accumulator has the query on the lane and 16 keys in registers, so the
+// softmax is in-lane + one cross-half shuffle and P never leaves registers
+// (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand").
+// Online softmax over 32-key tiles (running max m, partial sum l per lane half).
+// q_norm / k_norm (layers.py:236-237, :286) are applied while loading Q and
+// staging K; the 1/sqrt(hd) scale (and log2 e) is applied to S in fp32.
 // ---------------------------------------------------------------------------
-struct AttnGeom {
-  int N, H, hd, HDP, NP;   // HDP: hd padded to 32; NP: N padded to 32
-  int ldk, ldv, ldp;       // LDS row strides (elements), each = multiple of 8 + 8 pad
-  int k_off, v_off, p_off, p_wave;  // byte offsets
-  int bytes;
-};
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
-static AttnGeom attn_geom(int N, int H, int hd) {
-  AttnGeom g;
-  g.N = N; g.H = H; g.hd = hd;
-  g.HDP = (hd + 31) / 32 * 32;
-  g.NP = (N + 31) / 32 * 32;
-  g.ldk = g.HDP + 8;
-  g.ldv = g.NP + 8;
-  g.ldp = g.NP + 8;
-  g.k_off = 0;
-  g.v_off = g.NP * g.ldk * 2;
-  g.p_off = g.v_off + g.HDP * g.ldv * 2;
-  const int ptile = 16 * g.ldp * 2;
-  const int otile = 16 * (g.HDP + 8) * 2;
-  g.p_wave = ptile > otile ? ptile : otile;
-  g.bytes = g.p_off + 4 * g.p_wave;
-  return g;
-}
-
-template <int NKT>  // number of 16-key tiles = NP / 16 (compile time: the score row lives in registers)
-__global__ __launch_bounds__(256) void attn_mfma_bf16(const bf16_t* __restrict__ QKV, int64_t ldq,
-                                                      bf16_t* __restrict__ O, int64_t ldo, AttnGeom g,
-                                                      float scale_log2) {
+template <int HDT>  // O d-tiles of 32 (hd <= 32 * HDT)
+__global__ __launch_bounds__(640) void attn_fa_bf16(const bf16_t* __restrict__ QKV, int64_t ldq,
+                                                     bf16_t* __restrict__ O, int64_t ldo, int N, int H, int hd,
+                                                     const float* __restrict__ gq, const float* __restrict__ bq,
+                                                     const float* __restrict__ gk, const float* __restrict__ bk,
+                                                     float eps, float scale_log2, int ldk, int ldv) {
   extern __shared__ __attribute__((aligned(16))) char sm[];
-  bf16_t* Ks = (bf16_t*)(sm + g.k_off);   // [NP][ldk]   K rows (zero pad)
-  bf16_t* Vt = (bf16_t*)(sm + g.v_off);   // [HDP][ldv]  V transposed (zero pad)
-  const int b = blockIdx.x / g.H, h = blockIdx.x % g.H;
-  const int N = g.N, hd = g.hd, HDP = g.HDP, NP = g.NP;
-  const int C = g.H * hd;
+  const int NP = (N + 31) / 32 * 32;
+  bf16_t* Ks = (bf16_t*)sm;            // [NP][ldk]  k-normed K rows
+  bf16_t* Vs = Ks + (size_t)NP * ldk;  // [NP][ldv]  V rows (read transposed by ds_read_b64_tr_b16)
+  const int b = blockIdx.x / H, hh = blockIdx.x % H;
+  const int C = H * hd;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bf16_t* base = QKV + (int64_t)b * N * ldq + h * hd;
+  const int nwaves = blockDim.x >> 6;
+  const bf16_t* base = QKV + (int64_t)b * N * ldq + hh * hd;
 
-  // ---- stage K (row-major) and V^T, 8 elements (16 B) per load ----
-  const int cpr = HDP / 8;  // chunks per padded row
-  for (int idx = tid; idx < NP * cpr; idx += 256) {
-    const int j = idx / cpr, c8 = (idx % cpr) * 8;
-    bf16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (j < N) {
-      const bf16_t* kr = base + (int64_t)j * ldq + C + c8;
-      const bf16_t* vr = base + (int64_t)j * ldq + 2 * C + c8;
-      if (c8 + 8 <= hd) {
-        kv = *(const bf16x8*)kr;
-        vv = *(const bf16x8*)vr;
-      } else {
+  // ---- stage K (k-normed) and V: 16 lanes per key row, 8 elements per lane.
+  // Loads of up to 8 rows per thread are issued before any is consumed. ----
+  {
+    const int sub = tid & 15;
+    const int c8 = sub * 8;
+    const int rstep = blockDim.x >> 4;
+    constexpr int UNR = 8;
+    for (int j0 = tid >> 4; j0 < NP; j0 += rstep * UNR) {
+      bf16x8 kr[UNR], vr[UNR];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          if (c8 + e < hd) {
-            kv[e] = (short)kr[e];
-            vv[e] = (short)vr[e];
-          }
+      for (int u = 0; u < UNR; ++u) {
+        const int j = j0 + u * rstep;
+        kr[u] = vr[u] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (j < N && c8 < hd) {
+          kr[u] = *(const bf16x8*)(base + (int64_t)j * ldq + C + c8);
+          vr[u] = *(const bf16x8*)(base + (int64_t)j * ldq + 2 * C + c8);
         }
       }
-    }
-    *(bf16x8*)&Ks[j * g.ldk + c8] = kv;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) Vt[(c8 + e) * g.ldv + j] = (bf16_t)vv[e];
+      for (int u = 0; u < UNR; ++u) {
+        const int j = j0 + u * rstep;
+        if (j >= NP) break;  // uniform per 16-lane group
+        const bool ok = (j < N) && (c8 < hd);
+        if (gk) {
+          float kv[8];
+          float s = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            kv[e] = bf2f((bf16_t)kr[u][e]);
+            s += kv[e];
+          }
+#pragma unroll
+          for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+          const float mean = s / (float)hd;
+          float ss = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = ok ? kv[e] - mean : 0.f;
+            ss += d * d;
+          }
+#pragma unroll
+          for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
+          const float rstd = 1.0f / sqrtf(ss / (float)hd + eps);
+          if (ok) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) kr[u][e] = (short)f2bf((kv[e] - mean) * rstd * gk[c8 + e] + bk[c8 + e]);
+          }
+        }
+        if (c8 < hd) *(bf16x8*)&Ks[(size_t)j * ldk + c8] = kr[u];
+        if (c8 < ldv) *(bf16x8*)&Vs[(size_t)j * ldv + c8] = vr[u];  // also zeroes the d-padding
+      }
+    }
   }
   __syncthreads();
 
-  bf16_t* Ps = (bf16_t*)(sm + g.p_off + wave * g.p_wave);  // [16][ldp], reused for O
-  const int fr = lane & 15, fq = lane >> 4;
-  const int nqt = (N + 15) / 16;
-  constexpr int MAXKT = NKT;
-  const int nkt = NKT;
-  const int nks = HDP / 32;  // k-steps over head dim
-  for (int qt = wave; qt < nqt; qt += 4) {
-    // Q fragments (A operand): Q[q = qt*16 + fr][d = 32*ks + 8*fq .. +7]
-    bf16x8 qf[4];
-    const int qrow = qt * 16 + fr;
+  const int r = lane & 31, hf = lane >> 5;
+  const int nds = hd / 16;          // k-steps of 16 over the head dim
+  const int nqt = NP / 32;
+  for (int qt = wave; qt < nqt; qt += nwaves) {
+    const int q = qt * 32 + r;
+    const bool qok = q < N;
+    // ---- Q fragments (B operand): Q[q][16s + 8hf + j], q-normed and pre-scaled ----
+    constexpr int NDS_MAX = 2 * HDT;  // hd <= 32 * HDT -> at most 2*HDT k-steps of 16
+    bf16x8 qf[NDS_MAX];
+    float qsum = 0.f;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      qf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (ks < nks && qrow < N) {
-        const int d0 = ks * 32 + fq * 8;
-        const bf16_t* qp = base + (int64_t)qrow * ldq + d0;
-        if (d0 + 8 <= hd) {
-          qf[ks] = *(const bf16x8*)qp;
-        } else {
+    for (int s = 0; s < NDS_MAX; ++s) {
+      qf[s] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (s < nds && qok) qf[s] = *(const bf16x8*)(base + (int64_t)q * ldq + 16 * s + 8 * hf);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) if (d0 + e < hd) qf[ks][e] = (short)qp[e];
+      for (int e = 0; e < 8; ++e) qsum += bf2f((bf16_t)qf[s][e]);
+    }
+    float qmean = 0.f, qrstd = 1.f;
+    if (gq) {
+      qsum += __shfl_xor(qsum, 32, 64);
+      qmean = qsum / (float)hd;
+      float ss = 0.f;
+#pragma unroll
+      for (int s = 0; s < NDS_MAX; ++s) {
+        if (s < nds) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = bf2f((bf16_t)qf[s][e]) - qmean;
+            ss += d * d;
+          }
+        }
+      }
+      ss += __shfl_xor(ss, 32, 64);
+      qrstd = 1.0f / sqrtf(ss / (float)hd + eps);
+    }
+#pragma unroll
+    for (int s = 0; s < NDS_MAX; ++s) {
+      if (s < nds) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int d = 16 * s + 8 * hf + e;
+          float x = bf2f((bf16_t)qf[s][e]);
+          if (gq) x = (x - qmean) * qrstd * gq[d] + bq[d];
+          qf[s][e] = (short)f2bf(qok ? x : 0.f);
         }
       }
     }
-    // S = Q K^T: D[q][key], lane holds rows 4*fq + r of column key = 16*t + fr
-    f32x4 s[MAXKT];
+
+    f32x16 acc[HDT];
 #pragma unroll
-    for (int t = 0; t < MAXKT; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (t < nkt) {
+    for (int dt = 0; dt < HDT; ++dt)
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          if (ks < nks) {
-            const bf16x8 kf = *(const bf16x8*)&Ks[(t * 16 + fr) * g.ldk + ks * 32 + fq * 8];
-            s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, s[t], 0, 0, 0);
+      for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    for (int kt = 0; kt < nqt; ++kt) {
+      f32x16 st;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st[i] = 0.f;
+      const bf16_t* krow = Ks + (size_t)(kt * 32 + r) * ldk + 8 * hf;
+#pragma unroll
+      for (int s = 0; s < NDS_MAX; ++s) {
+        if (s < nds) {
+          const bf16x8 kf = *(const bf16x8*)(krow + 16 * s);
+          st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st[i] *= scale_log2;  // fp32 scale (bf16 Q stays unscaled)
+      if (kt * 32 + 32 > N) {  // mask padded keys of the last tile
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+          if (key >= N) st[i] = -INFINITY;
+        }
+      }
+      float tmax = st[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, st[i]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mn = fmaxf(m, tmax);
+      if (__any(mn > m)) {  // wave-uniform: rescale only when some running max moved
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < HDT; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
+        m = mn;
+      }
+      float p[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        p[i] = __builtin_amdgcn_exp2f(st[i] - m);
+        l += p[i];
+      }
+      // A = V^T fragment via transposed LDS reads of the row-major V tile: the
+      // 16-lane group g = lane/16 reads the 4-key x 16-d block (keys key0..key0+3,
+      // d = 32*dt + 16*(g&1) ..+15); lane 4q+p addresses key key0+q, d +4p..+4p+3,
+      // and receives d = its own column for the 4 keys (= fragment elements 0..3;
+      // the +8-key read gives elements 4..7, matching P^T's register order).
+      const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = (short)f2bf(p[8 * s2 + j]);
+        const int key0 = kt * 32 + 16 * s2 + 4 * hf;
+#pragma unroll
+        for (int dt = 0; dt < HDT; ++dt) {
+          const bf16_t* vb = Vs + (size_t)(key0 + tq) * ldv + dt * 32 + 16 * ((lane >> 4) & 1) + 4 * tp;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)vb);
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(vb + 8 * ldv));
+          const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb, acc[dt], 0, 0, 0);
+        }
+      }
+    }
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
+    if (qok) {
+      bf16_t* orow = O + ((int64_t)b * N + q) * ldo + hh * hd;
+#pragma unroll
+      for (int dt = 0; dt < HDT; ++dt) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = dt * 32 + 8 * g + 4 * hf;
+          if (d < hd) {
+            bf16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(acc[dt][4 * g + e] * inv);
+            *(bf16x4*)(orow + d) = o;
           }
         }
       }
     }
-    // softmax over keys (mask padded keys)
-    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-    for (int t = 0; t < MAXKT; ++t) {
-      if (t < nkt) {
-        const bool kv = (t * 16 + fr) < N;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s[t][r] = kv ? s[t][r] * scale_log2 : -INFINITY;
-          mx[r] = fmaxf(mx[r], s[t][r]);
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o, 64));
-    float sum[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < MAXKT; ++t) {
-      if (t < nkt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(s[t][r] - mx[r]);
-          sum[r] += p;
-          Ps[(fq * 4 + r) * g.ldp + t * 16 + fr] = f2bf(p);
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) sum[r] += __shfl_xor(sum[r], o, 64);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): P writes landed (single wave owns Ps)
-    __builtin_amdgcn_wave_barrier();
-
-    // O = P V: D[q][d], A = P[q][key], B = V[key][d] read from V^T[d][key]
-    f32x4 o[8];
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kk = 0; kk < NP / 32; ++kk) {
-      const bf16x8 pf = *(const bf16x8*)&Ps[fr * g.ldp + kk * 32 + fq * 8];
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        if (dt * 16 < HDP) {
-          const bf16x8 vf = *(const bf16x8*)&Vt[(dt * 16 + fr) * g.ldv + kk * 32 + fq * 8];
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[dt], 0, 0, 0);
-        }
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    // normalise, stage O tile [16][HDP+8] in the P region, store 16-B chunks
-    const int ldo_s = HDP + 8;
-    float inv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) inv[r] = 1.0f / sum[r];
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      if (dt * 16 < HDP) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Ps[(fq * 4 + r) * ldo_s + dt * 16 + fr] = f2bf(o[dt][r] * inv[r]);
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    const int cpr_o = HDP / 8;
-    for (int idx = lane; idx < 16 * cpr_o; idx += 64) {
-      const int r = idx / cpr_o, c8 = (idx % cpr_o) * 8;
-      const int q = qt * 16 + r;
-      if (q < N && c8 < hd) {
-        bf16_t* op = O + ((int64_t)b * N + q) * ldo + h * hd + c8;
-        const bf16x8 v = *(const bf16x8*)&Ps[r * ldo_s + c8];
-        if (c8 + 8 <= hd) {
-          *(bf16x8*)op = v;
-        } else {
-          for (int e = 0; e < 8 && c8 + e < hd; ++e) op[e] = (bf16_t)v[e];
-        }
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
-template <int NKT>
-static int launch_attn_mfma(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, const AttnGeom& g,
-                            float scale, hipStream_t s) {
-  if (g.bytes > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)attn_mfma_bf16<NKT>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, g.bytes);
+template <int HDT>
+static int launch_attn_fa(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H, int hd,
+                          const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
+                          hipStream_t s) {
+  const int NP = (N + 31) / 32 * 32;
+  const int ldk = hd + 8, ldv = 32 * HDT + 8;
+  const size_t bytes = ((size_t)NP * ldk + (size_t)NP * ldv) * 2;
+  if (bytes > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)attn_fa_bf16<HDT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)bytes);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL(attn_mfma_bf16<NKT>, dim3(B * g.H), dim3(256), g.bytes, s, (const bf16_t*)QKV, ldq,
-                     (bf16_t*)O, ldo, g, scale * 1.4426950408889634f);
+  int waves = NP / 32;
+  if (waves > 10) waves = 10;  // __launch_bounds__(640): <= 168 VGPRs
+  hipLaunchKernelGGL(attn_fa_bf16<HDT>, dim3(B * H), dim3(64 * waves), bytes, s, (const bf16_t*)QKV, ldq,
+                     (bf16_t*)O, ldo, N, H, hd, gq, bq, gk, bk, eps, scale * 1.4426950408889634f, ldk, ldv);
   return SDP_CHECK_LAUNCH();
 }
 
-extern "C" int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask) {
-  if (dtype != 1 || has_mask || head_dim > 128 || head_dim % 8 != 0) return 0;
-  const AttnGeom g = attn_geom(N, n_head, head_dim);
-  if (g.NP > 384 || g.bytes > 160 * 1024) return 0;
-  return 1;
+static size_t attn_fa_bytes(int N, int hd) {
+  const int NP = (N + 31) / 32 * 32;
+  const int HDT = (hd + 31) / 32;
+  return ((size_t)NP * (hd + 8) + (size_t)NP * (32 * HDT + 8)) * 2;
 }
 
+extern "C" int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask) {
+  if (dtype != 1 || has_mask || head_dim > 128 || head_dim % 16 != 0) return 0;
+  if (attn_fa_bytes(N, head_dim) > 160 * 1024) return 0;
+  return 2;
+}
+
+int sdp_qk_headnorm(int dtype, void* QKV, int64_t ld, int64_t rows, int n_head, int head_dim, const float* gq,
+                    const float* bq, const float* gk, const float* bk, float eps, void* stream);
+
 extern "C" int sdp_attention(int dtype, const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N,
-                             int n_head, int head_dim, const float* mask, int64_t mask_sb, int64_t mask_sh,
-                             void* stream) {
+                             int n_head, int head_dim, const float* q_gamma, const float* q_beta,
+                             const float* k_gamma, const float* k_beta, float eps, const float* mask, int64_t mask_sb,
+                             int64_t mask_sh, void* stream) {
   if (!QKV || !O || B < 0 || N <= 0 || n_head <= 0 || head_dim <= 0 || head_dim > 128)
     return (int)hipErrorInvalidValue;
+  const bool norm = q_gamma != nullptr;
+  if (norm && (!q_beta || !k_gamma || !k_beta)) return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const float scale = 1.0f / sqrtf((float)head_dim);
-  if (sdp_attention_variant(dtype, N, n_head, head_dim, mask != nullptr) == 1 && (ldq % 8 == 0) &&
-      (ldo % 8 == 0) && ((uintptr_t)QKV % 16 == 0) && ((uintptr_t)O % 16 == 0)) {
-    const AttnGeom g = attn_geom(N, n_head, head_dim);
-    switch (g.NP / 16) {
-#define SDP_ATT(NKT) case NKT: return launch_attn_mfma<NKT>(QKV, ldq, O, ldo, B, g, scale, s);
-      SDP_ATT(2) SDP_ATT(4) SDP_ATT(6) SDP_ATT(8) SDP_ATT(10) SDP_ATT(12)
-      SDP_ATT(14) SDP_ATT(16) SDP_ATT(18) SDP_ATT(20) SDP_ATT(22) SDP_ATT(24)
-#undef SDP_ATT
-      default: return (int)hipErrorInvalidValue;
+  if (sdp_attention_variant(dtype, N, n_head, head_dim, mask != nullptr) == 2 && (ldq % 8 == 0) && (ldo % 4 == 0) &&
+      ((uintptr_t)QKV % 16 == 0) && ((uintptr_t)O % 8 == 0)) {
+    const int HDT = (head_dim + 31) / 32;
+    const float *gq = norm ? q_gamma : nullptr, *bq = norm ? q_beta : nullptr;
+    const float *gk = norm ? k_gamma : nullptr, *bk = norm ? k_beta : nullptr;
+    switch (HDT) {
+      case 1: return launch_attn_fa<1>(QKV, ldq, O, ldo, B, N, n_head, head_dim, gq, bq, gk, bk, eps, scale, s);
+      case 2: return launch_attn_fa<2>(QKV, ldq, O, ldo, B, N, n_head, head_dim, gq, bq, gk, bk, eps, scale, s);
+      case 3: return launch_attn_fa<3>(QKV, ldq, O, ldo, B, N, n_head, head_dim, gq, bq, gk, bk, eps, scale, s);
+      default: return launch_attn_fa<4>(QKV, ldq, O, ldo, B, N, n_head, head_dim, gq, bq, gk, bk, eps, scale, s);
     }
+  }
+  // generic path: head norms in place on the QKV rows, then the VALU kernel
+  if (norm) {
+    const int rc = sdp_qk_headnorm(dtype, (void*)QKV, ldq, (int64_t)B * N, n_head, head_dim, q_gamma, q_beta, k_gamma,
+                                   k_beta, eps, stream);
+    if (rc) return rc;
   }
   dim3 grid((N + 63) / 64, n_head, B);
   if (dtype == 1)

@@ -142,7 +142,8 @@ SDP_DEV float epi_act(int code, float v) {
   else return apply_act(code, v);
 }
 
-// Epilogue of one 256x256 tile held as acc[4 n-tiles][8 m-tiles] per wave.
+// Epilogue of one tile held as acc[4 n-tiles][8 m-tiles] per wave (wave's n base:
+// n0 + wn*64, m base: m0 + wm*128).
 template <int ACT>
 SDP_DEV void tile_epilogue(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int M, int N, int wm, int wn,
                            int fr, int fq) {
@@ -201,10 +202,10 @@ SDP_DEV void tile_epilogue(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, i
 // stores become one 16-B access per lane per pair (half the store instructions).
 SDP_DEV int pair_col0(int fq) { return 8 * (((fq & 1) << 1) | (fq >> 1)); }
 
-template <int ACT>
+template <int ACT, int TBN = BN>
 SDP_DEV void tile_epilogue16(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int M, int N, int wm,
                              int wn, int fr, int fq) {
-  if (n0 + BN > N) {  // ragged N: generic per-4 path
+  if (n0 + TBN > N) {  // ragged N: generic per-4 path
     tile_epilogue<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
     return;
   }
@@ -393,7 +394,103 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_deepx(
   }
   tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
 }
+
 }  // namespace fast
+
+// Half-width tile for two blocks per CU: 256x128x32 tiles, 4 waves (2 along M x 2
+// along N, 128x64 each as above), 3-slot LDS ring per operand (3 x 24 KiB = 72 KiB)
+// -> two co-resident blocks per CU, so one block's prologue / epilogue overlaps
+// the other's MFMAs.  LDS rows are 64 B (32 bf16): 16-B chunk c of row r at
+// c ^ ((r >> 2) & 3), conflict-free for 16 consecutive rows.
+namespace half {
+constexpr int BM = 256, BN = 128, BK = 32;
+constexpr int XT = BM * BK * 2, WT = BN * BK * 2, STAGE = XT + WT;  // 16 + 8 KiB
+constexpr int NT = 256;
+SDP_DEV int swz(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+// rows [row0, row0+nrows_tile) x 32 k, per wave `pieces` glds of 16 rows x 64 B
+template <int PIECES>
+SDP_DEV void stage(const bf16_t* __restrict__ base, int64_t ld, RowMap map, int row0, int nrows, int k0, char* lds,
+                   int wave, int lane) {
+  const int rr = lane >> 2, pc = lane & 3;
+#pragma unroll
+  for (int i = 0; i < PIECES; ++i) {
+    const int piece = wave * PIECES + i;
+    const int r = piece * 16 + rr;
+    const int c = swz(r, pc);
+    int grow = row0 + r;
+    grow = grow < nrows ? grow : nrows - 1;
+    const bf16_t* src = base + map(grow) * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const AS1 void*)src, (AS3 void*)(lds + piece * 1024), 16, 0, 0);
+  }
+}
+SDP_DEV bf16x8 frag(const char* lds, int r, int c) { return *(const bf16x8*)(lds + r * 64 + swz(r, c) * 16); }
+
+template <int ACT>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_256x128(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
+                                                           const bf16_t* __restrict__ W, int64_t ldw,
+                                                           Epi<bf16_t> epi, int M, int N, int K, int tiles_m,
+                                                           int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
+  const int nwg = tiles_m * tiles_n;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  const RowMap wmap{0x7fffffff, 0, 0};
+  const int nk = K / BK;
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: stages 0 and 1 (6 glds per wave each)
+  stage<4>(X, ldx, xmap, m0, M, 0, smem, wave, lane);
+  stage<2>(W, ldw, wmap, n0, N, 0, smem + XT, wave, lane);
+  if (nk > 1) {
+    stage<4>(X, ldx, xmap, m0, M, BK, smem + STAGE, wave, lane);
+    stage<2>(W, ldw, wmap, n0, N, BK, smem + STAGE + XT, wave, lane);
+    asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more2 = kt + 2 < nk;
+    if (more2) {
+      const int nx = cur >= 1 ? cur - 1 : 2;  // (cur + 2) % 3
+      char* st = smem + nx * STAGE;
+      stage<4>(X, ldx, xmap, m0, M, (kt + 2) * BK, st, wave, lane);
+      stage<2>(W, ldw, wmap, n0, N, (kt + 2) * BK, st + XT, wave, lane);
+    }
+    const char* xt = smem + cur * STAGE;
+    const char* wt = xt + XT;
+    bf16x8 bx[8], aw[4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bx[j] = frag(xt, wm * 128 + j * 16 + fr, fq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aw[i] = frag(wt, wn * 64 + i * 16 + fr, fq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[i], bx[j], acc[i][j], 0, 0, 0);
+    if (more2) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+  fast::tile_epilogue16<ACT, BN>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
+}
+}  // namespace half
+
 
 // ---------------------------------------------------------------------------
 // Generic masked kernel (fp32 exact-MFMA path and odd bf16 shapes).
@@ -498,12 +595,13 @@ extern "C" int sdp_gemm_force_generic(int on) {
 }
 
 // bf16 fast-kernel selection: 1 = 2-stage ring + 8-B stores, 3 = 2-stage ring + paired
-// 16-B stores, 5 = deep-X ring (3 X slots, 2 W slots, counted vmcnt) + 16-B stores
-// (default), 4 = no-store timing probe (wrong results; benchmarks only).
-static int g_fast_kernel = 5;
+// 16-B stores, 5 = deep-X ring (3 X slots, 2 W slots, counted vmcnt) + 16-B stores,
+// 7 = 256x128 tiles, 3-slot ring, two blocks per CU (default), 4 = no-store timing
+// probe (wrong results; benchmarks only).
+static int g_fast_kernel = 7;
 extern "C" int sdp_gemm_set_fast_kernel(int k) {
   int old = g_fast_kernel;
-  if (k == 1 || k == 3 || k == 4 || k == 5) g_fast_kernel = k;
+  if (k == 1 || k == 3 || k == 4 || k == 5 || k == 7) g_fast_kernel = k;
   return old;
 }
 
@@ -537,6 +635,14 @@ extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_
       const int tm = (M + fast::BM - 1) / fast::BM, tn = (N + fast::BN - 1) / fast::BN;
 #define SDP_FAST(A, E) hipLaunchKernelGGL((fast::gemm_bf16_256x256<A, E>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
                                        (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
+      if (g_fast_kernel == 7) {
+        const int hm = (M + half::BM - 1) / half::BM, hn = (N + half::BN - 1) / half::BN;
+#define SDP_HALF(A) hipLaunchKernelGGL((half::gemm_bf16_256x128<A>), dim3(hm * hn), dim3(half::NT), 0, s, \
+                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, hm, hn)
+        if (act == ACT_NONE) SDP_HALF(ACT_NONE); else if (act == ACT_GELU) SDP_HALF(ACT_GELU); else SDP_HALF(-1);
+#undef SDP_HALF
+        return SDP_CHECK_LAUNCH();
+      }
       if (g_fast_kernel == 5) {
 #define SDP_DEEP(A) hipLaunchKernelGGL((fast::gemm_bf16_deepx<A>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
                                        (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)

@@ -290,123 +290,146 @@ extern "C" int sdp_rowstats(int dtype, const void* X, int64_t ldx, int x_grp, in
 // ConvMixer's layer_norm_1, layers.py:102 + :20-24); the zero "same" padding is
 // applied to that normalised input, as in the reference.
 // Block = 32 channels x a band of output rows (+ halo) of one image, 128 threads.
-// The band is staged in LDS (storage type T, rows padded to an odd pixel pitch
-// -> conflict-free 8/16-B reads); thread = 4 channels x a 16-pixel output strip,
-// sliding the k-wide window along the row with the k*k taps read from LDS.
+// The band is staged in LDS (storage type T, rows padded with zeros to an odd
+// pixel pitch -> conflict-free 8-B reads, no bounds checks in the inner loop);
+// thread = 4 channels x a STRIP-pixel output strip: per kernel row it loads the
+// STRIP+k-1 window into registers and accumulates STRIP independent outputs.
 // ---------------------------------------------------------------------------
 constexpr int DW_CB = 32;
-constexpr int DW_STRIP = 16;
 constexpr int DW_THREADS = 128;
-constexpr int DW_LDS_BYTES = 64 * 1024;
+constexpr int DW_LDS_BYTES = 64 * 1024;       // preferred (several blocks per CU)
+constexpr int DW_LDS_MAX = 160 * 1024;        // fallback for wide images
 
-template <typename T, int KS>
+// Row maps used here are dense or group whole images (grp % (H*W) == 0), so the
+// physical row of pixel `local` of image b is xm(b*H*W) + local: one map
+// evaluation per block instead of a 64-bit division per pixel.
+template <typename T, int KS, int STRIP>
 __global__ __launch_bounds__(DW_THREADS) void dwconv_ln_nhwc(
     const T* __restrict__ X, int64_t ldx, RowMap xm, const float* __restrict__ stats, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ Wt, const float* __restrict__ bias, T* __restrict__ Y,
     int64_t ldy, RowMap ym, int H, int W, int C, int band, int pitch, int vec_in) {
   constexpr int PAD = KS / 2;
   extern __shared__ __attribute__((aligned(16))) char dsm[];
-  T* tile = (T*)dsm;                                                         // [TH][pitch][32]
+  T* tile = (T*)dsm;  // [TH][pitch][32]; columns >= W + KS - 1 are zero
   const int b = blockIdx.z;
   const int h0 = blockIdx.y * band;
   const int c0 = blockIdx.x * DW_CB;
   const int hb = min(band, H - h0);
-  const int TH = hb + KS - 1, TW = W + KS - 1;
+  const int TH = hb + KS - 1;
   float* wts = (float*)(dsm + (((size_t)band + KS - 1) * pitch * DW_CB * sizeof(T) + 15) / 16 * 16);  // [KS*KS][32]
   const int64_t img0 = (int64_t)b * H * W;
+  const int64_t xrow0 = xm(img0), yrow0 = ym(img0);
   const int tid = threadIdx.x;
 
   for (int i = tid; i < KS * KS * DW_CB; i += DW_THREADS) {
     const int tap = i / DW_CB, cc = i % DW_CB;
     wts[i] = (c0 + cc < C) ? Wt[(int64_t)(c0 + cc) * KS * KS + tap] : 0.f;
   }
-  // ---- stage LN(x) for the band + halo ----
+  // ---- stage LN(x) for the band + halo (zero outside the image / channel range) ----
   constexpr int EPL = 16 / sizeof(T);   // elements per 16-B lane load
   constexpr int LPP = DW_CB / EPL;      // lanes per pixel
-  for (int idx = tid; idx < TH * TW * LPP; idx += DW_THREADS) {
-    const int pix = idx / LPP, part = idx % LPP;
-    const int th = pix / TW, tw = pix % TW;
-    const int h = h0 + th - PAD, w = tw - PAD;
-    const int c = c0 + part * EPL;
-    float v[EPL];
+  constexpr int SLOTS = DW_THREADS / LPP;
+  const int part = tid % LPP, slot = tid / LPP;
+  const int c = c0 + part * EPL;
+  float g8[EPL], b8[EPL];
 #pragma unroll
-    for (int e = 0; e < EPL; ++e) v[e] = 0.f;
-    if (h >= 0 && h < H && w >= 0 && w < W) {
-      const int64_t m = img0 + (int64_t)h * W + w;
-      const T* src = X + xm(m) * ldx + c;
-      if (vec_in && c + EPL <= C) {
-        const f32x4 raw = *(const f32x4*)src;
-        const T* rv = (const T*)&raw;
+  for (int e = 0; e < EPL; ++e) {
+    g8[e] = (stats && c + e < C) ? lg[c + e] : 1.f;
+    b8[e] = (stats && c + e < C) ? lb[c + e] : 0.f;
+  }
+  // All loads of a batch of 8 items are issued before any is consumed (the loop
+  // is HBM-latency-bound otherwise: one dependent round trip per pixel row).
+  const int nitems = TH * pitch;  // pixels of the padded band, SLOTS per pass
+  const float inv_pitch = 1.0f / (float)pitch;
+  constexpr int UNR = 8;
+  for (int base = slot; base < nitems; base += SLOTS * UNR) {
+    f32x4 raw[UNR];
+    float2 st[UNR];
+    bool inb[UNR];
+    int local[UNR];
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) v[e] = to_f<T>(rv[e]);
-      } else {
+    for (int u = 0; u < UNR; ++u) {
+      const int pix = base + u * SLOTS;
+      const int th = (int)(((float)pix + 0.5f) * inv_pitch);
+      const int tw = pix - th * pitch;
+      const int h = h0 + th - PAD, w = tw - PAD;
+      inb[u] = pix < nitems && h >= 0 && h < H && w >= 0 && w < W;
+      local[u] = h * W + w;
+      raw[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      st[u] = float2{0.f, 1.f};
+      if (inb[u]) {
+        const T* src = X + (xrow0 + local[u]) * ldx + c;
+        if (vec_in && c + EPL <= C) {
+          raw[u] = *(const f32x4*)src;
+        } else {
+          T* rv = (T*)&raw[u];
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) if (c + e < C) v[e] = to_f<T>(src[e]);
-      }
-      if (stats) {
-        const float mean = stats[2 * m], rstd = stats[2 * m + 1];
-#pragma unroll
-        for (int e = 0; e < EPL; ++e)
-          if (c + e < C) v[e] = (v[e] - mean) * rstd * lg[c + e] + lb[c + e];
+          for (int e = 0; e < EPL; ++e) rv[e] = (c + e < C) ? src[e] : from_f<T>(0.f);
+        }
+        if (stats) st[u] = *(const float2*)(stats + 2 * (img0 + local[u]));
       }
     }
-    T* dst = tile + ((size_t)th * pitch + tw) * DW_CB + part * EPL;
-    if constexpr (sizeof(T) == 2) {
-      bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(v[e]);
-      *(bf16x8*)dst = o;
-    } else {
-      *(f32x4*)dst = f32x4{v[0], v[1], v[2], v[3]};
+    for (int u = 0; u < UNR; ++u) {
+      const int pix = base + u * SLOTS;
+      if (pix >= nitems) break;
+      float v[EPL];
+      const T* rv = (const T*)&raw[u];
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        v[e] = inb[u] ? to_f<T>(rv[e]) : 0.f;
+        if (stats && inb[u]) v[e] = (v[e] - st[u].x) * st[u].y * g8[e] + b8[e];
+        if (c + e >= C) v[e] = 0.f;
+      }
+      T* dst = tile + (size_t)pix * DW_CB + part * EPL;
+      if constexpr (sizeof(T) == 2) {
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(v[e]);
+        *(bf16x8*)dst = o;
+      } else {
+        *(f32x4*)dst = f32x4{v[0], v[1], v[2], v[3]};
+      }
     }
   }
   __syncthreads();
 
-  const int cq = tid & 7;          // channels 4cq .. 4cq+3 of the block
-  const int grp = tid >> 3;        // 16 strip workers
+  const int cq = tid & 7;    // channels 4cq .. 4cq+3 of the block
+  const int grp = tid >> 3;  // 16 strip workers
   const int cg = c0 + cq * 4;
   const f32x4 bv = (bias && cg + 3 < C) ? *(const f32x4*)(bias + cg) : f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nstrip = (W + DW_STRIP - 1) / DW_STRIP;
+  const int nstrip = (W + STRIP - 1) / STRIP;
   for (int job = grp; job < hb * nstrip; job += DW_THREADS / 8) {
     const int oh = job / nstrip;
-    const int w0 = (job % nstrip) * DW_STRIP;
-    f32x4 acc[DW_STRIP];
+    const int w0 = (job - oh * nstrip) * STRIP;
+    f32x4 acc[STRIP];
 #pragma unroll
-    for (int o = 0; o < DW_STRIP; ++o) acc[o] = bv;
+    for (int o = 0; o < STRIP; ++o) acc[o] = bv;
     for (int ky = 0; ky < KS; ++ky) {
-      f32x4 wk[KS];
-#pragma unroll
-      for (int kx = 0; kx < KS; ++kx) wk[kx] = *(const f32x4*)&wts[(ky * KS + kx) * DW_CB + cq * 4];
       const T* trow = tile + ((size_t)(oh + ky) * pitch + w0) * DW_CB + cq * 4;
+      f32x4 win[STRIP + KS - 1];
 #pragma unroll
-      for (int ix = 0; ix < DW_STRIP + KS - 1; ++ix) {
-        f32x4 v;
-        if (w0 + ix < TW) {
-          if constexpr (sizeof(T) == 2) {
-            const bf16x4 t = *(const bf16x4*)(trow + ix * DW_CB);
-            v = f32x4{bf2f((bf16_t)t[0]), bf2f((bf16_t)t[1]), bf2f((bf16_t)t[2]), bf2f((bf16_t)t[3])};
-          } else {
-            v = *(const f32x4*)(trow + ix * DW_CB);
-          }
+      for (int ix = 0; ix < STRIP + KS - 1; ++ix) {
+        if constexpr (sizeof(T) == 2) {
+          const bf16x4 t = *(const bf16x4*)(trow + ix * DW_CB);
+          win[ix] = f32x4{bf2f((bf16_t)t[0]), bf2f((bf16_t)t[1]), bf2f((bf16_t)t[2]), bf2f((bf16_t)t[3])};
         } else {
-          v = f32x4{0.f, 0.f, 0.f, 0.f};
+          win[ix] = *(const f32x4*)(trow + ix * DW_CB);
         }
+      }
 #pragma unroll
-        for (int kx = 0; kx < KS; ++kx) {
-          const int o = ix - kx;
-          if (o >= 0 && o < DW_STRIP) {
+      for (int kx = 0; kx < KS; ++kx) {
+        const f32x4 wv = *(const f32x4*)&wts[(ky * KS + kx) * DW_CB + cq * 4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[o][r] = fmaf(v[r], wk[kx][r], acc[o][r]);
-          }
-        }
+        for (int o = 0; o < STRIP; ++o) acc[o] += win[o + kx] * wv;
       }
     }
     const int gh = h0 + oh;
 #pragma unroll
-    for (int o = 0; o < DW_STRIP; ++o) {
+    for (int o = 0; o < STRIP; ++o) {
       const int w = w0 + o;
       if (w < W) {
-        T* dst = Y + ym(img0 + (int64_t)gh * W + w) * ldy + cg;
+        T* dst = Y + (yrow0 + (int64_t)gh * W + w) * ldy + cg;
         if (cg + 3 < C) {
           if constexpr (sizeof(T) == 2) {
             bf16x4 t;
@@ -425,24 +448,40 @@ __global__ __launch_bounds__(DW_THREADS) void dwconv_ln_nhwc(
   }
 }
 
-template <typename T, int KS>
+template <typename T, int KS, int STRIP>
 static int launch_dw(const void* X, int64_t ldx, RowMap xm, const float* stats, const float* lg, const float* lb,
                      const float* Wt, const float* bias, void* Y, int64_t ldy, RowMap ym, int B, int H, int W, int C,
                      hipStream_t s) {
-  const int TW = W + KS - 1;
-  const int pitch = TW | 1;  // odd pixel pitch: rows land on different LDS banks
+  const int nstrip = (W + STRIP - 1) / STRIP;
+  const int TWp = nstrip * STRIP + KS - 1;  // widest column a strip window touches
+  const int pitch = TWp | 1;                // odd pixel pitch: rows land on different LDS banks
   const size_t row_bytes = (size_t)pitch * DW_CB * sizeof(T);
   const size_t wbytes = (size_t)KS * KS * DW_CB * 4 + 16;
   int band = (int)((DW_LDS_BYTES - wbytes) / row_bytes) - (KS - 1);
+  if (band < 1) band = (int)((DW_LDS_MAX - wbytes) / row_bytes) - (KS - 1);
   if (band < 1) return (int)hipErrorInvalidValue;  // image too wide for the LDS band
   band = band > H ? H : band;
   const int nb = (H + band - 1) / band;
   const size_t lds = ((size_t)(band + KS - 1) * row_bytes + 15) / 16 * 16 + (size_t)KS * KS * DW_CB * 4;
   dim3 grid((C + DW_CB - 1) / DW_CB, nb, B);
   const int vec_in = ((ldx * (int64_t)sizeof(T)) % 16 == 0) && ((uintptr_t)X % 16 == 0);
-  hipLaunchKernelGGL((dwconv_ln_nhwc<T, KS>), grid, dim3(DW_THREADS), lds, s, (const T*)X, ldx, xm, stats, lg, lb,
-                     Wt, bias, (T*)Y, ldy, ym, H, W, C, band, pitch, vec_in);
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)dwconv_ln_nhwc<T, KS, STRIP>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL((dwconv_ln_nhwc<T, KS, STRIP>), grid, dim3(DW_THREADS), lds, s, (const T*)X, ldx, xm, stats, lg,
+                     lb, Wt, bias, (T*)Y, ldy, ym, H, W, C, band, pitch, vec_in);
   return SDP_CHECK_LAUNCH();
+}
+
+template <typename T, int KS>
+static int dw_strip(int W, const void* X, int64_t ldx, RowMap xm, const float* stats, const float* lg,
+                    const float* lb, const float* Wt, const float* bias, void* Y, int64_t ldy, RowMap ym, int B, int H,
+                    int C, hipStream_t s) {
+  if (W % 14 == 0)  // SdP-Net-M (14x14): no wasted strip columns
+    return launch_dw<T, KS, 14>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
+  return launch_dw<T, KS, 16>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
 }
 
 template <typename T>
@@ -450,11 +489,11 @@ static int dw_dispatch(int k, const void* X, int64_t ldx, RowMap xm, const float
                        const float* lb, const float* Wt, const float* bias, void* Y, int64_t ldy, RowMap ym, int B,
                        int H, int W, int C, hipStream_t s) {
   switch (k) {
-    case 1: return launch_dw<T, 1>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
-    case 3: return launch_dw<T, 3>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
-    case 5: return launch_dw<T, 5>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
-    case 7: return launch_dw<T, 7>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
-    case 9: return launch_dw<T, 9>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s);
+    case 1: return dw_strip<T, 1>(W, X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, C, s);
+    case 3: return dw_strip<T, 3>(W, X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, C, s);
+    case 5: return dw_strip<T, 5>(W, X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, C, s);
+    case 7: return dw_strip<T, 7>(W, X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, C, s);
+    case 9: return dw_strip<T, 9>(W, X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, C, s);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -469,6 +508,8 @@ extern "C" int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int6
   if ((ldy * esz) % 8 || ((uintptr_t)Y % 8) || ((uintptr_t)X % esz)) return (int)hipErrorInvalidValue;
   if (bias && ((uintptr_t)bias % 16)) return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
+  // row maps must be dense or group whole images (see dwconv_ln_nhwc)
+  if ((x_grp > 0 && x_grp % (H * W)) || (y_grp > 0 && y_grp % (H * W))) return (int)hipErrorInvalidValue;
   const RowMap xm = mk_rmap(x_grp, x_gstride, x_off), ym = mk_rmap(y_grp, y_gstride, y_off);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == 1) return dw_dispatch<bf16_t>(k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s);

@@ -376,14 +376,13 @@ class EncoderLayer(nn.Module):
         sp.layernorm(_dense(tok), w["n1g"], w["n1b"], w["n1e"], _dense(h), T, C)            # :280
         qkv = torch.empty(T, 3 * C, dtype=dt, device=dev)
         sp.gemm(_dense(h), w["wqkv"], _dense(qkv), T, 3 * C, C)                            # :282-284
-        if "qg" in w:
-            sp.qk_headnorm(qkv, T, Hn, hd, w["qg"], w["qb"], w["kg"], w["kb"], w["qe"])     # :286
+        qkn = (w["qg"], w["qb"], w["kg"], w["kb"]) if "qg" in w else None                  # :286 (fused)
         att = torch.empty(T, C, dtype=dt, device=dev)
         if mask is not None:
             mb, sb, sh = self._mask_bias(mask, B, N)
-            sp.attention(qkv, att, B, N, Hn, hd, mb, sb, sh)                                # :289-298
+            sp.attention(qkv, att, B, N, Hn, hd, mb, sb, sh, qk_norm=qkn, eps=w.get("qe", 1e-5))  # :289-298
         else:
-            sp.attention(qkv, att, B, N, Hn, hd)
+            sp.attention(qkv, att, B, N, Hn, hd, qk_norm=qkn, eps=w.get("qe", 1e-5))
         sp.gemm(_dense(att), w["wo"], _dense(tok), T, C, C, resid=_dense(tok))             # :300-303
         sp.layernorm(_dense(tok), w["n2g"], w["n2b"], w["n2e"], _dense(h), T, C)            # :307
         F_ = w["w1"].shape[0]
@@ -525,8 +524,9 @@ class ClassificationHead(nn.Module):
             return d
         return cached(self, "w", params, dt, build)
 
-    def _run(self, src: Rows, B: int, rows: int, C: int, dt) -> torch.Tensor:
-        """src: B groups of `rows` logical rows to average (registers or pixels)."""
+    def _run(self, src: Rows, B: int, rows: int, C: int, dt, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """src: B groups of `rows` logical rows to average (registers or pixels).
+        Logits go to ``out`` [B, classes] when given (written in place)."""
         w = self._prep(dt)
         dev = src.t.device
         h = torch.empty(B, C, dtype=dt, device=dev)
@@ -536,15 +536,15 @@ class ClassificationHead(nn.Module):
             sp.layernorm(_dense(h), g, b, eps, _dense(h), B, C)
         (w1, b1) = w["lin"][0]
         n1 = w1.shape[0]
-        y = torch.empty(B, n1, dtype=dt, device=dev)
         two = len(w["lin"]) == 2
+        y = out if (out is not None and not two) else torch.empty(B, n1, dtype=dt, device=dev)
         sp.gemm(_dense(h), w1, _dense(y), B, n1, C, bias=b1, act=sp.ACT_CODES["tanh"] if two else 0)
         if not two:
             return y
         (w2, b2) = w["lin"][1]
-        out = torch.empty(B, w2.shape[0], dtype=dt, device=dev)
-        sp.gemm(_dense(y), w2, _dense(out), B, w2.shape[0], n1, bias=b2)
-        return out
+        res = out if out is not None else torch.empty(B, w2.shape[0], dtype=dt, device=dev)
+        sp.gemm(_dense(y), w2, _dense(res), B, w2.shape[0], n1, bias=b2)
+        return res
 
     def forward(self, x: torch.Tensor, registers: torch.Tensor) -> torch.Tensor:
         check_eval(self)

@@ -17,6 +17,7 @@ CUDA bf16 autocast region run the bf16 path (bf16 storage, fp32 accumulate).
 """
 from __future__ import annotations
 
+import os
 from typing import Callable
 
 import torch
@@ -121,6 +122,26 @@ class MainModel(SdPModel):
             return pos
         return cached(emb, f"pos{Hp}x{Wp}_{dt}", [pos], dt, lambda: as_dtype(pos, dt))
 
+    def _prepare(self, dt, Hp: int, Wp: int):
+        """Build every prepared-weight cache on the current stream (before any fork)."""
+        self.conv_init._weight(dt)
+        self._pos_rows(Hp, Wp, dt)
+        for blk in self.blocks:
+            blk.t_block._prep(dt)
+            for mx in blk.conv_blocks:
+                mx._prep(dt)
+                mx.layer_norm_1._params()
+                mx.layer_norm_2._params()
+        self.final_block.t_block._prep(dt)
+        self.output_head._prep(dt)
+
+    def _num_streams(self, B: int) -> int:
+        n = getattr(self, "num_streams", None)
+        if n is None:
+            env = os.environ.get("SDPNET_STREAMS")
+            n = int(env) if env else (2 if B >= 64 else 1)
+        return max(1, min(int(n), B))
+
     def forward(self, x: torch.Tensor, num_registers: int = 3, return_raw_outputs: bool = False):
         check_eval(self)
         if _hooked(self):
@@ -130,35 +151,63 @@ class MainModel(SdPModel):
             B, _, Hi, Wi = x.shape
             p = self.conv_init.patch_size
             Hp, Wp = Hi // p, Wi // p
-            P = Hp * Wp
             C = self.conv_init.conv.out_channels
-            emb = self.embedding_layer
-            table, R = emb._register_rows(num_registers)
-            N = R + P
-            tok = torch.empty(B * N, C, dtype=dt, device=x.device)
-            img = Rows(tok, C, P, N, R)
-            # patch GEMM + positional table (+ embedding activation) into the image rows
-            # (layers.py:40-42, :157-168 / :205)
-            self.conv_init._run(x, dt, img,
-                                resid=Rows(self._pos_rows(Hp, Wp, dt), C, P, 0, 0), act=act_code(emb.activation))
-            if R:
-                sp.copy_rows(table.contiguous(), C, 0, tok, C, N * C, B, R, C)
-            for block in self.blocks:                                     # model.py:139-140
-                block._run_tokens(tok, B, R, Hp, Wp, dt)
-            self.final_block._run_tokens(tok, B, R, Hp, Wp, dt)           # model.py:143
-            head = self.output_head                                       # model.py:146
-            if head.from_register:
-                logits = head._run(Rows(tok, C, R, N, 0), B, R, C, dt)
-            else:
-                logits = head._run(img, B, P, C, dt)
-            if not return_raw_outputs:
-                return logits
-            xo = torch.empty(B, C, Hp, Wp, dtype=dt, device=x.device)
-            sp.rows_to_nchw(img, xo)
-            regs = torch.empty(B, R, C, dtype=dt, device=x.device)
-            if R:
-                sp.copy_rows(tok, C, N * C, regs, C, R * C, B, R, C)
-            return logits, xo, regs
+            ncls = self.output_head._prep(dt)["lin"][-1][0].shape[0]
+            self._prepare(dt, Hp, Wp)
+            x = x.contiguous()
+            logits = torch.empty(B, ncls, dtype=dt, device=x.device)
+            ns = 1 if return_raw_outputs else self._num_streams(B)
+            if ns == 1:
+                raw = self._forward_chunk(x, logits, num_registers, dt, Hp, Wp, C, return_raw_outputs)
+                return logits if not return_raw_outputs else (logits, *raw)
+            # Independent sub-batches on concurrent HIP streams: one chunk's tail waves and
+            # memory-bound kernels overlap the other's GEMMs (no data dependence between images).
+            main = torch.cuda.current_stream(x.device)
+            streams = self.__dict__.setdefault("_sdp_streams", {}).setdefault(
+                (x.device, ns), [torch.cuda.Stream(device=x.device) for _ in range(ns)])
+            step = (B + ns - 1) // ns
+            for i, s in enumerate(streams):
+                lo, hi = i * step, min(B, (i + 1) * step)
+                if lo >= hi:
+                    continue
+                s.wait_stream(main)
+                with torch.cuda.stream(s):
+                    self._forward_chunk(x[lo:hi], logits[lo:hi], num_registers, dt, Hp, Wp, C, False)
+            for s in streams:
+                main.wait_stream(s)
+            return logits
+
+    def _forward_chunk(self, x, logits, num_registers, dt, Hp, Wp, C, return_raw_outputs):
+        """Fused forward of one (sub-)batch on the current stream; logits written in place."""
+        B = x.shape[0]
+        P = Hp * Wp
+        emb = self.embedding_layer
+        table, R = emb._register_rows(num_registers)
+        N = R + P
+        tok = torch.empty(B * N, C, dtype=dt, device=x.device)
+        img = Rows(tok, C, P, N, R)
+        # patch GEMM + positional table (+ embedding activation) into the image rows
+        # (layers.py:40-42, :157-168 / :205)
+        self.conv_init._run(x, dt, img, resid=Rows(self._pos_rows(Hp, Wp, dt), C, P, 0, 0),
+                            act=act_code(emb.activation))
+        if R:
+            sp.copy_rows(table.contiguous(), C, 0, tok, C, N * C, B, R, C)
+        for block in self.blocks:                                     # model.py:139-140
+            block._run_tokens(tok, B, R, Hp, Wp, dt)
+        self.final_block._run_tokens(tok, B, R, Hp, Wp, dt)           # model.py:143
+        head = self.output_head                                       # model.py:146
+        if head.from_register:
+            head._run(Rows(tok, C, R, N, 0), B, R, C, dt, out=logits)
+        else:
+            head._run(img, B, P, C, dt, out=logits)
+        if not return_raw_outputs:
+            return None
+        xo = torch.empty(B, C, Hp, Wp, dtype=dt, device=x.device)
+        sp.rows_to_nchw(img, xo)
+        regs = torch.empty(B, R, C, dtype=dt, device=x.device)
+        if R:
+            sp.copy_rows(tok, C, N * C, regs, C, R * C, B, R, C)
+        return xo, regs
 
     def _forward_modules(self, x, num_registers, return_raw_outputs):
         """Module-by-module composition (model.py:129-149) used while forward hooks

@@ -40,7 +40,8 @@ _SIGS = {
     "sdp_rowstats": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _i32, _i32, _vp], _i32),
     "sdp_dwconv": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _i32,
                     _i32, _i32, _vp], _i32),
-    "sdp_attention": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _vp], _i32),
+    "sdp_attention": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _i64,
+                       _i64, _vp], _i32),
     "sdp_attention_variant": ([_i32, _i32, _i32, _i32, _i32], _i32),
     "sdp_patchify": ([_i32, _vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp], _i32),
     "sdp_pos_table": ([_vp, _vp, _vp, _i32, _i32, _i32, _vp], _i32),
@@ -195,11 +196,16 @@ def dwconv(x: Rows, weight: torch.Tensor, bias: Optional[torch.Tensor], y: Rows,
 
 
 def attention(qkv: torch.Tensor, out: torch.Tensor, B: int, N: int, n_head: int, head_dim: int,
-              mask: Optional[torch.Tensor] = None, mask_sb: int = 0, mask_sh: int = 0):
+              mask: Optional[torch.Tensor] = None, mask_sb: int = 0, mask_sh: int = 0, qk_norm=None,
+              eps: float = 1e-5):
+    """qk_norm = (q_gamma, q_beta, k_gamma, k_beta) fp32 or None.  NOTE: when the
+    generic kernel is taken the norms are applied in place on ``qkv``."""
     _need_cuda(qkv, out, mask)
     assert qkv.dtype == out.dtype
+    gq, bq, gk, bk = qk_norm if qk_norm is not None else (None, None, None, None)
     rc = lib().sdp_attention(dcode(qkv.dtype), qkv.data_ptr(), qkv.stride(0), out.data_ptr(), out.stride(0), B, N,
-                             n_head, head_dim, _ptr(mask), mask_sb, mask_sh, _stream(out))
+                             n_head, head_dim, _ptr(gq), _ptr(bq), _ptr(gk), _ptr(bk), float(eps), _ptr(mask),
+                             mask_sb, mask_sh, _stream(out))
     _check(rc, "attention")
 
 

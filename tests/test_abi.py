@@ -41,8 +41,8 @@ def test_gemm_variant_selection():
 
 def test_attention_variant_selection():
     L = sp.lib()
-    assert L.sdp_attention_variant(1, 200, 8, 96, 0) == 1
-    assert L.sdp_attention_variant(1, 260, 8, 96, 0) == 1
+    assert L.sdp_attention_variant(1, 200, 8, 96, 0) == 2
+    assert L.sdp_attention_variant(1, 260, 8, 96, 0) == 2
     assert L.sdp_attention_variant(1, 200, 8, 96, 1) == 0   # masks -> generic
     assert L.sdp_attention_variant(0, 200, 8, 96, 0) == 0   # fp32 -> generic
     assert L.sdp_attention_variant(1, 53, 8, 12, 0) == 0    # hd % 8 != 0
@@ -54,7 +54,7 @@ def test_invalid_arguments_rejected_before_launch():
     assert L.sdp_gemm(1, None, 64, 0, 0, 0, None, 64, None, None, 0, 0, 0, 0, None, 64, 0, 0, 0,
                       128, 128, 64, 0, 0, None) == 1
     assert L.sdp_layernorm(1, None, 8, 0, 0, 0, None, None, 1e-5, None, 8, 0, 0, 0, 4, 8, None) == 1
-    assert L.sdp_attention(1, None, 8, None, 8, 1, 4, 1, 8, None, 0, 0, None) == 1
+    assert L.sdp_attention(1, None, 8, None, 8, 1, 4, 1, 8, None, None, None, None, 1e-5, None, 0, 0, None) == 1
     assert L.sdp_patchify(0, None, 1, None, 1, 224, 224, 16, 768, None) == 1
     assert L.sdp_cast(0, None, 1, None, 10, None) == 1
     # degenerate sizes are no-ops

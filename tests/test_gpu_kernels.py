@@ -211,9 +211,26 @@ def test_attention(dtype, B, N, H, hd):
 
 
 def test_attention_mfma_path_is_taken_for_canonical_shapes():
-    assert sp.attention_variant(BF, 200, 8, 96) == 1
-    assert sp.attention_variant(BF, 260, 8, 96) == 1
-    assert sp.attention_variant(BF, 200, 8, 16) == 1
+    assert sp.attention_variant(BF, 200, 8, 96) == 2
+    assert sp.attention_variant(BF, 260, 8, 96) == 2
+    assert sp.attention_variant(BF, 200, 8, 16) == 2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("B,N,H,hd", [(2, 200, 8, 96), (1, 260, 8, 96), (2, 53, 4, 16), (1, 77, 2, 64),
+                                      (2, 33, 8, 12), (1, 300, 2, 128)])
+def test_attention_fused_qk_norm(dtype, B, N, H, hd):
+    C = H * hd
+    qkv = rnd(B * N, 3 * C, dtype=dtype, seed=44, scale=2.0)
+    gq, bq, gk, bk = (rnd(hd, seed=s) * 0.1 + (1 if s % 2 == 0 else 0) for s in (45, 46, 47, 48))
+    ref_in = qkv.float().clone()
+    ref_in[:, :C] = F.layer_norm(ref_in[:, :C].view(-1, H, hd), (hd,), gq, bq).view(-1, C)
+    ref_in[:, C:2 * C] = F.layer_norm(ref_in[:, C:2 * C].view(-1, H, hd), (hd,), gk, bk).view(-1, C)
+    ref = attn_ref(ref_in.to(dtype), B, N, H, hd)
+    o = torch.empty(B * N, C, dtype=dtype, device=DEV)
+    sp.attention(qkv, o, B, N, H, hd, qk_norm=(gq, bq, gk, bk), eps=1e-5)
+    close(o, ref, dtype, rel=2e-5 if dtype == torch.float32 else 2e-2,
+          what=f"fused qk-norm attn variant {sp.attention_variant(dtype, N, H, hd)}")
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
@@ -311,10 +328,11 @@ def test_nchw_add_table():
     assert torch.allclose(x, ref, atol=1e-6)
 
 
-@pytest.mark.parametrize("kern", [1, 3, 5])
+@pytest.mark.parametrize("kern", [1, 3, 5, 7])
 @pytest.mark.parametrize("M,N,K,act,res", [(1000, 768, 768, 1, True), (300, 384, 128, 0, False),
                                            (777, 3072, 768, 1, False), (520, 768, 3072, 0, True),
-                                           (256, 256, 64, 3, True), (600, 2304, 192, 0, False)])
+                                           (256, 256, 64, 3, True), (600, 2304, 192, 0, False),
+                                           (5000, 768, 768, 1, True), (3000, 512, 640, 0, True)])
 def test_gemm_fast_kernel_variants(kern, M, N, K, act, res):
     x = rnd(M, K, dtype=BF, seed=60)
     w = rnd(N, K, dtype=BF, seed=61, scale=0.05)

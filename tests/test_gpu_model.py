@@ -238,3 +238,17 @@ def test_cuda_graph_capture_replays_identically():
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(y_static, y_eager)
+
+
+def test_multistream_equals_single_stream():
+    m, meta, arr, x = get_model("xxs_cf_b4")
+    xd = x.to(DEV).to(torch.bfloat16).repeat(20, 1, 1, 1)[:70]
+    m.num_streams = 1
+    y1 = m(xd)
+    m.num_streams = 3
+    try:
+        y3 = m(xd)
+    finally:
+        del m.num_streams
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y3)

@@ -19,7 +19,17 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) step benchq 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
-    gemm) step gemm 600 python tools/gemm_bench.py --streams 1 --kernels 3,5 ;;
+    gemm) step gemm 600 python tools/gemm_bench.py --streams 1 --kernels 5,7 ;;
+    streams) step s1 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 1 &&
+             step s2 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 2 &&
+             step s3 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 3 &&
+             step s4 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 4 ;;
+    kb) step kb 300 python tools/kern_bench.py ;;
+    pmc) export TMPDIR=/tmp; rm -rf gpurun_out/pmc*
+         step pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES -d gpurun_out/pmc1 -o run --output-format csv -- python tools/kern_bench.py --reps 3 &&
+         step pmc2 600 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmc2 -o run --output-format csv -- python tools/kern_bench.py --reps 3 &&
+         step pmc3 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc3 -o run --output-format csv -- python tools/kern_bench.py --reps 3 &&
+         step pmc4 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc4 -o run --output-format csv -- python tools/kern_bench.py --reps 3 ;;
     prof) export TMPDIR=/tmp; rm -rf gpurun_out/prof
           step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-graph --prof-steps 1 ;;
   esac
