@@ -11,7 +11,7 @@ its own independent batch shard (weak scaling), no data-path collective; barrier
 + max-over-ranks timing only.
 
 Also reported on the same JSON line:
-  roofline     — dominant kernel (gemm_bf16_256x256, ~98 % of FLOPs): algorithmic
+  roofline     — dominant kernel (the bf16 fast GEMM, ~98 % of FLOPs): algorithmic
                  FLOPs of its launches / their HIP-event durations (on the launch
                  stream), vs the dense bf16 MFMA peak.
   cpu_baseline — the oracle (the reference's math in stock PyTorch CPU ops,
@@ -29,6 +29,8 @@ sys.path.insert(0, os.path.join(REPO, "sdp-net_amd"))
 
 METRIC = "images/sec fwd SdP-Net-M 224×224 bs=256 @1 GPU; scaling 1/2/4/8"
 MFMA_BF16_PEAK_TFLOPS = 2516.6   # 256 CU x 2.4 GHz x 4096 FLOP/clk/CU (dense)
+FAST_GEMM_NAMES = {1: "gemm_bf16_256x256", 3: "gemm_bf16_256x256", 5: "gemm_bf16_deepx", 7: "gemm_bf16_256x128",
+                   8: "gemm_bf16_256x128i", 9: "gemm_bf16_8ph"}
 
 M_CFG = dict(embedding_dim=768, num_blocks=12, n_head=8, activation="gelu", embedding_activation="none",
              conv_kernel_size=7, patch_size=16, ffn_dropout=0.2, attn_dropout=0.2, output_classes=1000,
@@ -155,11 +157,17 @@ def main():
         rec.setdefault(key, []).append((flops, e0, e1))
 
     old = sp.set_launch_timer(timer)
+    ns_saved = getattr(m, "num_streams", None)
+    m.num_streams = 1  # per-launch events must not include the other stream's overlap
     try:
         for _ in range(max(1, args.prof_steps)):
             step()
     finally:
         sp.set_launch_timer(old)
+        if ns_saved is None:
+            del m.num_streams
+        else:
+            m.num_streams = ns_saved
     torch.cuda.synchronize()
     fast_fl = fast_ms = 0.0
     fast_n = 0
@@ -169,7 +177,7 @@ def main():
         fl = sum(f for f, _, _ in lst)
         per_shape[f"{key[0]}x{key[1]}x{key[2]}"] = dict(launches=len(lst), avg_us=round(1e3 * ms / len(lst), 2),
                                                         tflops=round(fl / (ms * 1e-3) / 1e12, 1),
-                                                        kernel="gemm_bf16_256x256" if key[3] == 1 else "gemm_generic")
+                                                        kernel="gemm_bf16_fast" if key[3] == 1 else "gemm_generic")
         if key[3] == 1:
             fast_fl += fl
             fast_ms += ms
@@ -199,7 +207,7 @@ def main():
                    "parallelism": f"dp{world} independent batch shards (no collective)"},
         "model_flops_per_image_gf": round(gf, 3),
         "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
-        "roofline": {"bound": "mfma", "kernel": "gemm_bf16_256x256",
+        "roofline": {"bound": "mfma", "kernel": FAST_GEMM_NAMES.get(sp.lib().sdp_gemm_set_fast_kernel(0), "?"),
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
                      "launches_per_step": fast_n // max(1, args.prof_steps),

@@ -13,12 +13,15 @@
 // covers  act(conv)+x  (ConvMixer), x + FFN (+bias) (Encoder), pos-emb add +
 // embedding activation (EmbeddingLayer), Tanh (head).
 //
-// Two kernels:
-//  * gemm_bf16_256x256 — the hot kernel: 256x256x64 tiles, 8 waves (2 along M x
+// Kernels (bf16 fast path selected by sdp_gemm_set_fast_kernel, default 9):
+//  * gemm_bf16_8ph (9) — the hot kernel: 256x256x64 tiles, 8 waves (2 along M x
 //    4 along N, 128x64 per wave), v_mfma_f32_16x16x32_bf16, both operands staged
 //    HBM->LDS by global_load_lds_dwordx4 into an XOR-swizzled [row][64] image
-//    (conflict-free ds_read_b128), two LDS stages, XCD-aware tile order.
+//    (conflict-free ds_read_b128), 4 phases per K-tile with the two wave groups
+//    ping-ponging MFMA against LDS traffic, XCD-aware tile order.
 //    Requires K % 64 == 0; any M, N (clamped loads, masked stores).
+//  * gemm_bf16_256x256 (1/3/4), gemm_bf16_deepx (5), half::gemm_bf16_256x128[i]
+//    (7/8) — earlier schedules kept for A/B measurement.
 //  * gemm_generic<T> — correctness path for fp32 (exact f32 MFMA
 //    v_mfma_f32_16x16x4_f32) and for odd bf16 shapes; fully masked.
 //
@@ -395,18 +398,180 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_deepx(
   tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
 }
 
+// ---------------------------------------------------------------------------
+// 8-phase ping-pong kernel: 256x256x64 tiles, 8 waves (2 along M x 4 along N,
+// 128x64 per wave), two LDS buffers of one K-tile each (X + W = 64 KiB).
+//
+// A K-tile is consumed in 4 phases, one 64(m) x 32(n) C-quadrant x K=64 each
+// (16 MFMAs): Q(m0,n0), Q(m0,n1), Q(m1,n1), Q(m1,n0), so a phase reads 12, 4, 8
+// or 0 fragments.  Each phase is
+//     ds_read fragments ; issue LDS-DMA ; [counted vmcnt] ; s_barrier ;
+//     lgkmcnt(0) ; setprio(1) ; 16 MFMA ; setprio(0) ; s_barrier
+// and the wave group wm=1 runs one barrier behind wm=0, so on every SIMD one
+// wave is in its MFMA burst while the other issues its LDS reads / DMA.
+//
+// The K-tile's LDS image is filled in three sub-stages, ordered by first use:
+//   S1 = X rows of m-half 0 of both wave groups + W rows of n-half 0 of all waves
+//        (read in phase 0; 4 DMA per wave), S2 = W rows of n-half 1 (phase 1; 2),
+//   S3 = X rows of m-half 1 (phase 2; 2).
+// Schedule (tile t): phase 0 issues S3(t+1), phase 2 S1(t+2), phase 3 S2(t+2).
+// With the staggered groups a DMA'd region may be read in phase p only after
+// every wave's vmcnt wait in phase p-1, and overwritten in phase p only if its
+// last read was in phase <= p-2; the schedule meets both with 5 phases
+// (about one K-tile of MFMA time) between issue and retirement:
+//   phase 0: vmcnt(10) retires S2(t); phase 1: vmcnt(8) retires S3(t);
+//   phase 3: vmcnt(10) retires S1(t+1)   (smaller counts at the K tail).
+// ---------------------------------------------------------------------------
+constexpr int BUF8 = 2 * TILE_BYTES;
+
+#define SDP_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+template <int ACT>
+__global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
+                                                         const bf16_t* __restrict__ W, int64_t ldw, Epi<bf16_t> epi,
+                                                         int M, int N, int K, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF8];
+  const int nwg = tiles_m * tiles_n;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = K / BK;
+
+  // The wave's 8 DMA pieces per K-tile (8 rows x 128 B each): [0,1] S1-X,
+  // [2,3] S1-W, [4,5] S2-W, [6,7] S3-X.  Source pointers advance by BK per tile.
+  const bf16_t* src[8];
+  int loff[8];
+  {
+    const int rr = lane >> 3, pc = lane & 7;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int idx = wave * 2 + (s & 1);  // 0..15
+      int piece;
+      bool isx;
+      if (s < 2) { piece = idx < 8 ? idx : idx + 8; isx = true; }
+      else if (s < 4) { piece = (idx >> 2) * 8 + (idx & 3); isx = false; }
+      else if (s < 6) { piece = (idx >> 2) * 8 + 4 + (idx & 3); isx = false; }
+      else { piece = idx < 8 ? idx + 8 : idx + 16; isx = true; }
+      const int r = piece * 8 + rr;
+      const int c = swz(r, pc);
+      if (isx) {
+        int g = m0 + r;
+        g = g < M ? g : M - 1;
+        src[s] = X + xmap(g) * ldx + c * 8;
+        loff[s] = piece * 1024;
+      } else {
+        int g = n0 + r;
+        g = g < N ? g : N - 1;
+        src[s] = W + (int64_t)g * ldw + c * 8;
+        loff[s] = TILE_BYTES + piece * 1024;
+      }
+    }
+  }
+  auto dma = [&](int s, int kt) {
+    __builtin_amdgcn_global_load_lds((const AS1 void*)(src[s] + (int64_t)kt * BK),
+                                     (AS3 void*)(smem + (kt & 1) * BUF8 + loff[s]), 16, 0, 0);
+  };
+  auto S1 = [&](int kt) { dma(0, kt); dma(1, kt); dma(2, kt); dma(3, kt); };
+  auto S2 = [&](int kt) { dma(4, kt); dma(5, kt); };
+  auto S3 = [&](int kt) { dma(6, kt); dma(7, kt); };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 xf[8], w0[4], w1[4];
+  auto read_x = [&](const char* xt, int jm) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) xf[j * 2 + ks] = lds_frag(xt, wm * 128 + jm * 64 + j * 16 + fr, ks * 4 + fq);
+  };
+  auto read_w = [&](const char* wt, int in, bf16x8(&wf)[4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) wf[i * 2 + ks] = lds_frag(wt, wn * 64 + in * 32 + i * 16 + fr, ks * 4 + fq);
+  };
+  auto quad = [&](int jm, int in, const bf16x8(&wf)[4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          acc[in * 2 + i][jm * 4 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i * 2 + ks], xf[j * 2 + ks], acc[in * 2 + i][jm * 4 + j], 0, 0, 0);
+  };
+  auto mfma_section = [&](auto&& body) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    body();
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: S1(0) S2(0) S3(0) [S1(1) S2(1)]; retire S1(0)
+  S1(0); S2(0); S3(0);
+  if (nk > 1) { S1(1); S2(1); SDP_VMCNT(10); }
+  else SDP_VMCNT(4);
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one barrier
+  __builtin_amdgcn_sched_barrier(0);
+
+  for (int t = 0; t < nk; ++t) {
+    const char* xt = smem + (t & 1) * BUF8;
+    const char* wt = xt + TILE_BYTES;
+    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
+    // phase 0: Q(m0, n0)
+    read_w(wt, 0, w0);
+    read_x(xt, 0);
+    if (more1) { S3(t + 1); SDP_VMCNT(10); } else SDP_VMCNT(2);
+    mfma_section([&] { quad(0, 0, w0); });
+    // phase 1: Q(m0, n1)
+    read_w(wt, 1, w1);
+    if (more1) SDP_VMCNT(8); else SDP_VMCNT(0);
+    mfma_section([&] { quad(0, 1, w1); });
+    // phase 2: Q(m1, n1)
+    read_x(xt, 1);
+    if (more2) S1(t + 2);
+    mfma_section([&] { quad(1, 1, w1); });
+    // phase 3: Q(m1, n0)
+    if (more2) { S2(t + 2); SDP_VMCNT(10); }
+    else if (more1) SDP_VMCNT(4);
+    mfma_section([&] { quad(1, 0, w0); });
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
+}
+#undef SDP_VMCNT
+
 }  // namespace fast
 
 // Half-width tile for two blocks per CU: 256x128x32 tiles, 4 waves (2 along M x 2
 // along N, 128x64 each as above), 3-slot LDS ring per operand (3 x 24 KiB = 72 KiB)
 // -> two co-resident blocks per CU, so one block's prologue / epilogue overlaps
 // the other's MFMAs.  LDS rows are 64 B (32 bf16): 16-B chunk c of row r at
-// c ^ ((r >> 2) & 3), conflict-free for 16 consecutive rows.
+// c ^ H[(r >> 2) & 3], H = {0,2,3,1}.  ds_read_b128 serves the wave in the lane
+// groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59},
+// {36-43,48-51,60-63}; with this H every group's 16 (row, chunk) reads land on
+// 16 distinct 16-B bank slots (a plain c ^ ((r>>2)&3) collides 2-way in group 0).
 namespace half {
 constexpr int BM = 256, BN = 128, BK = 32;
 constexpr int XT = BM * BK * 2, WT = BN * BK * 2, STAGE = XT + WT;  // 16 + 8 KiB
 constexpr int NT = 256;
-SDP_DEV int swz(int r, int c) { return c ^ ((r >> 2) & 3); }
+SDP_DEV int swz(int r, int c) { return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3); }  // H = {0,2,3,1}
 
 // rows [row0, row0+nrows_tile) x 32 k, per wave `pieces` glds of 16 rows x 64 B
 template <int PIECES>
@@ -482,6 +647,98 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_256x128(const bf16_t* __restr
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[i], bx[j], acc[i][j], 0, 0, 0);
+    if (more2) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+  fast::tile_epilogue16<ACT, BN>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
+}
+
+// Same tile / ring as gemm_bf16_256x128, but the six global_load_lds of the
+// prefetched stage are spread between the MFMA groups of the current K-step
+// (one piece before each group of 8 MFMAs) instead of a burst at the top of the
+// step, so a wave's LDS-DMA issue cost overlaps its own / its partner's MFMAs.
+template <int ACT>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_256x128i(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
+                                                            const bf16_t* __restrict__ W, int64_t ldw,
+                                                            Epi<bf16_t> epi, int M, int N, int K, int tiles_m,
+                                                            int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
+  const int nwg = tiles_m * tiles_n;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  const RowMap wmap{0x7fffffff, 0, 0};
+  const int nk = K / BK;
+
+  // per-lane source rows of this wave's 6 pieces (4 of X, 2 of W), fixed over K
+  const int rr = lane >> 2, pc = lane & 3;
+  const bf16_t* src[6];
+  int ldsoff[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const bool isx = i < 4;
+    const int piece = isx ? wave * 4 + i : wave * 2 + (i - 4);
+    const int r = piece * 16 + rr;
+    const int c = swz(r, pc);
+    if (isx) {
+      int grow = m0 + r;
+      grow = grow < M ? grow : M - 1;
+      src[i] = X + xmap(grow) * ldx + c * 8;
+      ldsoff[i] = piece * 1024;
+    } else {
+      int grow = n0 + r;
+      grow = grow < N ? grow : N - 1;
+      src[i] = W + (int64_t)grow * ldw + c * 8;
+      ldsoff[i] = XT + piece * 1024;
+    }
+  }
+  auto piece = [&](int i, int kt, char* st) {
+    __builtin_amdgcn_global_load_lds((const AS1 void*)(src[i] + (int64_t)kt * BK), (AS3 void*)(st + ldsoff[i]), 16,
+                                     0, 0);
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int i = 0; i < 6; ++i) piece(i, 0, smem);
+  if (nk > 1) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) piece(i, 1, smem + STAGE);
+    asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more2 = kt + 2 < nk;
+    char* nst = smem + (cur >= 1 ? cur - 1 : 2) * STAGE;
+    const char* xt = smem + cur * STAGE;
+    const char* wt = xt + XT;
+    bf16x8 bx[8], aw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aw[i] = frag(wt, wn * 64 + i * 16 + fr, fq);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bx[j] = frag(xt, wm * 128 + j * 16 + fr, fq);
+    if (more2) { piece(0, kt + 2, nst); piece(1, kt + 2, nst); }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (more2 && i < 2) piece(2 + 2 * i, kt + 2, nst), piece(3 + 2 * i, kt + 2, nst);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[i], bx[j], acc[i][j], 0, 0, 0);
+    }
     if (more2) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -596,12 +853,13 @@ extern "C" int sdp_gemm_force_generic(int on) {
 
 // bf16 fast-kernel selection: 1 = 2-stage ring + 8-B stores, 3 = 2-stage ring + paired
 // 16-B stores, 5 = deep-X ring (3 X slots, 2 W slots, counted vmcnt) + 16-B stores,
-// 7 = 256x128 tiles, 3-slot ring, two blocks per CU (default), 4 = no-store timing
-// probe (wrong results; benchmarks only).
-static int g_fast_kernel = 7;
+// 7 = 256x128 tiles, 3-slot ring, two blocks per CU, 8 = same with interleaved DMA,
+// 9 = 8-phase ping-pong 256x256 (default), 4 = no-store timing probe (wrong results;
+// benchmarks only).
+static int g_fast_kernel = 9;
 extern "C" int sdp_gemm_set_fast_kernel(int k) {
   int old = g_fast_kernel;
-  if (k == 1 || k == 3 || k == 4 || k == 5 || k == 7) g_fast_kernel = k;
+  if (k == 1 || k == 3 || k == 4 || k == 5 || k == 7 || k == 8 || k == 9) g_fast_kernel = k;
   return old;
 }
 
@@ -635,12 +893,27 @@ extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_
       const int tm = (M + fast::BM - 1) / fast::BM, tn = (N + fast::BN - 1) / fast::BN;
 #define SDP_FAST(A, E) hipLaunchKernelGGL((fast::gemm_bf16_256x256<A, E>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
                                        (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
-      if (g_fast_kernel == 7) {
+      if (g_fast_kernel == 7 || g_fast_kernel == 8) {
         const int hm = (M + half::BM - 1) / half::BM, hn = (N + half::BN - 1) / half::BN;
-#define SDP_HALF(A) hipLaunchKernelGGL((half::gemm_bf16_256x128<A>), dim3(hm * hn), dim3(half::NT), 0, s, \
-                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, hm, hn)
-        if (act == ACT_NONE) SDP_HALF(ACT_NONE); else if (act == ACT_GELU) SDP_HALF(ACT_GELU); else SDP_HALF(-1);
+#define SDP_HALF(KN, A) hipLaunchKernelGGL((half::KN<A>), dim3(hm * hn), dim3(half::NT), 0, s, \
+                                           (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, hm, hn)
+        if (g_fast_kernel == 7) {
+          if (act == ACT_NONE) SDP_HALF(gemm_bf16_256x128, ACT_NONE);
+          else if (act == ACT_GELU) SDP_HALF(gemm_bf16_256x128, ACT_GELU);
+          else SDP_HALF(gemm_bf16_256x128, -1);
+        } else {
+          if (act == ACT_NONE) SDP_HALF(gemm_bf16_256x128i, ACT_NONE);
+          else if (act == ACT_GELU) SDP_HALF(gemm_bf16_256x128i, ACT_GELU);
+          else SDP_HALF(gemm_bf16_256x128i, -1);
+        }
 #undef SDP_HALF
+        return SDP_CHECK_LAUNCH();
+      }
+      if (g_fast_kernel == 9) {
+#define SDP_8PH(A) hipLaunchKernelGGL((fast::gemm_bf16_8ph<A>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
+                                      (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
+        if (act == ACT_NONE) SDP_8PH(ACT_NONE); else if (act == ACT_GELU) SDP_8PH(ACT_GELU); else SDP_8PH(-1);
+#undef SDP_8PH
         return SDP_CHECK_LAUNCH();
       }
       if (g_fast_kernel == 5) {

@@ -80,6 +80,9 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
+        kern = os.environ.get("SDPNET_GEMM_KERNEL")  # A/B switch for the bf16 fast GEMM (benchmarks)
+        if kern:
+            L.sdp_gemm_set_fast_kernel(int(kern))
         _lib = L
     return _lib
 

@@ -34,7 +34,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--streams", default="1")
     ap.add_argument("--shapes", default=",".join(SHAPES))
-    ap.add_argument("--kernels", default="3", help="bf16 fast kernel ids to A/B (1 tile/block, 2 persistent)")
+    ap.add_argument("--kernels", default="8", help="bf16 fast kernel ids to A/B")
+    ap.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) as a yardstick")
     args = ap.parse_args()
     dev = torch.device("cuda")
     bf = torch.bfloat16
@@ -81,6 +82,21 @@ def main():
             total_us[(name, kern, ns)] = us
             print(f"{name:11s} M={M:6d} N={N:5d} K={K:5d} kern={kern} streams={ns} variant={sp.gemm_variant(bf, M, N, K)} "
                   f"{us:9.1f} us  {tf:7.1f} TF/s  ({100 * tf / 2516.6:4.1f}% of bf16 peak)", flush=True)
+        if args.torch:  # vendor-library yardstick (plain GEMM, no epilogue) -- not used by the product
+            import torch.nn.functional as F
+            f = lambda: F.linear(x, w)  # noqa: E731
+            for _ in range(3):
+                f()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                f()
+            e1.record()
+            torch.cuda.synchronize()
+            us = 1e3 * e0.elapsed_time(e1) / args.reps
+            print(f"{name:11s} torch.F.linear (hipBLASLt, no epilogue) {us:9.1f} us  "
+                  f"{2.0 * M * N * K / (us * 1e-6) / 1e12:7.1f} TF/s", flush=True)
     # per-forward estimate for M (launch counts per forward)
     counts = dict(mixer_cc=24, mixer_up=24, mixer_down=24, enc_qkv=13, enc_o=13, enc_ff1=13, enc_ff2=13)
     for kern, ns in [(kk, int(s)) for kk in args.kernels.split(",") for s in args.streams.split(",")]:
