@@ -56,6 +56,23 @@ def flops_per_image(cfg, img=224, num_registers=3):
     return patch + cfg["num_blocks"] * (cfg["conv_block_num"] * mixer + enc) + enc + head
 
 
+def measured_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/r*_gemm_traffic.json, written by tools/prof_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command,
+    gfx950 correction bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024).  PMC counters
+    cannot be read live without the profiler, hence the file."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_gemm_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel") == kernel:
+            return int(d["hbm_bytes_per_launch"]), os.path.relpath(f, REPO)
+    return None, None
+
+
 def cpu_baseline(model_cpu_sd, cfg, seconds=12.0):
     import torch
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -153,8 +170,8 @@ def main():
     # ---- dominant-kernel roofline: HIP events around every GEMM launch -------------
     rec = {}
 
-    def timer(name, key, flops, e0, e1):
-        rec.setdefault(key, []).append((flops, e0, e1))
+    def timer(name, key, flops, nbytes, e0, e1):
+        rec.setdefault(key, []).append((flops, nbytes, e0, e1))
 
     old = sp.set_launch_timer(timer)
     ns_saved = getattr(m, "num_streams", None)
@@ -169,20 +186,24 @@ def main():
         else:
             m.num_streams = ns_saved
     torch.cuda.synchronize()
-    fast_fl = fast_ms = 0.0
+    fast_fl = fast_ms = fast_by = 0.0
     fast_n = 0
     per_shape = {}
     for key, lst in rec.items():
-        ms = sum(e0.elapsed_time(e1) for _, e0, e1 in lst)
-        fl = sum(f for f, _, _ in lst)
+        ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in lst)
+        fl = sum(f for f, _, _, _ in lst)
+        by = sum(b for _, b, _, _ in lst)
         per_shape[f"{key[0]}x{key[1]}x{key[2]}"] = dict(launches=len(lst), avg_us=round(1e3 * ms / len(lst), 2),
                                                         tflops=round(fl / (ms * 1e-3) / 1e12, 1),
-                                                        kernel="gemm_bf16_fast" if key[3] == 1 else "gemm_generic")
+                                                        kernel="fast" if key[3] == 1 else "gemm_generic")
         if key[3] == 1:
             fast_fl += fl
             fast_ms += ms
+            fast_by += by
             fast_n += len(lst)
     achieved = fast_fl / (fast_ms * 1e-3) / 1e12 if fast_ms else 0.0
+    kname = FAST_GEMM_NAMES.get(sp.lib().sdp_gemm_set_fast_kernel(0), "?")
+    traffic, traffic_src = measured_traffic(kname)
 
     gf = flops_per_image(M_CFG) / 1e9
     total_imgs = B * args.steps * world
@@ -207,9 +228,11 @@ def main():
                    "parallelism": f"dp{world} independent batch shards (no collective)"},
         "model_flops_per_image_gf": round(gf, 3),
         "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
-        "roofline": {"bound": "mfma", "kernel": FAST_GEMM_NAMES.get(sp.lib().sdp_gemm_set_fast_kernel(0), "?"),
+        "roofline": {"bound": "mfma", "kernel": kname,
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "traffic_unit": "bytes per launch (HBM-side, PMC)", "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": int(fast_by / max(1, fast_n)),
                      "launches_per_step": fast_n // max(1, args.prof_steps),
                      "avg_launch_us": round(1e3 * fast_ms / max(1, fast_n), 2),
                      "algorithmic_gflop_per_launch": round(fast_fl / max(1, fast_n) / 1e9, 3),

@@ -426,7 +426,9 @@ constexpr int BUF8 = 2 * TILE_BYTES;
 
 #define SDP_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
-template <int ACT>
+// EPI: 1 = production epilogue, 2 = timing probe (stores only if a sentinel value
+// appears, i.e. never: measures main loop + prologue alone).
+template <int ACT, int EPI = 1>
 __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
                                                          const bf16_t* __restrict__ W, int64_t ldw, Epi<bf16_t> epi,
                                                          int M, int N, int K, int tiles_m, int tiles_n) {
@@ -553,6 +555,15 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     mfma_section([&] { quad(1, 0, w0); });
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  if constexpr (EPI == 2) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v += acc[i][j][0] + acc[i][j][3];
+    if (v == 1234.5f) epi.out[tid] = f2bf(v);
+    return;
+  }
   tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
 }
 #undef SDP_VMCNT
@@ -854,12 +865,12 @@ extern "C" int sdp_gemm_force_generic(int on) {
 // bf16 fast-kernel selection: 1 = 2-stage ring + 8-B stores, 3 = 2-stage ring + paired
 // 16-B stores, 5 = deep-X ring (3 X slots, 2 W slots, counted vmcnt) + 16-B stores,
 // 7 = 256x128 tiles, 3-slot ring, two blocks per CU, 8 = same with interleaved DMA,
-// 9 = 8-phase ping-pong 256x256 (default), 4 = no-store timing probe (wrong results;
-// benchmarks only).
+// 9 = 8-phase ping-pong 256x256 (default), 4 / 10 = no-store timing probes of 3 / 9
+// (wrong results; benchmarks only).
 static int g_fast_kernel = 9;
 extern "C" int sdp_gemm_set_fast_kernel(int k) {
   int old = g_fast_kernel;
-  if (k == 1 || k == 3 || k == 4 || k == 5 || k == 7 || k == 8 || k == 9) g_fast_kernel = k;
+  if (k == 1 || k == 3 || k == 4 || k == 5 || k == 7 || k == 8 || k == 9 || k == 10) g_fast_kernel = k;
   return old;
 }
 
@@ -907,6 +918,11 @@ extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_
           else SDP_HALF(gemm_bf16_256x128i, -1);
         }
 #undef SDP_HALF
+        return SDP_CHECK_LAUNCH();
+      }
+      if (g_fast_kernel == 10) {
+        hipLaunchKernelGGL((fast::gemm_bf16_8ph<ACT_NONE, 2>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,
+                           (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn);
         return SDP_CHECK_LAUNCH();
       }
       if (g_fast_kernel == 9) {

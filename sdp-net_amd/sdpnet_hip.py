@@ -62,6 +62,9 @@ _TIMER = None
 
 
 def set_launch_timer(fn):
+    """Install fn(name, key, flops, algorithmic_bytes, ev_start, ev_end), called after
+    every GEMM launch with HIP events recorded around it on the launch stream
+    (bench.py's roofline).  Returns the previous timer."""
     global _TIMER
     old = _TIMER
     _TIMER = fn
@@ -162,7 +165,9 @@ def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Option
     _check(rc, "gemm")
     if timer is not None:
         e1.record()
-        timer("gemm", (M, N, K, lib().sdp_gemm_variant(dt, M, N, K)), 2.0 * M * N * K, e0, e1)
+        es = x.t.element_size()
+        nbytes = es * (M * K + N * K + M * N * (2 if resid is not None else 1)) + (4 * N if bias is not None else 0)
+        timer("gemm", (M, N, K, lib().sdp_gemm_variant(dt, M, N, K)), 2.0 * M * N * K, nbytes, e0, e1)
 
 
 def layernorm(x: Rows, gamma: torch.Tensor, beta: torch.Tensor, eps: float, y: Rows, M: int, C: int):

@@ -26,6 +26,9 @@ SHAPES = {
     "enc_ff1": (51200, 3072, 768, True, 1, False),
     "enc_ff2": (51200, 768, 3072, True, 0, True),
     "sq8192": (8192, 8192, 8192, False, 0, False),
+    "mixer_up_noact": (50176, 3072, 768, False, 0, False),
+    "mixer_cc_noact": (50176, 768, 768, False, 0, True),
+    "mixer_cc_nores": (50176, 768, 768, False, 1, False),
 }
 
 

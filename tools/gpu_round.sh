@@ -19,7 +19,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) step benchq 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
-    gemm) step gemm 600 python tools/gemm_bench.py --streams 1 --kernels 8,9 ;;
+    gemm) step gemm 600 python tools/gemm_bench.py --streams 1 --kernels 9,10 ;;
     streams) step s1 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 1 &&
              step s2 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 2 &&
              step s3 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 3 &&
@@ -38,7 +38,10 @@ for s in "$@"; do
          step gpmcB 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_LDS_UNALIGNED_STALL GRBM_GUI_ACTIVE SQ_INSTS_VMEM -d gpurun_out/gpmcB -o run --output-format csv -- $GB &&
          step gpmcC 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/gpmcC -o run --output-format csv -- $GB &&
          step gpmcD 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/gpmcD -o run --output-format csv -- $GB ;;
-    prof) export TMPDIR=/tmp; rm -rf gpurun_out/prof
-          step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-graph --prof-steps 1 ;;
+    prof) export TMPDIR=/tmp; rm -rf gpurun_out/prof gpurun_out/pmcF gpurun_out/pmcW
+          BP="python bench.py --steps 3 --warmup 1 --no-graph --streams 1 --no-cpu-baseline --prof-steps 1"
+          step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- $BP &&
+          step pmcF 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcF -o run --output-format csv -- $BP &&
+          step pmcW 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcW -o run --output-format csv -- $BP ;;
   esac
 done
