@@ -120,6 +120,7 @@ def main():
 
     import model as sdp
     import sdpnet_hip as sp
+    import sharding
 
     torch.manual_seed(231424314)  # model_train.py:61
     m = sdp.MainModel.from_dict(**M_CFG).eval()
@@ -127,7 +128,10 @@ def main():
         m.num_streams = args.streams
     cpu_sd = {k: v.detach().clone() for k, v in m.state_dict().items()} if rank == 0 else None
     m = m.to(dev)
-    B = args.batch
+    # weak scaling: the global batch is world x per-GPU batch, each rank owns one
+    # contiguous shard (images are independent, no collective on the data path)
+    lo, hi = sharding.shard_bounds(args.batch * world, world, rank)
+    B = hi - lo
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     x = torch.randn(B, 3, 224, 224, generator=g).to(dev).to(torch.bfloat16)   # resident in HBM
 
@@ -160,11 +164,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = sharding.max_over_ranks(time.perf_counter() - t0, device=dev)
+    total_imgs = int(sharding.sum_over_ranks(B * args.steps, device=dev))
     assert torch.isfinite(y.float()).all()
 
     # ---- dominant-kernel roofline: HIP events around every GEMM launch -------------
@@ -206,7 +207,6 @@ def main():
     traffic, traffic_src = measured_traffic(kname)
 
     gf = flops_per_image(M_CFG) / 1e9
-    total_imgs = B * args.steps * world
     value = total_imgs / el
     out = {
         "metric": METRIC,
@@ -224,7 +224,7 @@ def main():
         "config": {"workload": "SdP-Net-M eval forward (12 blocks, d=768, patch 16, 200 tokens), "
                                "bf16 storage / fp32 accumulate, HIP-graph replay",
                    "streams_per_gpu": m._num_streams(B),
-                   "global_batch": B * world, "per_gpu_batch": B, "image": 224, "tokens": 200,
+                   "global_batch": args.batch * world, "per_gpu_batch": B, "image": 224, "tokens": 200,
                    "parallelism": f"dp{world} independent batch shards (no collective)"},
         "model_flops_per_image_gf": round(gf, 3),
         "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
