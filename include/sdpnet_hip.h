@@ -54,7 +54,9 @@ int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride
 int sdp_gemm_variant(int dtype, int M, int N, int K);
 /* Test hook: force the generic kernel (returns the previous setting). */
 int sdp_gemm_force_generic(int on);
-/* Select the bf16 fast kernel: 9 = 8-phase ping-pong 256x256x64 (default);
+/* Select the bf16 fast kernel: 12 = 8-phase ping-pong 256x256x64 with the
+ * whole-line (LDS-staged) epilogue (default); 9 = same with the direct epilogue;
+ * 11 / 13 = persistent forms of 9 / 12;
  * 1 = 256x256 tiles, 2-stage LDS ring, 8-byte stores; 3 = same with
  * permlane-paired 16-byte stores; 5 = 256x256, deep X ring (3 slots); 7 = 256x128
  * tiles, 3-slot ring, two blocks per CU; 8 = 7 with interleaved DMA; 4 / 10 =

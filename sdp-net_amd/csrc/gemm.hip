@@ -13,8 +13,8 @@
 // covers  act(conv)+x  (ConvMixer), x + FFN (+bias) (Encoder), pos-emb add +
 // embedding activation (EmbeddingLayer), Tanh (head).
 //
-// Kernels (bf16 fast path selected by sdp_gemm_set_fast_kernel, default 9):
-//  * gemm_bf16_8ph (9) — the hot kernel: 256x256x64 tiles, 8 waves (2 along M x
+// Kernels (bf16 fast path selected by sdp_gemm_set_fast_kernel, default 12):
+//  * gemm_bf16_8ph (9; 12 with tile_epilogue_rows) — the hot kernel: 256x256x64 tiles, 8 waves (2 along M x
 //    4 along N, 128x64 per wave), v_mfma_f32_16x16x32_bf16, both operands staged
 //    HBM->LDS by global_load_lds_dwordx4 into an XOR-swizzled [row][64] image
 //    (conflict-free ds_read_b128), 4 phases per K-tile with the two wave groups
@@ -205,10 +205,12 @@ SDP_DEV void tile_epilogue(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, i
 // stores become one 16-B access per lane per pair (half the store instructions).
 SDP_DEV int pair_col0(int fq) { return 8 * (((fq & 1) << 1) | (fq >> 1)); }
 
-template <int ACT, int TBN = BN>
+template <int ACT, int TBN = BN, int JB = 8, bool FULL = false>
 SDP_DEV void tile_epilogue16(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int M, int N, int wm,
                              int wn, int fr, int fq) {
-  if (n0 + TBN > N) {  // ragged N: generic per-4 path
+  // FULL: the caller guarantees m0 + 256 <= M and n0 + TBN <= N (no row checks, so
+  // every residual load is consumed on every path)
+  if (!FULL && n0 + TBN > N) {  // ragged N: generic per-4 path
     tile_epilogue<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
     return;
   }
@@ -223,37 +225,121 @@ SDP_DEV void tile_epilogue16(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0,
       bv[p][0] = bv[p][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
+  // Residual loads are issued JB row groups at a time (one 16-B load per lane per
+  // (row group, pair)) ahead of their use, so a tile waits on memory 8 / JB times
+  // instead of once per row group.
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int m = m0 + wm * 128 + j * 16 + fr;
-    if (m >= M) continue;
-    bf16x8 rr[2];
+  for (int j0 = 0; j0 < 8; j0 += JB) {
+    bf16x8 rres[JB][2];
     if (epi.resid) {
-      const bf16_t* rp = epi.resid + epi.rmap(m) * epi.ldr + cbase;
 #pragma unroll
-      for (int p = 0; p < 2; ++p) rr[p] = *(const bf16x8*)(rp + 32 * p);
+      for (int jj = 0; jj < JB; ++jj) {
+        int m = m0 + wm * 128 + (j0 + jj) * 16 + fr;
+        if (!FULL) m = m < M ? m : M - 1;
+        const bf16_t* rp = epi.resid + epi.rmap(m) * epi.ldr + cbase;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) rres[jj][p] = *(const bf16x8*)(rp + 32 * p);
+      }
     }
-    bf16_t* op = epi.out + epi.cmap(m) * epi.ldc + cbase;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      float v[8];
+    for (int jj = 0; jj < JB; ++jj) {
+      const int j = j0 + jj;
+      const int m = m0 + wm * 128 + j * 16 + fr;
+      if (!FULL && m >= M) continue;
+      const bf16x8* rr = rres[jj];
+      bf16_t* op = epi.out + epi.cmap(m) * epi.ldc + cbase;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
-                                                   __float_as_uint(acc[2 * p + 1][j][r]), false, false);
-        v[r] = __uint_as_float(sw[0]);
-        v[4 + r] = __uint_as_float(sw[1]);
+      for (int p = 0; p < 2; ++p) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                     __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+          v[r] = __uint_as_float(sw[0]);
+          v[4 + r] = __uint_as_float(sw[1]);
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = v[e] + bv[p][e >> 2][e & 3];
+          if (epi.resid && epi.resid_pre) x += bf2f((bf16_t)rr[p][e]);
+          x = epi_act<ACT>(epi.act, x);
+          if (epi.resid && !epi.resid_pre) x += bf2f((bf16_t)rr[p][e]);
+          o[e] = (short)f2bf(x);
+        }
+        *(bf16x8*)(op + 32 * p) = o;
       }
-      bf16x8 o;
+    }
+  }
+}
+
+// Full-tile epilogue with whole-line memory accesses.  A wave's 16-row x 64-col
+// slice (row group j) is packed to bf16 in the MFMA layout (row fr, 8 columns per
+// lane after the permlane16 pairing), written to the wave's private 2 KiB LDS slot
+// (XOR-swizzled 16-B chunks), and read back so that lane l owns row (l>>3) + 8q,
+// chunk l&7: each 16-B store (and residual load) instruction then covers 8 full
+// 128-B rows instead of 16 half rows.  The residual is added after the staging
+// (v = bf16(act(acc + b)) + R, rounded again), i.e. resid_pre = 0 semantics; the
+// caller routes resid_pre with an activation elsewhere.  Same-wave LDS accesses
+// execute in order, so the slot needs no barrier.
+template <int ACT, int JB = 4>
+SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int wm, int wn,
+                                int lane, int fr, int fq, char* stg) {
+  const int cbase = n0 + wn * 64 + pair_col0(fq);
+  f32x4 bv[2][2];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float x = v[e] + bv[p][e >> 2][e & 3];
-        if (epi.resid && epi.resid_pre) x += bf2f((bf16_t)rr[p][e]);
-        x = epi_act<ACT>(epi.act, x);
-        if (epi.resid && !epi.resid_pre) x += bf2f((bf16_t)rr[p][e]);
-        o[e] = (short)f2bf(x);
+  for (int p = 0; p < 2; ++p) {
+    if (epi.bias) {
+      bv[p][0] = *(const f32x4*)(epi.bias + cbase + 32 * p);
+      bv[p][1] = *(const f32x4*)(epi.bias + cbase + 32 * p + 4);
+    } else {
+      bv[p][0] = bv[p][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  const int rlo = lane >> 3, ch = lane & 7;
+  const int col = n0 + wn * 64 + ch * 8;
+  const int wchunk0 = ((fq & 1) << 1) | (fq >> 1);  // 16-B chunk of pair 0 (pair 1: +4)
+#pragma unroll
+  for (int j0 = 0; j0 < 8; j0 += JB) {
+    bf16x8 rres[JB][2];
+    if (epi.resid) {
+#pragma unroll
+      for (int jj = 0; jj < JB; ++jj)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int m = m0 + wm * 128 + (j0 + jj) * 16 + rlo + 8 * q;
+          rres[jj][q] = *(const bf16x8*)(epi.resid + epi.rmap(m) * epi.ldr + col);
+        }
+    }
+#pragma unroll
+    for (int jj = 0; jj < JB; ++jj) {
+      const int j = j0 + jj;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                     __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+          v[r] = __uint_as_float(sw[0]);
+          v[4 + r] = __uint_as_float(sw[1]);
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(epi_act<ACT>(epi.act, v[e] + bv[p][e >> 2][e & 3]));
+        *(bf16x8*)(stg + fr * 128 + (((4 * p + wchunk0) ^ (fr & 7)) << 4)) = o;
       }
-      *(bf16x8*)(op + 32 * p) = o;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int r = rlo + 8 * q;
+        bf16x8 o = *(const bf16x8*)(stg + r * 128 + ((ch ^ (r & 7)) << 4));
+        if (epi.resid) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(bf2f((bf16_t)o[e]) + bf2f((bf16_t)rres[jj][q][e]));
+        }
+        const int m = m0 + wm * 128 + j * 16 + r;
+        *(bf16x8*)(epi.out + epi.cmap(m) * epi.ldc + col) = o;
+      }
     }
   }
 }
@@ -555,6 +641,12 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     mfma_section([&] { quad(1, 0, w0); });
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  if constexpr (EPI == 3) {  // whole-line epilogue through the (drained) LDS buffers
+    if (n0 + BN <= N && m0 + BM <= M && !(epi.resid && epi.resid_pre && epi.act != ACT_NONE)) {
+      tile_epilogue_rows<ACT>(epi, acc, m0, n0, wm, wn, lane, fr, fq, smem + wave * 2048);
+      return;
+    }
+  }
   if constexpr (EPI == 2) {
     float v = 0.f;
 #pragma unroll
@@ -565,6 +657,209 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     return;
   }
   tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
+}
+// ---------------------------------------------------------------------------
+// Persistent form of gemm_bf16_8ph: one block per CU walks a tile sequence and
+// the K-tile stream (and its 3-sub-stage DMA schedule) runs on across tile
+// boundaries, so the next tile's first K-tiles are already in flight when a
+// tile's epilogue starts, and the epilogue's stores drain underneath the next
+// tile's MFMAs instead of ending the block.
+//
+// Tile sequence: block b takes virtual ids b, b+G, b+2G, ... (G = grid, a
+// multiple of 8), each mapped through the same XCD-aware remap as the one-shot
+// kernel; b+iG and b share b's XCD, so an XCD's resident blocks stay on
+// neighbouring tiles.  A sub-stage's source pointers are recomputed when its own
+// stream reaches K-tile 0 of a new tile.
+//
+// vmcnt: the epilogue issues E store instructions (16 on full tiles, counted as 0
+// on ragged ones) after S2(g+2) and before S3(g+1)-of-the-next-step; the four
+// waits that retire a DMA issued before those stores (t = 0: phases 0, 1, 3;
+// t = 1: phase 0) add E so the stores are not drained.  Counting fewer
+// instructions than were issued only waits longer, never shorter, so E may be a
+// lower bound (epilogue loads are older than its stores and consumed by them).
+// ---------------------------------------------------------------------------
+SDP_DEV void tile_of(int v, int nwg, int tiles_n, int& m0, int& n0) {
+  const int xcd = v & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (v >> 3);
+  m0 = (wgid / tiles_n) * BM;
+  n0 = (wgid % tiles_n) * BN;
+}
+
+template <int ACT, bool ROWS = false>
+__global__ __launch_bounds__(NTHREADS) void gemm_bf16_8php(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
+                                                          const bf16_t* __restrict__ W, int64_t ldw, Epi<bf16_t> epi,
+                                                          int M, int N, int K, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF8 + (ROWS ? 8 * 2048 : 0)];
+  const int nwg = tiles_m * tiles_n;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int ntile = (nwg - b + G - 1) / G;  // tiles of this block
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = K / BK;
+  const int total = ntile * nk;
+  if (ntile <= 0) return;
+
+  // Piece s of this wave (8 rows x 128 B; [0,1] S1-X, [2,3] S1-W, [4,5] S2-W,
+  // [6,7] S3-X): tile row and LDS offset are compile-time functions of (s, wave);
+  // the source is kept as a 32-bit element offset from X or W (K-tile 0 of the
+  // piece's current tile), recomputed when the sub-stage enters a new tile.
+  auto piece_of = [&](int s) {
+    const int idx = wave * 2 + (s & 1);
+    if (s < 2) return idx < 8 ? idx : idx + 8;
+    if (s < 4) return (idx >> 2) * 8 + (idx & 3);
+    if (s < 6) return (idx >> 2) * 8 + 4 + (idx & 3);
+    return idx < 8 ? idx + 8 : idx + 16;
+  };
+  uint32_t soff[8];
+  auto set_src = [&](int s, int m0, int n0) {
+    const int r = piece_of(s) * 8 + (lane >> 3);
+    const int c = swz(r, lane & 7);
+    if (s < 2 || s >= 6) {
+      int g = m0 + r;
+      g = g < M ? g : M - 1;
+      soff[s] = (uint32_t)(xmap(g) * ldx + c * 8);
+    } else {
+      int g = n0 + r;
+      g = g < N ? g : N - 1;
+      soff[s] = (uint32_t)((int64_t)g * ldw + c * 8);
+    }
+  };
+  // issue sub-stage pieces [s0, s1) for K-tile t of the block's tile i (global
+  // K-tile index g = i * nk + t picks the LDS buffer)
+  auto stage = [&](int s0, int s1, int i, int t, int g) {
+    if (t == 0) {
+      int m0, n0;
+      tile_of(b + i * G, nwg, tiles_n, m0, n0);
+#pragma unroll
+      for (int s = s0; s < s1; ++s) set_src(s, m0, n0);
+    }
+#pragma unroll
+    for (int s = s0; s < s1; ++s) {
+      const bf16_t* base = (s < 2 || s >= 6) ? X : W;
+      const int lo = ((s < 2 || s >= 6) ? 0 : TILE_BYTES) + piece_of(s) * 1024;
+      __builtin_amdgcn_global_load_lds((const AS1 void*)(base + soff[s] + (uint32_t)(t * BK)),
+                                       (AS3 void*)(smem + (g & 1) * BUF8 + lo), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 xf[8], w0[4], w1[4];
+  auto read_x = [&](const char* xt, int jm) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) xf[j * 2 + ks] = lds_frag(xt, wm * 128 + jm * 64 + j * 16 + fr, ks * 4 + fq);
+  };
+  auto read_w = [&](const char* wt, int in, bf16x8(&wf)[4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) wf[i * 2 + ks] = lds_frag(wt, wn * 64 + in * 32 + i * 16 + fr, ks * 4 + fq);
+  };
+  auto quad = [&](int jm, int in, const bf16x8(&wf)[4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          acc[in * 2 + i][jm * 4 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i * 2 + ks], xf[j * 2 + ks], acc[in * 2 + i][jm * 4 + j], 0, 0, 0);
+  };
+  auto mfma_section = [&](auto&& body) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    body();
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // (i, t) of K-tiles g+1 and g+2, advanced incrementally (no division in the loop)
+  int i1 = nk > 1 ? 0 : 1, t1 = nk > 1 ? 1 : 0;
+  int i2 = i1, t2 = t1;
+  if (++t2 == nk) { t2 = 0; ++i2; }
+  stage(0, 4, 0, 0, 0); stage(4, 6, 0, 0, 0); stage(6, 8, 0, 0, 0);
+  if (total > 1) { stage(0, 4, i1, t1, 1); stage(4, 6, i1, t1, 1); SDP_VMCNT(10); }
+  else SDP_VMCNT(4);
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  // e0: stores of the previous epilogue are younger than the DMA retired by the
+  // waits of t = 0 (phases 0, 1, 3); e1: of t = 1 phase 0.
+  bool e0 = false, e1 = false;
+  int tile = 0, t = 0;
+  for (int g = 0; g < total; ++g) {
+    const char* xt = smem + (g & 1) * BUF8;
+    const char* wt = xt + TILE_BYTES;
+    const bool more1 = g + 1 < total, more2 = g + 2 < total;
+    const bool ee = e0 || e1;
+    // phase 0: Q(m0, n0); retire S2(g)
+    read_w(wt, 0, w0);
+    read_x(xt, 0);
+    if (more1) {
+      stage(6, 8, i1, t1, g + 1);
+      if (ee) SDP_VMCNT(26); else SDP_VMCNT(10);
+    } else {
+      SDP_VMCNT(2);
+    }
+    mfma_section([&] { quad(0, 0, w0); });
+    // phase 1: Q(m0, n1); retire S3(g)
+    read_w(wt, 1, w1);
+    if (more1) { if (e0) SDP_VMCNT(24); else SDP_VMCNT(8); }
+    else SDP_VMCNT(0);
+    mfma_section([&] { quad(0, 1, w1); });
+    // phase 2: Q(m1, n1)
+    read_x(xt, 1);
+    if (more2) stage(0, 4, i2, t2, g + 2);
+    mfma_section([&] { quad(1, 1, w1); });
+    // phase 3: Q(m1, n0); retire S1(g+1)
+    if (more2) { stage(4, 6, i2, t2, g + 2); if (e0) SDP_VMCNT(26); else SDP_VMCNT(10); }
+    else if (more1) SDP_VMCNT(4);
+    mfma_section([&] { quad(1, 0, w0); });
+    e1 = e0;
+    e0 = false;
+    i1 = i2; t1 = t2;
+    if (++t2 == nk) { t2 = 0; ++i2; }
+    if (++t == nk) {
+      int m0, n0;
+      tile_of(b + tile * G, nwg, tiles_n, m0, n0);
+      const bool full = n0 + BN <= N && m0 + BM <= M;
+      // Close each epilogue with a wait the compiler's waitcnt pass can see (the
+      // builtin, not inline asm), so no epilogue load stays "pending" into the
+      // next K-tile and forces a vmcnt(0) at the loop header: full tiles end with
+      // 16 stores younger than every epilogue load -> vmcnt(16); ragged: vmcnt(0).
+      if (full) {
+        if (ROWS && !(epi.resid && epi.resid_pre && epi.act != ACT_NONE))
+          tile_epilogue_rows<ACT, 2>(epi, acc, m0, n0, wm, wn, lane, fr, fq, smem + 2 * BUF8 + wave * 2048);
+        else
+          tile_epilogue16<ACT, BN, 4, true>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
+        __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16) expcnt(7) lgkmcnt(15)
+      } else {
+        tile_epilogue<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      }
+      e0 = nk >= 2 && full;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      t = 0;
+      ++tile;
+    }
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();
 }
 #undef SDP_VMCNT
 
@@ -841,6 +1136,14 @@ __global__ __launch_bounds__(256) void gemm_generic(const T* __restrict__ X, int
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
+// Largest physical row index a row map produces for logical rows [0, M).
+static int64_t max_phys_row(int M, const RowMap& m) {
+  if (M <= 0) return 0;
+  if (m.grp >= 0x7fffffff) return M - 1;
+  const int64_t last = M - 1;
+  return (last / m.grp) * m.gstride + m.off + (m.grp - 1);
+}
+
 static RowMap mk_map(int grp, int64_t gstride, int off) {
   RowMap r;
   r.grp = grp > 0 ? grp : 0x7fffffff;
@@ -865,12 +1168,14 @@ extern "C" int sdp_gemm_force_generic(int on) {
 // bf16 fast-kernel selection: 1 = 2-stage ring + 8-B stores, 3 = 2-stage ring + paired
 // 16-B stores, 5 = deep-X ring (3 X slots, 2 W slots, counted vmcnt) + 16-B stores,
 // 7 = 256x128 tiles, 3-slot ring, two blocks per CU, 8 = same with interleaved DMA,
-// 9 = 8-phase ping-pong 256x256 (default), 4 / 10 = no-store timing probes of 3 / 9
+// 9 = 8-phase ping-pong 256x256, 11 = persistent form of 9, 12 (default) / 13 = 9 / 11
+// with the whole-line LDS-staged epilogue,
+// 4 / 10 = no-store timing probes of 3 / 9
 // (wrong results; benchmarks only).
-static int g_fast_kernel = 9;
+static int g_fast_kernel = 12;
 extern "C" int sdp_gemm_set_fast_kernel(int k) {
   int old = g_fast_kernel;
-  if (k == 1 || k == 3 || k == 4 || k == 5 || k == 7 || k == 8 || k == 9 || k == 10) g_fast_kernel = k;
+  if (k == 1 || k == 3 || k == 4 || k == 5 || (k >= 7 && k <= 13)) g_fast_kernel = k;
   return old;
 }
 
@@ -925,7 +1230,30 @@ extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_
                            (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn);
         return SDP_CHECK_LAUNCH();
       }
-      if (g_fast_kernel == 9) {
+      // persistent form: epilogues GELU / none only (the runtime-activation variant
+      // spills), 32-bit element offsets must cover both operands
+      if ((g_fast_kernel == 11 || g_fast_kernel == 13) && (act == ACT_NONE || act == ACT_GELU) &&
+          max_phys_row(M, xm) * ldx + K <= 0xffffffffLL && (int64_t)N * ldw <= 0xffffffffLL) {
+        const int nwg = tm * tn, ncu = num_cus();
+        const int grid = nwg <= ncu ? nwg : (ncu & ~7);
+#define SDP_8PHP(A, R) hipLaunchKernelGGL((fast::gemm_bf16_8php<A, R>), dim3(grid), dim3(fast::NTHREADS), 0, s, \
+                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
+        if (g_fast_kernel == 13) {
+          if (act == ACT_NONE) SDP_8PHP(ACT_NONE, true); else SDP_8PHP(ACT_GELU, true);
+        } else {
+          if (act == ACT_NONE) SDP_8PHP(ACT_NONE, false); else SDP_8PHP(ACT_GELU, false);
+        }
+#undef SDP_8PHP
+        return SDP_CHECK_LAUNCH();
+      }
+      if (g_fast_kernel == 12) {
+#define SDP_8PH(A) hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, 3>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
+                                      (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
+        if (act == ACT_NONE) SDP_8PH(ACT_NONE); else if (act == ACT_GELU) SDP_8PH(ACT_GELU); else SDP_8PH(-1);
+#undef SDP_8PH
+        return SDP_CHECK_LAUNCH();
+      }
+      if (g_fast_kernel == 9 || g_fast_kernel == 11 || g_fast_kernel == 13) {
 #define SDP_8PH(A) hipLaunchKernelGGL((fast::gemm_bf16_8ph<A>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
         if (act == ACT_NONE) SDP_8PH(ACT_NONE); else if (act == ACT_GELU) SDP_8PH(ACT_GELU); else SDP_8PH(-1);

@@ -328,7 +328,7 @@ def test_nchw_add_table():
     assert torch.allclose(x, ref, atol=1e-6)
 
 
-@pytest.mark.parametrize("kern", [1, 3, 5, 7, 8, 9])
+@pytest.mark.parametrize("kern", [1, 3, 5, 7, 8, 9, 11, 12, 13])
 @pytest.mark.parametrize("M,N,K,act,res", [(1000, 768, 768, 1, True), (300, 384, 128, 0, False),
                                            (777, 3072, 768, 1, False), (520, 768, 3072, 0, True),
                                            (256, 256, 64, 3, True), (600, 2304, 192, 0, False),

@@ -19,13 +19,13 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) step benchq 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
-    gemm) step gemm 600 python tools/gemm_bench.py --streams 1 --kernels 9,10 ;;
+    gemm) step gemm 600 python tools/gemm_bench.py --streams 1 --kernels 9,11,12,13 ;;
     streams) step s1 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 1 &&
              step s2 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 2 &&
              step s3 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 3 &&
              step s4 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 4 ;;
-    ab) step ab8 600 env SDPNET_GEMM_KERNEL=8 python bench.py --steps 10 --warmup 3 --no-cpu-baseline &&
-        step ab9 600 env SDPNET_GEMM_KERNEL=9 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    ab) step ab8 600 env SDPNET_GEMM_KERNEL=9 python bench.py --steps 10 --warmup 3 --no-cpu-baseline &&
+        step ab9 600 env SDPNET_GEMM_KERNEL=12 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     kb) step kb 300 python tools/kern_bench.py ;;
     pmc) export TMPDIR=/tmp; rm -rf gpurun_out/pmc*
          step pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES -d gpurun_out/pmc1 -o run --output-format csv -- python tools/kern_bench.py --reps 3 &&
