@@ -48,6 +48,27 @@ SDP_DEV float gelu_fast(float x) {
   return x * (x >= 0.0f ? 1.0f - q : q);
 }
 
+// gelu_fast on a pair: the same Abramowitz-Stegun erf (|err| <= 1.5e-7) written on
+// float2 so the polynomial / scaling run as v_pk_fma_f32 / v_pk_mul_f32 (two
+// elements per issue); 0.5 is folded into the coefficients and
+// Phi(x) = 0.5 + copysign(0.5 - q, x) with q = 0.5 * (1 - erf(|x| / sqrt2)).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+SDP_DEV f32x2 gelu_fast2(f32x2 x) {
+  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
+  const f32x2 d = ax * 0.231641900f + 1.0f;             // 1 + 0.3275911 |x| / sqrt2
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = t * 0.5307027145f - 0.7265760135f;
+  p = p * t + 0.7107068705f;
+  p = p * t - 0.142248368f;
+  p = p * t + 0.127414796f;
+  p = p * t;
+  const f32x2 w = (x * x) * -0.72134752044448170f;      // -x^2/2 * log2(e)
+  const f32x2 e = {__builtin_amdgcn_exp2f(w.x), __builtin_amdgcn_exp2f(w.y)};
+  const f32x2 h = 0.5f - p * e;
+  const f32x2 phi = f32x2{copysignf(h.x, x.x), copysignf(h.y, x.y)} + 0.5f;
+  return x * phi;
+}
+
 SDP_DEV float apply_act(int act, float x) {
   switch (act) {
     case ACT_GELU: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));  // exact erf GELU

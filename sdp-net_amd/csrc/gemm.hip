@@ -283,21 +283,27 @@ SDP_DEV void tile_epilogue16(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0,
 // caller routes resid_pre with an activation elsewhere.  Same-wave LDS accesses
 // execute in order, so the slot needs no barrier.
 template <int ACT, int JB = 4>
-SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int wm, int wn,
-                                int lane, int fr, int fq, char* stg) {
+SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int M, int N, int wm,
+                                int wn, int lane, int fr, int fq, char* stg) {
+  // Ragged tiles take the same arithmetic with masked rows / 8-column chunks
+  // (host guarantees N % 8 == 0 and 16-B aligned rows), so a row's result never
+  // depends on where the tile boundaries fall (batch invariance).
   const int cbase = n0 + wn * 64 + pair_col0(fq);
   f32x4 bv[2][2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     if (epi.bias) {
-      bv[p][0] = *(const f32x4*)(epi.bias + cbase + 32 * p);
-      bv[p][1] = *(const f32x4*)(epi.bias + cbase + 32 * p + 4);
+      const int c0 = min(cbase + 32 * p, N - 8);
+      bv[p][0] = *(const f32x4*)(epi.bias + c0);
+      bv[p][1] = *(const f32x4*)(epi.bias + c0 + 4);
     } else {
       bv[p][0] = bv[p][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
   const int rlo = lane >> 3, ch = lane & 7;
   const int col = n0 + wn * 64 + ch * 8;
+  const bool col_ok = col < N;
+  const int lcol = col_ok ? col : N - 8;
   const int wchunk0 = ((fq & 1) << 1) | (fq >> 1);  // 16-B chunk of pair 0 (pair 1: +4)
 #pragma unroll
   for (int j0 = 0; j0 < 8; j0 += JB) {
@@ -307,8 +313,8 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
       for (int jj = 0; jj < JB; ++jj)
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const int m = m0 + wm * 128 + (j0 + jj) * 16 + rlo + 8 * q;
-          rres[jj][q] = *(const bf16x8*)(epi.resid + epi.rmap(m) * epi.ldr + col);
+          const int m = min(m0 + wm * 128 + (j0 + jj) * 16 + rlo + 8 * q, M - 1);
+          rres[jj][q] = *(const bf16x8*)(epi.resid + epi.rmap(m) * epi.ldr + lcol);
         }
     }
 #pragma unroll
@@ -326,7 +332,17 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
         }
         bf16x8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(epi_act<ACT>(epi.act, v[e] + bv[p][e >> 2][e & 3]));
+        for (int e = 0; e < 8; e += 2) {
+          f32x2 x2 = f32x2{v[e], v[e + 1]} + f32x2{bv[p][e >> 2][e & 3], bv[p][e >> 2][(e & 3) + 1]};
+          if constexpr (ACT == ACT_GELU) {
+            x2 = gelu_fast2(x2);
+          } else {
+            x2.x = epi_act<ACT>(epi.act, x2.x);
+            x2.y = epi_act<ACT>(epi.act, x2.y);
+          }
+          o[e] = (short)f2bf(x2.x);
+          o[e + 1] = (short)f2bf(x2.y);
+        }
         *(bf16x8*)(stg + fr * 128 + (((4 * p + wchunk0) ^ (fr & 7)) << 4)) = o;
       }
 #pragma unroll
@@ -338,7 +354,7 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
           for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(bf2f((bf16_t)o[e]) + bf2f((bf16_t)rres[jj][q][e]));
         }
         const int m = m0 + wm * 128 + j * 16 + r;
-        *(bf16x8*)(epi.out + epi.cmap(m) * epi.ldc + col) = o;
+        if (m < M && col_ok) *(bf16x8*)(epi.out + epi.cmap(m) * epi.ldc + col) = o;
       }
     }
   }
@@ -641,11 +657,10 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     mfma_section([&] { quad(1, 0, w0); });
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
-  if constexpr (EPI == 3) {  // whole-line epilogue through the (drained) LDS buffers
-    if (n0 + BN <= N && m0 + BM <= M && !(epi.resid && epi.resid_pre && epi.act != ACT_NONE)) {
-      tile_epilogue_rows<ACT>(epi, acc, m0, n0, wm, wn, lane, fr, fq, smem + wave * 2048);
-      return;
-    }
+  if constexpr (EPI == 3) {  // whole-line epilogue through the (drained) LDS buffers; the
+    // host routes resid_pre-with-activation and unaligned calls to EPI 1
+    tile_epilogue_rows<ACT>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + wave * 2048);
+    return;
   }
   if constexpr (EPI == 2) {
     float v = 0.f;
@@ -840,11 +855,12 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8php(const bf16_t* __restr
       // builtin, not inline asm), so no epilogue load stays "pending" into the
       // next K-tile and forces a vmcnt(0) at the loop header: full tiles end with
       // 16 stores younger than every epilogue load -> vmcnt(16); ragged: vmcnt(0).
-      if (full) {
-        if (ROWS && !(epi.resid && epi.resid_pre && epi.act != ACT_NONE))
-          tile_epilogue_rows<ACT, 2>(epi, acc, m0, n0, wm, wn, lane, fr, fq, smem + 2 * BUF8 + wave * 2048);
-        else
-          tile_epilogue16<ACT, BN, 4, true>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
+      if (ROWS) {
+        tile_epilogue_rows<ACT, 2>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + 2 * BUF8 + wave * 2048);
+        if (full) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+        else __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0)
+      } else if (full) {
+        tile_epilogue16<ACT, BN, 4, true>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
         __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16) expcnt(7) lgkmcnt(15)
       } else {
         tile_epilogue<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
@@ -1230,15 +1246,20 @@ extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_
                            (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn);
         return SDP_CHECK_LAUNCH();
       }
+      // the whole-line epilogue needs 16-B aligned output / residual rows and N % 8 == 0,
+      // and implements resid_pre only without an activation
+      const bool rows_ok = (N % 8 == 0) && (ldy % 8 == 0) && ((uintptr_t)Y % 16 == 0) &&
+                           (!R || ((ldr % 8 == 0) && ((uintptr_t)R % 16 == 0))) && !(R && resid_pre && act != ACT_NONE);
+      const int fk = (!rows_ok && g_fast_kernel == 12) ? 9 : (!rows_ok && g_fast_kernel == 13) ? 11 : g_fast_kernel;
       // persistent form: epilogues GELU / none only (the runtime-activation variant
       // spills), 32-bit element offsets must cover both operands
-      if ((g_fast_kernel == 11 || g_fast_kernel == 13) && (act == ACT_NONE || act == ACT_GELU) &&
+      if ((fk == 11 || fk == 13) && (act == ACT_NONE || act == ACT_GELU) &&
           max_phys_row(M, xm) * ldx + K <= 0xffffffffLL && (int64_t)N * ldw <= 0xffffffffLL) {
         const int nwg = tm * tn, ncu = num_cus();
         const int grid = nwg <= ncu ? nwg : (ncu & ~7);
 #define SDP_8PHP(A, R) hipLaunchKernelGGL((fast::gemm_bf16_8php<A, R>), dim3(grid), dim3(fast::NTHREADS), 0, s, \
                                        (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
-        if (g_fast_kernel == 13) {
+        if (fk == 13) {
           if (act == ACT_NONE) SDP_8PHP(ACT_NONE, true); else SDP_8PHP(ACT_GELU, true);
         } else {
           if (act == ACT_NONE) SDP_8PHP(ACT_NONE, false); else SDP_8PHP(ACT_GELU, false);
@@ -1246,14 +1267,14 @@ extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_
 #undef SDP_8PHP
         return SDP_CHECK_LAUNCH();
       }
-      if (g_fast_kernel == 12) {
+      if (fk == 12) {
 #define SDP_8PH(A) hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, 3>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
         if (act == ACT_NONE) SDP_8PH(ACT_NONE); else if (act == ACT_GELU) SDP_8PH(ACT_GELU); else SDP_8PH(-1);
 #undef SDP_8PH
         return SDP_CHECK_LAUNCH();
       }
-      if (g_fast_kernel == 9 || g_fast_kernel == 11 || g_fast_kernel == 13) {
+      if (fk == 9 || fk == 11 || fk == 13) {
 #define SDP_8PH(A) hipLaunchKernelGGL((fast::gemm_bf16_8ph<A>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
         if (act == ACT_NONE) SDP_8PH(ACT_NONE); else if (act == ACT_GELU) SDP_8PH(ACT_GELU); else SDP_8PH(-1);

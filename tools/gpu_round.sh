@@ -19,7 +19,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) step benchq 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
-    gemm) step gemm 600 python tools/gemm_bench.py --streams 1 --kernels 9,11,12,13 ;;
+    gemm) step gemm 600 python tools/gemm_bench.py --streams 1 --kernels 12,13 ;;
     streams) step s1 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 1 &&
              step s2 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 2 &&
              step s3 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 3 &&
