@@ -117,8 +117,14 @@ int sdp_attention(int dtype, const void* QKV, int64_t ld_qkv, void* O, int64_t l
                   int n_head, int head_dim, const float* q_gamma, const float* q_beta,
                   const float* k_gamma, const float* k_beta, float eps, const float* mask,
                   int64_t mask_sb, int64_t mask_sh, void* stream);
-/* 2 if sdp_attention takes the flash-style MFMA kernel for this shape, else 0. */
+/* Kernel sdp_attention takes for this shape: 4 = two persistent 4-wave flash
+ * workgroups per CU, one LDS-DMA K/V buffer each (hd % 32 == 0, N <= 256), 3 = two-workgroups-per-CU
+ * flash kernel (hd % 32 == 0), 2 = one-workgroup flash kernel, 0 = generic. */
 int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask);
+/* Select the bf16 flash kernel: 4 (default) = attn_fa4, 3 = attn_fa2, 2 = attn_fa
+ * (each where it applies, else the next lower one).
+ * Other values leave the selection unchanged.  Returns the previous selection. */
+int sdp_attention_set_kernel(int k);
 
 /*
  * im2col of the patch conv: image [B,3,Hi,Wi] -> rows [B*(Hi/p)*(Wi/p), Kpad],

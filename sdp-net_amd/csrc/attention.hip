@@ -298,6 +298,764 @@ __global__ __launch_bounds__(640) void attn_fa_bf16(const bf16_t* __restrict__ Q
   }
 }
 
+#ifndef ATTN_CH
+#define ATTN_CH 4  // key tiles per softmax chunk of attn_qtile_chunked
+#endif
+// ---------------------------------------------------------------------------
+// Per-wave pieces of the two-workgroup / persistent flash kernels (hd = 32*HDT).
+// Lane (r = lane & 31, hf = lane >> 5) owns query r of a 32-query tile and, in
+// every fragment, the 8 head dims 16s + 8hf .. +7 (k-step s).
+// ---------------------------------------------------------------------------
+// qrow must be a valid row (callers clamp padded queries to row N-1: their
+// fragments are finite and their outputs are never stored).  Unconditional loads,
+// so a prefetch into qf is not waited for until qf is used.
+template <int HDT>
+SDP_DEV void attn_load_q(const bf16_t* qrow, int hf, bf16x8 (&qf)[2 * HDT]) {
+#pragma unroll
+  for (int s = 0; s < 2 * HDT; ++s) qf[s] = *(const bf16x8*)(qrow + 16 * s + 8 * hf);
+}
+
+// q_norm (layers.py:236, :286) on the fragments: mean / biased var over the head
+// dim (the two halves of a query meet through one cross-half shuffle).
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+// two fp32 -> one dword of two bf16 (RNE), a single v_cvt_pk_bf16_f32
+SDP_DEV uint32_t pack_bf16x2(float a, float b) {
+  const bf16x2v v = __builtin_convertvector((f32x2){a, b}, bf16x2v);
+  return __builtin_bit_cast(uint32_t, v);
+}
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+// Partial LayerNorm statistics of one 8 x bf16 fragment: {sum x, sum x^2} with
+// v_dot2_f32_bf16 (fp32 accumulation), 8 instructions per fragment.
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+SDP_DEV f32x2 frag_stats(const bf16x8& v, f32x2 acc) {
+  // (element-wise pairs: bit-casting a u32x4 lane to bf16x2 miscompiles in ROCm 7.2 hipcc,
+  // every pair then reads dword 0)
+  const bf16x8v v8 = __builtin_bit_cast(bf16x8v, v);
+  const bf16x2v one = __builtin_bit_cast(bf16x2v, 0x3F803F80u);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bf16x2v x = {v8[2 * k], v8[2 * k + 1]};
+    acc.x = __builtin_amdgcn_fdot2_f32_bf16(x, one, acc.x, false);
+    acc.y = __builtin_amdgcn_fdot2_f32_bf16(x, x, acc.y, false);
+  }
+  return acc;
+}
+// y = (x - mean) * rstd * g + b on one fragment (g, b: its 8 columns), packed f32
+// math: y = x * t + (b - mean * t) with t = rstd * g.
+SDP_DEV bf16x8 frag_norm(const bf16x8& v, float mean, float rstd, const float* g, const float* b) {
+  const u32x4 w = __builtin_bit_cast(u32x4, v);
+  const f32x4 g0 = *(const f32x4*)g, g1 = *(const f32x4*)(g + 4);
+  const f32x4 b0 = *(const f32x4*)b, b1 = *(const f32x4*)(b + 4);
+  const f32x2 r2 = {rstd, rstd}, m2 = {-mean, -mean};
+  u32x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f32x2 x = {__uint_as_float(w[k] << 16), __uint_as_float(w[k] & 0xFFFF0000u)};
+    const f32x2 gg = k < 2 ? f32x2{g0[2 * k], g0[2 * k + 1]} : f32x2{g1[2 * k - 4], g1[2 * k - 3]};
+    const f32x2 bb = k < 2 ? f32x2{b0[2 * k], b0[2 * k + 1]} : f32x2{b1[2 * k - 4], b1[2 * k - 3]};
+    const f32x2 t = gg * r2;
+    const f32x2 c = t * m2 + bb;
+    const f32x2 y = x * t + c;
+    o[k] = pack_bf16x2(y.x, y.y);
+  }
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+template <int HDT>
+SDP_DEV void attn_norm_q(bf16x8 (&qf)[2 * HDT], bool qok, int hf, const float* gq, const float* bq, float eps) {
+  constexpr int HD = 32 * HDT;
+  f32x2 st = {0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 2 * HDT; ++s) st = frag_stats(qf[s], st);
+  st.x += __shfl_xor(st.x, 32, 64);
+  st.y += __shfl_xor(st.y, 32, 64);
+  const float qmean = st.x * (1.0f / HD);
+  const float qrstd = rsqrtf(fmaxf(st.y * (1.0f / HD) - qmean * qmean, 0.f) + eps);
+#pragma unroll
+  for (int s = 0; s < 2 * HDT; ++s) {
+    const int d = 16 * s + 8 * hf;
+    qf[s] = qok ? frag_norm(qf[s], qmean, qrstd, gq + d, bq + d) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+
+// One 32-query tile against all keys: K rows in Ks ([.][HD], 16-B chunk c of row
+// r at c ^ ((r >> 2) & 3)), V rows in Vs ([NP16][HD] row-major).  Online softmax
+// over 32-key tiles; O row written (bf16) to orow unless null.
+template <int HDT>
+SDP_DEV void attn_qtile(const bf16_t* Ks, const bf16_t* Vs, const bf16x8 (&qf)[2 * HDT], int N, int nkt,
+                        float scale_log2, int lane, bf16_t* orow) {
+  constexpr int HD = 32 * HDT;
+  constexpr int NDS = HD / 16;
+  const int r = lane & 31, hf = lane >> 5;
+  f32x16 acc[HDT];
+#pragma unroll
+  for (int dt = 0; dt < HDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int kswz = (r >> 2) & 3;  // K row (kt*32 + r) swizzle
+  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  for (int kt = 0; kt < nkt; ++kt) {
+    f32x16 st;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) st[i] = 0.f;
+    const bf16x8* krow = (const bf16x8*)(Ks + (size_t)(kt * 32 + r) * HD);
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(krow[(2 * s + hf) ^ kswz], qf[s], st, 0, 0, 0);
+    if (kt * 32 + 32 > N) {  // mask padded keys of the last tile
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+        if (key >= N) st[i] = -INFINITY;
+      }
+    }
+    float tmax = fmaxf(fmaxf(st[0], st[1]), st[2]);
+#pragma unroll
+    for (int i = 3; i < 15; i += 2) tmax = fmaxf(fmaxf(tmax, st[i]), st[i + 1]);
+    tmax = fmaxf(tmax, st[15]);
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    if (__any(mn > m)) {  // wave-uniform: rescale only when some running max moved
+      const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < HDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
+      m = mn;
+    }
+    const float msc = -m * scale_log2;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      if (kt * 32 + 16 * s2 >= N) break;  // whole half past the keys (wave-uniform)
+      float p[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        p[j] = __builtin_amdgcn_exp2f(fmaf(st[8 * s2 + j], scale_log2, msc));
+        l += p[j];
+      }
+      bf16x8 pb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[j] = (short)f2bf(p[j]);
+      const int key0 = kt * 32 + 16 * s2 + 4 * hf;
+      // V^T fragments by inline-asm ds_read_b64_tr_b16: the builtin makes hipcc wait
+      // vmcnt(0) (an in-flight LDS-DMA might alias), which would drain the next
+      // pair's prefetch here; the reads' own completion is waited for explicitly.
+      bf16x4 lo[HDT], hi[HDT];
+#pragma unroll
+      for (int dt = 0; dt < HDT; ++dt) {
+        const uint32_t va = (uint32_t)(uintptr_t)(const AS3 bf16_t*)(Vs + (size_t)(key0 + tq) * HD + dt * 32 +
+                                                                     16 * ((lane >> 4) & 1) + 4 * tp);
+        asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:%3"
+                     : "=&v"(lo[dt]), "=&v"(hi[dt])
+                     : "v"(va), "i"(16 * HD)
+                     : "memory");
+      }
+#pragma unroll
+      for (int dt = 0; dt < HDT; ++dt) asm volatile("" : "+v"(lo[dt]), "+v"(hi[dt]));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int dt = 0; dt < HDT; ++dt) {
+        asm volatile("" : "+v"(lo[dt]), "+v"(hi[dt]));
+        const bf16x8 vf = {lo[dt][0], lo[dt][1], lo[dt][2], lo[dt][3], hi[dt][0], hi[dt][1], hi[dt][2], hi[dt][3]};
+        acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb, acc[dt], 0, 0, 0);
+      }
+    }
+  }
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.0f / l;
+  if (orow) {
+#pragma unroll
+    for (int dt = 0; dt < HDT; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(acc[dt][4 * g + e] * inv);
+        *(bf16x4*)(orow + dt * 32 + 8 * g + 4 * hf) = o;
+      }
+    }
+  }
+}
+
+// Software-pipelined form of attn_qtile for the 256-VGPR persistent kernel: the
+// QK^T MFMAs of key tile kt+1 are issued before the softmax of tile kt (the MFMA
+// pipe works while the VALU exponentiates), the V^T fragments of tile kt are
+// read before its softmax, and the cross-half max uses v_permlane32_swap.
+template <int HDT>
+SDP_DEV f32x16 attn_qk(const bf16_t* Ks, const bf16x8 (&qf)[2 * HDT], int kt, int r, int hf) {
+  constexpr int HD = 32 * HDT;
+  const int kswz = (r >> 2) & 3;
+  const bf16x8* krow = (const bf16x8*)(Ks + (size_t)(kt * 32 + r) * HD);
+  f32x16 st;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) st[i] = 0.f;
+#pragma unroll
+  for (int s = 0; s < 2 * HDT; ++s)
+    st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(krow[(2 * s + hf) ^ kswz], qf[s], st, 0, 0, 0);
+  return st;
+}
+
+// Same with the K row reads addressed from two per-lane bases: chunk (2s + hf) ^ kswz
+// = 4 (s >> 1) + ((2 (s & 1) + hf) ^ kswz), so k-steps s and s + 2 differ by an
+// immediate 64 B and key tiles by an immediate 32 * HD * 2 B.
+template <int HDT>
+SDP_DEV f32x16 attn_qk2(const char* k0, const char* k1, const bf16x8 (&qf)[2 * HDT], int kt) {
+  constexpr int HD = 32 * HDT;
+  f32x16 st;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) st[i] = 0.f;
+#pragma unroll
+  for (int s = 0; s < 2 * HDT; ++s) {
+    const char* a = ((s & 1) ? k1 : k0) + kt * 32 * HD * 2 + 64 * (s >> 1);
+    st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)a, qf[s], st, 0, 0, 0);
+  }
+  return st;
+}
+
+SDP_DEV float xhalf_max(float v) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+}
+SDP_DEV float xhalf_sum(float v) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+}
+
+template <int HDT>
+SDP_DEV void attn_qtile_pipe(const bf16_t* Ks, const bf16_t* Vs, const bf16x8 (&qf)[2 * HDT], int N, int nkt,
+                             float scale_log2, int lane, bf16_t* orow) {
+  constexpr int HD = 32 * HDT;
+  const int r = lane & 31, hf = lane >> 5;
+  f32x16 acc[HDT];
+#pragma unroll
+  for (int dt = 0; dt < HDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  const uint32_t vbase = (uint32_t)(uintptr_t)(const AS3 bf16_t*)(Vs + (size_t)(4 * hf + tq) * HD +
+                                                                  16 * ((lane >> 4) & 1) + 4 * tp);
+  f32x16 st = attn_qk<HDT>(Ks, qf, 0, r, hf);
+  for (int kt = 0; kt < nkt; ++kt) {
+    f32x16 stn;
+    if (kt + 1 < nkt) stn = attn_qk<HDT>(Ks, qf, kt + 1, r, hf);
+    const bool h1 = kt * 32 + 16 < N;  // second 16-key half has keys (wave-uniform)
+    // V^T fragments of tile kt (inline asm: see attn_qtile)
+    bf16x4 lo[2][HDT], hi[2][HDT];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      if (s2 == 1 && !h1) break;
+#pragma unroll
+      for (int dt = 0; dt < HDT; ++dt) {
+        const uint32_t va = vbase + (uint32_t)(((kt * 32 + 16 * s2) * HD + dt * 32) * 2);
+        asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:%3"
+                     : "=&v"(lo[s2][dt]), "=&v"(hi[s2][dt])
+                     : "v"(va), "i"(16 * HD)
+                     : "memory");
+      }
+    }
+    if (kt * 32 + 32 > N) {  // mask padded keys of the last tile
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+        if (key >= N) st[i] = -INFINITY;
+      }
+    }
+    float tmax = fmaxf(fmaxf(st[0], st[1]), st[2]);
+#pragma unroll
+    for (int i = 3; i < 15; i += 2) tmax = fmaxf(fmaxf(tmax, st[i]), st[i + 1]);
+    tmax = xhalf_max(fmaxf(tmax, st[15]));
+    const float mn = fmaxf(m, tmax);
+    if (__any(mn > m)) {  // wave-uniform: rescale only when some running max moved
+      const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < HDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
+      m = mn;
+    }
+    const float msc = -m * scale_log2;
+    bf16x8 pb[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(st[8 * s2 + j], scale_log2, msc));
+        l += p;
+        pb[s2][j] = (short)f2bf(p);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < HDT; ++dt) asm volatile("" : "+v"(lo[s2][dt]), "+v"(hi[s2][dt]));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      if (s2 == 1 && !h1) break;
+#pragma unroll
+      for (int dt = 0; dt < HDT; ++dt) {
+        asm volatile("" : "+v"(lo[s2][dt]), "+v"(hi[s2][dt]));
+        const bf16x8 vf = {lo[s2][dt][0], lo[s2][dt][1], lo[s2][dt][2], lo[s2][dt][3],
+                           hi[s2][dt][0], hi[s2][dt][1], hi[s2][dt][2], hi[s2][dt][3]};
+        acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[s2], acc[dt], 0, 0, 0);
+      }
+    }
+    st = stn;
+  }
+  l = xhalf_sum(l);
+  const float inv = 1.0f / l;
+  if (orow) {
+#pragma unroll
+    for (int dt = 0; dt < HDT; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(acc[dt][4 * g + e] * inv);
+        *(bf16x4*)(orow + dt * 32 + 8 * g + 4 * hf) = o;
+      }
+    }
+  }
+}
+
+// Chunked form for N <= 32 * NKT keys, used by the persistent kernel: the key
+// tiles are taken CH at a time; a chunk's CH S^T tiles are computed first (CH
+// independent MFMA chains), then one max over the chunk (one rescale of O per
+// chunk after the first), one pass of exp2 / row sums / bf16 packing, then P V^T.
+// Few, long MFMA and VALU phases per wave instead of one short chain per key
+// tile, so the two waves of a SIMD overlap each other's phases.
+// The next Q tile (qnext) is loaded into qn after the last chunk's
+// exponentials, when the S^T registers are free: the loads overlap the P V^T phase.
+template <int HDT, int NKT, int CH>
+SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8 (&qf)[2 * HDT], int N,
+                                float scale_log2, int lane, bf16_t* orow, const bf16_t* qnext,
+                                bf16x8 (&qn)[2 * HDT]) {
+  constexpr int HD = 32 * HDT;
+  const int r = lane & 31, hf = lane >> 5;
+  f32x16 acc[HDT];  // first written by the first P V^T MFMA (zero C operand): not live before
+  float m = -INFINITY;
+  f32x2 l2 = {0.f, 0.f};  // row sum, two partial sums
+  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  const uint32_t vbase = (uint32_t)(uintptr_t)(const AS3 bf16_t*)(Vs + (size_t)(4 * hf + tq) * HD +
+                                                                  16 * ((lane >> 4) & 1) + 4 * tp);
+  const int kswz = (r >> 2) & 3;
+  const char* kb0 = (const char*)(Ks + (size_t)r * HD) + 16 * ((hf) ^ kswz);
+  const char* kb1 = (const char*)(Ks + (size_t)r * HD) + 16 * ((2 + hf) ^ kswz);
+#pragma unroll
+  for (int c0 = 0; c0 < NKT; c0 += CH) {
+    constexpr int dummy = 0;
+    (void)dummy;
+    const int n = NKT - c0 < CH ? NKT - c0 : CH;  // compile-time after unrolling
+    f32x16 st[CH];
+#pragma unroll
+    for (int t = 0; t < CH; ++t)
+      if (t < n) {
+        st[t] = attn_qk2<HDT>(kb0, kb1, qf, c0 + t);
+        // pin the phase order (IR passes would otherwise sink work to its uses and
+        // interleave the phases, multiplying the live registers)
+        asm volatile("" : "+v"(st[t]));
+      }
+    if (c0 + n == NKT && NKT * 32 > N) {  // mask padded keys of the last tile
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = (NKT - 1) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+        if (key >= N) st[n - 1][i] = -INFINITY;
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < CH; ++t)
+      if (t < n)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) mx = fmaxf(fmaxf(mx, st[t][i]), st[t][i + 1]);
+    mx = xhalf_max(mx);
+    if (c0 > 0) {  // acc holds earlier chunks
+      const float mn = fmaxf(m, mx);
+      const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+      l2 *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < HDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
+      m = mn;
+    } else {
+      m = mx;
+    }
+    const float msc = -m * scale_log2;
+    const f32x2 sl2 = {scale_log2, scale_log2}, msc2 = {msc, msc};
+    bf16x8 pb[CH][2];
+#pragma unroll
+    for (int t = 0; t < CH; ++t)
+      if (t < n) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          u32x4 pk;
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            // packed scale-and-subtract and packed row sum: 5 VALU per 2 elements
+            const f32x2 a = f32x2{st[t][8 * s2 + j], st[t][8 * s2 + j + 1]} * sl2 + msc2;
+            const f32x2 p2 = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+            l2 += p2;
+            pk[j >> 1] = pack_bf16x2(p2.x, p2.y);
+          }
+          pb[t][s2] = __builtin_bit_cast(bf16x8, pk);
+        }
+        asm volatile("" : "+v"(pb[t][0]), "+v"(pb[t][1]), "+v"(l2));  // one tile's exponentials at a time
+      }
+    if (c0 + n == NKT) {
+      asm volatile("" ::: "memory");
+      attn_load_q<HDT>(qnext, hf, qn);
+    }  // P complete before P V^T (bounds the live registers)
+#pragma unroll
+    for (int t = 0; t < CH; ++t) {
+      if (t >= n) break;
+      const int kt = c0 + t;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        if (kt == NKT - 1 && s2 == 1 && kt * 32 + 16 >= N) break;  // half past the keys (uniform)
+        bf16x4 lo[HDT], hi[HDT];
+#pragma unroll
+        for (int dt = 0; dt < HDT; ++dt) {
+          const uint32_t va = vbase + (uint32_t)(((kt * 32 + 16 * s2) * HD + dt * 32) * 2);
+          asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:%3"
+                       : "=&v"(lo[dt]), "=&v"(hi[dt])
+                       : "v"(va), "i"(16 * HD)
+                       : "memory");
+        }
+#pragma unroll
+        for (int dt = 0; dt < HDT; ++dt) asm volatile("" : "+v"(lo[dt]), "+v"(hi[dt]));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int dt = 0; dt < HDT; ++dt) {
+          asm volatile("" : "+v"(lo[dt]), "+v"(hi[dt]));
+          const bf16x8 vf = {lo[dt][0], lo[dt][1], lo[dt][2], lo[dt][3], hi[dt][0], hi[dt][1], hi[dt][2], hi[dt][3]};
+          if (kt == 0 && s2 == 0) {
+            const f32x16 z = {};
+            acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[t][s2], z, 0, 0, 0);
+          } else {
+            acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[t][s2], acc[dt], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  const float l = xhalf_sum(l2.x + l2.y);
+  const float inv = 1.0f / l;
+  if (orow) {
+#pragma unroll
+    for (int dt = 0; dt < HDT; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(acc[dt][4 * g + e] * inv);
+        *(bf16x4*)(orow + dt * 32 + 8 * g + 4 * hf) = o;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// attn_fa2_bf16 — same math and MFMA forms as attn_fa_bf16, laid out so that TWO
+// workgroups fit on a CU (one stages while the other computes):
+//   * LDS holds K and V unpadded, NP16 = ceil(N/16)*16 rows each (N = 200, hd = 96:
+//     2 x 39,936 B <= 80 KiB); both are filled by LDS-DMA (global_load_lds_dwordx4,
+//     no VGPR staging).  K's 16-B chunk c of row r sits at c ^ ((r >> 2) & 3):
+//     with a 192-B row pitch every ds_read_b128 lane group of the QK^T A-operand
+//     read hits 16 distinct 4-bank slots; V's 192-B pitch is already conflict-free
+//     for the 4-key x 32-d transposed reads.
+//   * k_norm runs in place over the staged K rows (one LDS read + write), q_norm
+//     on the Q fragments in registers.
+//   * the 1/sqrt(hd) * log2(e) scale is folded into the exponent's FMA.
+//   * keys >= NP16 are never read as V (the second 16-key half of a tile past N is
+//     skipped); K rows in [NP16, NP32) alias the start of V (finite, masked).
+//   * register budget 128 (4 waves / SIMD) for the 7-wave workgroups.
+// Needs hd % 32 == 0 (whole 4-chunk swizzle groups).
+// ---------------------------------------------------------------------------
+template <int HDT>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDT <= 3 ? 4 : 2))) void attn_fa2_bf16(
+    const bf16_t* __restrict__ QKV, int64_t ldq, bf16_t* __restrict__ O, int64_t ldo, int B, int N, int H,
+    const float* __restrict__ gq, const float* __restrict__ bq, const float* __restrict__ gk,
+    const float* __restrict__ bk, float eps, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  constexpr int HD = 32 * HDT;  // head dim (hd % 32 == 0 on this path)
+  constexpr int CPR = HD / 8;   // 16-B chunks per row
+  const int NP16 = (N + 15) / 16 * 16;
+  const int NP32 = (N + 31) / 32 * 32;
+  bf16_t* Ks = (bf16_t*)sm;               // [NP16][HD] swizzled chunks
+  bf16_t* Vs = Ks + (size_t)NP16 * HD;    // [NP16][HD] row-major
+  // XCD-aware pair order: consecutive (b, h) pairs (which share QKV cache lines)
+  // run on one XCD
+  const int nwg = B * H, x = blockIdx.x;
+  const int xcd = x & 7, qd = nwg >> 3, rem = nwg & 7;
+  const int pair = (xcd < rem ? xcd * (qd + 1) : rem * (qd + 1) + (xcd - rem) * qd) + (x >> 3);
+  const int b = pair / H, hh = pair % H;
+  const int C = H * HD;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwaves = blockDim.x >> 6;
+  const bf16_t* base = QKV + (int64_t)b * N * ldq + hh * HD;
+
+  // ---- K and V -> LDS by DMA: instruction i of the block moves chunks 64i..64i+63
+  // (lane-linear destination); source rows >= N are clamped to N-1 ----
+  {
+    const int nchunk = NP16 * CPR;
+    const int ninst = (nchunk + 63) / 64;
+    for (int i = wave; i < 2 * ninst; i += nwaves) {
+      const bool isv = i >= ninst;
+      const int ii = isv ? i - ninst : i;
+      const int g = ii * 64 + lane;
+      const int row = g / CPR, pc = g - row * CPR;
+      const int srow = row < N ? row : N - 1;
+      const int c = isv ? pc : (pc ^ ((row >> 2) & 3));
+      const bf16_t* src = base + (int64_t)srow * ldq + (isv ? 2 * C : C) + c * 8;
+      char* dst = (char*)(isv ? Vs : Ks) + ii * 1024;
+      if (g < nchunk) __builtin_amdgcn_global_load_lds((const AS1 void*)src, (AS3 void*)dst, 16, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // ---- k_norm in place: 16 lanes per row (CPR <= 16 active) ----
+  if (gk) {
+    const int sub = tid & 15;
+    const bool act = sub < CPR;
+    for (int row = tid >> 4; row < NP16; row += nwaves * 4) {
+      bf16x8* p = (bf16x8*)(Ks + (size_t)row * HD) + (act ? sub : 0);
+      const bf16x8 raw = *p;
+      float kv[8];
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        kv[e] = act ? bf2f((bf16_t)raw[e]) : 0.f;
+        s += kv[e];
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+      const float mean = s * (1.0f / HD);
+      float ss = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = act ? kv[e] - mean : 0.f;
+        ss += d * d;
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
+      const float rstd = 1.0f / sqrtf(ss * (1.0f / HD) + eps);
+      if (act) {
+        const int c8 = (sub ^ ((row >> 2) & 3)) * 8;  // logical columns of this chunk
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (short)f2bf((kv[e] - mean) * rstd * gk[c8 + e] + bk[c8 + e]);
+        *p = o;
+      }
+    }
+    __syncthreads();
+  }
+
+  const int r = lane & 31, hf = lane >> 5;
+  const int nqt = NP32 / 32;
+  for (int qt = wave; qt < nqt; qt += nwaves) {
+    const int q = qt * 32 + r;
+    const bool qok = q < N;
+    bf16x8 qf[2 * HDT];
+    attn_load_q<HDT>(base + (int64_t)(qok ? q : N - 1) * ldq, hf, qf);
+    if (gq) attn_norm_q<HDT>(qf, qok, hf, gq, bq, eps);
+    attn_qtile<HDT>(Ks, Vs, qf, N, nqt, scale_log2, lane, qok ? O + ((int64_t)b * N + q) * ldo + hh * HD : nullptr);
+  }
+}
+
+static size_t attn_fa2_bytes(int N, int hd) { return (size_t)2 * ((N + 15) / 16 * 16) * hd * 2; }
+
+template <int HDT>
+static int launch_attn_fa2(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H,
+                           const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
+                           hipStream_t s) {
+  const size_t bytes = attn_fa2_bytes(N, 32 * HDT);
+  if (bytes > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)attn_fa2_bf16<HDT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)bytes);
+    if (e != hipSuccess) return (int)e;
+  }
+  int waves = (N + 31) / 32;
+  if (waves > 8) waves = 8;
+  hipLaunchKernelGGL(attn_fa2_bf16<HDT>, dim3(B * H), dim3(64 * waves), bytes, s, (const bf16_t*)QKV, ldq,
+                     (bf16_t*)O, ldo, B, N, H, gq, bq, gk, bk, eps, scale * 1.4426950408889634f);
+  return SDP_CHECK_LAUNCH();
+}
+
+// k_norm (layers.py:237, :286) in place on 32 staged K rows row0 .. row0+31
+// (swizzled image, see attn_qtile): lane (r, hf) normalises head dims
+// [HD/2 * hf, HD/2 * (hf+1)) of row row0 + r; the halves meet by one permlane32
+// swap.  g / be: k_norm gamma / beta (LDS).
+template <int HDT>
+SDP_DEV void attn_knorm32(bf16_t* Kd, int row0, int NP16, int lane, const float* g, const float* be, float eps) {
+  constexpr int HD = 32 * HDT, NDS = HD / 16;
+  const int r = lane & 31, hf = lane >> 5;
+  const int row = row0 + r;
+  const bool ok = row < NP16;  // same for both halves of a row
+  bf16x8* kr = (bf16x8*)(Kd + (size_t)(ok ? row : 0) * HD);
+  const int sw = (row >> 2) & 3;
+  bf16x8 kv[NDS];
+  f32x2 st = {0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < NDS; ++i) {
+    kv[i] = kr[(NDS * hf + i) ^ sw];
+    st = frag_stats(kv[i], st);
+  }
+  st.x = xhalf_sum(st.x);
+  st.y = xhalf_sum(st.y);
+  const float mean = st.x * (1.0f / HD);
+  const float rstd = rsqrtf(fmaxf(st.y * (1.0f / HD) - mean * mean, 0.f) + eps);
+  if (ok) {
+#pragma unroll
+    for (int i = 0; i < NDS; ++i) {
+      const int c8 = (NDS * hf + i) * 8;
+      kr[(NDS * hf + i) ^ sw] = frag_norm(kv[i], mean, rstd, g + c8, be + c8);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// attn_fa4_bf16 — two persistent 4-wave workgroups per CU, each with ONE K/V
+// buffer (80 KiB): a workgroup loads a pair (LDS-DMA), k-norms it and computes it
+// while the other workgroup of the CU is in a different phase, so the two waves
+// of a SIMD (one per workgroup) are not in lockstep and one's MFMA phase overlaps
+// the other's VALU or load phase.  Wave w computes query tiles w and w + 4
+// (slots 0, 1) with the chunked whole-tile softmax; each slot prefetches the
+// next slot's Q fragments (the next pair's slot 0 after slot 1).
+// LDS: (K + V) x NP16 x HD x 2 B + 4 x HD x 4 B  (N = 200, hd = 96: 81,408 B).
+// ---------------------------------------------------------------------------
+template <int HDT, int NKT>
+__global__ __launch_bounds__(256, 2) void attn_fa4_bf16(const bf16_t* __restrict__ QKV, int64_t ldq,
+                                                     bf16_t* __restrict__ O, int64_t ldo, int B, int N, int H,
+                                                     const float* __restrict__ gq, const float* __restrict__ bq,
+                                                     const float* __restrict__ gk, const float* __restrict__ bk,
+                                                     float eps, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  constexpr int HD = 32 * HDT, CPR = HD / 8;
+  const int NP16 = (N + 15) / 16 * 16;
+  bf16_t* const Ks = (bf16_t*)sm;
+  bf16_t* const Vs = Ks + (size_t)NP16 * HD;
+  float* const prm = (float*)(sm + (size_t)2 * NP16 * HD * sizeof(bf16_t));  // gq | bq | gk | bk
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int npairs = B * H, G = gridDim.x, x = blockIdx.x;
+  const int nj = (npairs - x + G - 1) / G;
+  if (nj <= 0) return;
+  const int C = H * HD;
+  const bool norm = gq != nullptr;
+  if (norm) {
+    for (int i = tid; i < 4 * HD; i += 256) {
+      const int k = i / HD, d = i - k * HD;
+      prm[i] = (k == 0 ? gq : k == 1 ? bq : k == 2 ? gk : bk)[d];
+    }
+  }
+  // pair order: virtual id x + jG through the XCD-contiguous remap (G % 8 == 0)
+  auto pair_of = [&](int j) {
+    const int v = x + j * G;
+    const int xcd = v & 7, qd = npairs >> 3, rem = npairs & 7;
+    return (xcd < rem ? xcd * (qd + 1) : rem * (qd + 1) + (xcd - rem) * qd) + (v >> 3);
+  };
+  auto qkv_base = [&](int pair) {
+    const int b = pair / H, hh = pair - (pair / H) * H;
+    return QKV + (int64_t)b * N * ldq + hh * HD;
+  };
+  const int nchunk = NP16 * CPR, ninst = (nchunk + 63) / 64;
+  auto stage = [&](int pair) {
+    const bf16_t* base = qkv_base(pair);
+    for (int i = wave; i < 2 * ninst; i += 4) {
+      const bool isv = i >= ninst;
+      const int ii = isv ? i - ninst : i;
+      const int g = ii * 64 + lane;
+      const int row = g / CPR, pc = g - row * CPR;
+      const int srow = row < N ? row : N - 1;
+      const int c = isv ? pc : (pc ^ ((row >> 2) & 3));
+      const bf16_t* src = base + (int64_t)srow * ldq + (isv ? 2 * C : C) + c * 8;
+      char* dst = (char*)(isv ? Vs : Ks) + ii * 1024;
+      if (g < nchunk) __builtin_amdgcn_global_load_lds((const AS1 void*)src, (AS3 void*)dst, 16, 0, 0);
+    }
+  };
+  const int r = lane & 31, hf = lane >> 5;
+  // Every wave computes two query-tile slots per pair; a slot past the last tile
+  // (e.g. tile 7 at N = 200) is computed on row N-1 and not stored: it sits on a
+  // SIMD whose partner slots are real, so it costs no time on the critical path,
+  // and it keeps the Q prefetch unconditional (no register merges that would make
+  // the compiler wait for the loads).
+  const int q0 = wave * 32 + r, q1 = (wave + 4) * 32 + r;
+  const bool ok0 = q0 < N, ok1 = q1 < N;
+  const int64_t off0 = (int64_t)(ok0 ? q0 : N - 1) * ldq, off1 = (int64_t)(ok1 ? q1 : N - 1) * ldq;
+  bf16x8 qa[2 * HDT], qb[2 * HDT];
+  int pair = pair_of(0);
+  attn_load_q<HDT>(qkv_base(pair) + off0, hf, qa);
+  for (int j = 0; j < nj; ++j) {
+    const int nxt = j + 1 < nj ? pair_of(j + 1) : pair;  // last pair: a harmless re-load
+    stage(pair);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (norm) {
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
+        if (32 * (wave + 4 * rr) < NP16) attn_knorm32<HDT>(Ks, 32 * (wave + 4 * rr), NP16, lane, prm + 2 * HD, prm + 3 * HD, eps);
+      __syncthreads();
+    }
+    const int b = pair / H, hh = pair - (pair / H) * H;
+    bf16_t* obase = O + (int64_t)b * N * ldo + hh * HD;
+    // slot 0 (query tile w), prefetching slot 1's Q
+    if (norm) attn_norm_q<HDT>(qa, ok0, hf, prm, prm + HD, eps);
+    attn_qtile_chunked<HDT, NKT, ATTN_CH>(Ks, Vs, qa, N, scale_log2, lane, ok0 ? obase + q0 * ldo : nullptr,
+                                          qkv_base(pair) + off1, qb);
+    // slot 1 (query tile w + 4), prefetching the next pair's slot 0
+    if (norm) attn_norm_q<HDT>(qb, ok1, hf, prm, prm + HD, eps);
+    attn_qtile_chunked<HDT, NKT, ATTN_CH>(Ks, Vs, qb, N, scale_log2, lane, ok1 ? obase + q1 * ldo : nullptr,
+                                          qkv_base(nxt) + off0, qa);
+    pair = nxt;
+    __syncthreads();  // every wave is done with K / V before the next pair's DMA
+  }
+}
+
+static int g_attn_grid = 0;  // persistent grid override (0 = two workgroups per CU)
+
+static size_t attn_fa4_bytes(int N, int hd) { return (size_t)2 * ((N + 15) / 16 * 16) * hd * 2 + 16 * (size_t)hd; }
+
+template <int HDT>
+static int launch_attn_fa4(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H,
+                           const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
+                           hipStream_t s) {
+  const size_t bytes = attn_fa4_bytes(N, 32 * HDT);
+  const void* fn;
+  switch ((N + 31) / 32) {
+    case 1: fn = (const void*)attn_fa4_bf16<HDT, 1>; break;
+    case 2: fn = (const void*)attn_fa4_bf16<HDT, 2>; break;
+    case 3: fn = (const void*)attn_fa4_bf16<HDT, 3>; break;
+    case 4: fn = (const void*)attn_fa4_bf16<HDT, 4>; break;
+    case 5: fn = (const void*)attn_fa4_bf16<HDT, 5>; break;
+    case 6: fn = (const void*)attn_fa4_bf16<HDT, 6>; break;
+    case 7: fn = (const void*)attn_fa4_bf16<HDT, 7>; break;
+    case 8: fn = (const void*)attn_fa4_bf16<HDT, 8>; break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) return (int)e;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  const int per_cu = bytes <= 80 * 1024 ? 2 : 1;
+  int grid = g_attn_grid > 0 ? g_attn_grid : per_cu * ncu;
+  grid = grid / 8 * 8;
+  if (grid < 8) grid = 8;
+  if (grid > B * H) grid = B * H;
+  const float sl = scale * 1.4426950408889634f;
+  const bf16_t* q = (const bf16_t*)QKV;
+  bf16_t* o = (bf16_t*)O;
+  void* args[] = {(void*)&q, (void*)&ldq, (void*)&o, (void*)&ldo, (void*)&B, (void*)&N, (void*)&H, (void*)&gq,
+                  (void*)&bq, (void*)&gk, (void*)&bk, (void*)&eps, (void*)&sl};
+  e = hipLaunchKernel(fn, dim3(grid), dim3(256), args, bytes, s);
+  if (e != hipSuccess) return (int)e;
+  return SDP_CHECK_LAUNCH();
+}
+
 template <int HDT>
 static int launch_attn_fa(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H, int hd,
                           const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
@@ -323,8 +1081,19 @@ static size_t attn_fa_bytes(int N, int hd) {
   return ((size_t)NP * (hd + 8) + (size_t)NP * (32 * HDT + 8)) * 2;
 }
 
+// bf16 flash kernel selection: 2 = attn_fa_bf16, 3 = attn_fa2_bf16, 4 (default) =
+// attn_fa4_bf16 (each where it applies, else the next lower one)
+static int g_attn_kernel = 4;
+extern "C" int sdp_attention_set_kernel(int k) {
+  const int old = g_attn_kernel;
+  if (k >= 2 && k <= 4) g_attn_kernel = k;
+  return old;
+}
+
 extern "C" int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask) {
   if (dtype != 1 || has_mask || head_dim > 128 || head_dim % 16 != 0) return 0;
+  if (g_attn_kernel >= 4 && head_dim % 32 == 0 && N <= 256 && attn_fa4_bytes(N, head_dim) <= 160 * 1024) return 4;
+  if (g_attn_kernel >= 3 && head_dim % 32 == 0 && attn_fa2_bytes(N, head_dim) <= 160 * 1024) return 3;
   if (attn_fa_bytes(N, head_dim) > 160 * 1024) return 0;
   return 2;
 }
@@ -343,8 +1112,29 @@ extern "C" int sdp_attention(int dtype, const void* QKV, int64_t ldq, void* O, i
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const float scale = 1.0f / sqrtf((float)head_dim);
-  if (sdp_attention_variant(dtype, N, n_head, head_dim, mask != nullptr) == 2 && (ldq % 8 == 0) && (ldo % 4 == 0) &&
-      ((uintptr_t)QKV % 16 == 0) && ((uintptr_t)O % 8 == 0)) {
+  const bool al = (ldq % 8 == 0) && (ldo % 4 == 0) && ((uintptr_t)QKV % 16 == 0) && ((uintptr_t)O % 8 == 0);
+  const int variant = al ? sdp_attention_variant(dtype, N, n_head, head_dim, mask != nullptr) : 0;
+  if (variant == 4) {
+    const float *gq = norm ? q_gamma : nullptr, *bq = norm ? q_beta : nullptr;
+    const float *gk = norm ? k_gamma : nullptr, *bk = norm ? k_beta : nullptr;
+    switch (head_dim / 32) {
+      case 1: return launch_attn_fa4<1>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      case 2: return launch_attn_fa4<2>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      case 3: return launch_attn_fa4<3>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      default: return launch_attn_fa4<4>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+    }
+  }
+  if (variant == 3) {
+    const float *gq = norm ? q_gamma : nullptr, *bq = norm ? q_beta : nullptr;
+    const float *gk = norm ? k_gamma : nullptr, *bk = norm ? k_beta : nullptr;
+    switch (head_dim / 32) {
+      case 1: return launch_attn_fa2<1>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      case 2: return launch_attn_fa2<2>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      case 3: return launch_attn_fa2<3>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      default: return launch_attn_fa2<4>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+    }
+  }
+  if (variant == 2) {
     const int HDT = (head_dim + 31) / 32;
     const float *gq = norm ? q_gamma : nullptr, *bq = norm ? q_beta : nullptr;
     const float *gk = norm ? k_gamma : nullptr, *bk = norm ? k_beta : nullptr;

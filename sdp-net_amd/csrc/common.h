@@ -14,6 +14,8 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 #define SDP_DEV __device__ __forceinline__
+#define AS1 __attribute__((address_space(1)))
+#define AS3 __attribute__((address_space(3)))
 
 SDP_DEV float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
 SDP_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }

@@ -30,8 +30,6 @@
 // access (bias, residual, output) is an 8/16-byte vector per lane.
 #include "common.h"
 
-#define AS1 __attribute__((address_space(1)))
-#define AS3 __attribute__((address_space(3)))
 
 template <typename T>
 struct Epi {

@@ -43,6 +43,7 @@ _SIGS = {
     "sdp_attention": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _i64,
                        _i64, _vp], _i32),
     "sdp_attention_variant": ([_i32, _i32, _i32, _i32, _i32], _i32),
+    "sdp_attention_set_kernel": ([_i32], _i32),
     "sdp_patchify": ([_i32, _vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp], _i32),
     "sdp_pos_table": ([_vp, _vp, _vp, _i32, _i32, _i32, _vp], _i32),
     "sdp_avgpool_table": ([_vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp], _i32),
@@ -86,6 +87,9 @@ def lib():
         kern = os.environ.get("SDPNET_GEMM_KERNEL")  # A/B switch for the bf16 fast GEMM (benchmarks)
         if kern:
             L.sdp_gemm_set_fast_kernel(int(kern))
+        kern = os.environ.get("SDPNET_ATTN_KERNEL")  # A/B switch for the bf16 flash attention
+        if kern:
+            L.sdp_attention_set_kernel(int(kern))
         _lib = L
     return _lib
 

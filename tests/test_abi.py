@@ -41,8 +41,8 @@ def test_gemm_variant_selection():
 
 def test_attention_variant_selection():
     L = sp.lib()
-    assert L.sdp_attention_variant(1, 200, 8, 96, 0) == 2
-    assert L.sdp_attention_variant(1, 260, 8, 96, 0) == 2
+    assert L.sdp_attention_variant(1, 200, 8, 96, 0) == 4
+    assert L.sdp_attention_variant(1, 260, 8, 96, 0) == 3
     assert L.sdp_attention_variant(1, 200, 8, 96, 1) == 0   # masks -> generic
     assert L.sdp_attention_variant(0, 200, 8, 96, 0) == 0   # fp32 -> generic
     assert L.sdp_attention_variant(1, 53, 8, 12, 0) == 0    # hd % 8 != 0

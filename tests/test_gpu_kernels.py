@@ -202,24 +202,35 @@ def attn_ref(qkv, B, N, H, hd, add=None):
 @pytest.mark.parametrize("B,N,H,hd", [(2, 200, 8, 96), (1, 260, 8, 96), (3, 200, 8, 16), (2, 53, 4, 16),
                                       (1, 5, 2, 32), (2, 1, 8, 64), (1, 300, 2, 128), (2, 53, 8, 12),
                                       (1, 384, 8, 96), (1, 500, 4, 32)])
-def test_attention(dtype, B, N, H, hd):
+@pytest.mark.parametrize("kern", [2, 3, 4])
+def test_attention(dtype, B, N, H, hd, kern):
+    if dtype == torch.float32 and kern == 2:
+        pytest.skip("kernel selection applies to bf16 only")
     C = H * hd
     qkv = rnd(B * N, 3 * C, dtype=dtype, seed=40)
     o = torch.empty(B * N, C, dtype=dtype, device=DEV)
-    sp.attention(qkv, o, B, N, H, hd)
-    close(o, attn_ref(qkv, B, N, H, hd), dtype, what=f"attn variant {sp.attention_variant(dtype, N, H, hd)}")
+    old = sp.lib().sdp_attention_set_kernel(kern)
+    try:
+        sp.attention(qkv, o, B, N, H, hd)
+        v = sp.attention_variant(dtype, N, H, hd)
+    finally:
+        sp.lib().sdp_attention_set_kernel(old)
+    close(o, attn_ref(qkv, B, N, H, hd), dtype, what=f"attn variant {v}")
 
 
 def test_attention_mfma_path_is_taken_for_canonical_shapes():
-    assert sp.attention_variant(BF, 200, 8, 96) == 2
-    assert sp.attention_variant(BF, 260, 8, 96) == 2
-    assert sp.attention_variant(BF, 200, 8, 16) == 2
+    assert sp.attention_variant(BF, 200, 8, 96) == 4   # two persistent workgroups per CU
+    assert sp.attention_variant(BF, 260, 8, 96) == 3   # N > 256 -> two-workgroups-per-CU single-pass kernel
+    assert sp.attention_variant(BF, 200, 8, 16) == 2   # hd % 32 != 0 -> one-workgroup kernel
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
 @pytest.mark.parametrize("B,N,H,hd", [(2, 200, 8, 96), (1, 260, 8, 96), (2, 53, 4, 16), (1, 77, 2, 64),
                                       (2, 33, 8, 12), (1, 300, 2, 128)])
-def test_attention_fused_qk_norm(dtype, B, N, H, hd):
+@pytest.mark.parametrize("kern", [2, 3, 4])
+def test_attention_fused_qk_norm(dtype, B, N, H, hd, kern):
+    if dtype == torch.float32 and kern == 2:
+        pytest.skip("kernel selection applies to bf16 only")
     C = H * hd
     qkv = rnd(B * N, 3 * C, dtype=dtype, seed=44, scale=2.0)
     gq, bq, gk, bk = (rnd(hd, seed=s) * 0.1 + (1 if s % 2 == 0 else 0) for s in (45, 46, 47, 48))
@@ -228,9 +239,13 @@ def test_attention_fused_qk_norm(dtype, B, N, H, hd):
     ref_in[:, C:2 * C] = F.layer_norm(ref_in[:, C:2 * C].view(-1, H, hd), (hd,), gk, bk).view(-1, C)
     ref = attn_ref(ref_in.to(dtype), B, N, H, hd)
     o = torch.empty(B * N, C, dtype=dtype, device=DEV)
-    sp.attention(qkv, o, B, N, H, hd, qk_norm=(gq, bq, gk, bk), eps=1e-5)
-    close(o, ref, dtype, rel=2e-5 if dtype == torch.float32 else 2e-2,
-          what=f"fused qk-norm attn variant {sp.attention_variant(dtype, N, H, hd)}")
+    old = sp.lib().sdp_attention_set_kernel(kern)
+    try:
+        sp.attention(qkv, o, B, N, H, hd, qk_norm=(gq, bq, gk, bk), eps=1e-5)
+        v = sp.attention_variant(dtype, N, H, hd)
+    finally:
+        sp.lib().sdp_attention_set_kernel(old)
+    close(o, ref, dtype, rel=2e-5 if dtype == torch.float32 else 2e-2, what=f"fused qk-norm attn variant {v}")
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
@@ -246,7 +261,8 @@ def test_attention_mask(dtype):
     close(o, attn_ref(qkv, B, N, H, hd, add), dtype, what="masked attn")
 
 
-def test_attention_spiky_scores():
+@pytest.mark.parametrize("kern", [2, 3, 4])
+def test_attention_spiky_scores(kern):
     # large logits: softmax max-subtraction must hold (no inf/nan), one dominant key
     B, N, H, hd = 1, 200, 8, 96
     C = H * hd
@@ -254,7 +270,11 @@ def test_attention_spiky_scores():
     qkv[:, :C] *= 6
     qkv[7, C:2 * C] *= 8
     o = torch.empty(B * N, C, dtype=BF, device=DEV)
-    sp.attention(qkv, o, B, N, H, hd)
+    old = sp.lib().sdp_attention_set_kernel(kern)
+    try:
+        sp.attention(qkv, o, B, N, H, hd)
+    finally:
+        sp.lib().sdp_attention_set_kernel(old)
     close(o, attn_ref(qkv, B, N, H, hd), BF, rel=2e-2, what="spiky")
 
 

@@ -29,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="dw,attn,ln,stats")
+    ap.add_argument("--attn-kerns", default="2,3,4")
     args = ap.parse_args()
     dev, bf = "cuda", torch.bfloat16
     B, R, H, W, C, heads = 256, 4, 14, 14, 768, 8
@@ -58,10 +59,13 @@ def main():
         o = torch.empty(B * N, C, device=dev, dtype=bf)
         g = torch.ones(hd, device=dev)
         z = torch.zeros(hd, device=dev)
-        us = timeit(lambda: sp.attention(qkv, o, B, N, heads, hd, qk_norm=(g, z, g, z)), args.reps)
-        fl = 4.0 * B * heads * N * N * hd
-        by = B * N * 4 * C * 2
-        print(f"attention  {us:8.1f} us  {fl / us / 1e6:7.1f} TF/s  {by / us / 1e3:7.1f} GB/s")
+        for kern in [int(k) for k in args.attn_kerns.split(",")]:
+            old = sp.lib().sdp_attention_set_kernel(kern)
+            us = timeit(lambda: sp.attention(qkv, o, B, N, heads, hd, qk_norm=(g, z, g, z)), args.reps)
+            sp.lib().sdp_attention_set_kernel(old)
+            fl = 4.0 * B * heads * N * N * hd
+            by = B * N * 4 * C * 2
+            print(f"attention k{kern} {us:8.1f} us  {fl / us / 1e6:7.1f} TF/s  {by / us / 1e3:7.1f} GB/s")
 
 
 if __name__ == "__main__":
