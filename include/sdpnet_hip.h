@@ -102,6 +102,11 @@ int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstri
                const float* stats, const float* ln_gamma, const float* ln_beta,
                const float* weight, const float* bias, void* Y, int64_t ldy, int y_grp,
                int64_t y_gstride, int y_off, int B, int H, int W, int C, int k, void* stream);
+/* Select the depthwise kernel: 2 (default) = 64-channel x band blocks with an fp32
+ * LDS tile (C % 8 == 0, k in {3,5,7}, 16-B aligned rows), 1 = 32-channel blocks
+ * with a bf16 tile (any shape).  Other values leave the selection unchanged.
+ * Returns the previous selection. */
+int sdp_dwconv_set_kernel(int k);
 
 /*
  * softmax(LN_q(Q) LN_k(K)^T / sqrt(hd) + mask) V per (batch, head) from fused QKV

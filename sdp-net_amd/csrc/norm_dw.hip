@@ -498,6 +498,207 @@ static int dw_dispatch(int k, const void* X, int64_t ldx, RowMap xm, const float
   }
 }
 
+// ---------------------------------------------------------------------------
+// dwconv2_nhwc — the default depthwise kernel (C % 8 == 0, image width <= 57).
+// Block = 64 channels (one full 128-B bf16 line per pixel) x a band of output
+// rows of one image, 256 threads; two blocks per CU (<= 80 KiB LDS each).
+//  * The band + halo is staged ONCE as fp32 in LDS (LN applied, zero padding
+//    materialised), so the inner loop is ds_read_b128 + packed fp32 FMA only.
+//    A pixel is 256 B = all 64 banks: every b128 lane group is conflict-free.
+//  * thread = 4 channels x a STRIP of output pixels of one row; per kernel row it
+//    reads the STRIP+KS-1 window once and accumulates STRIP outputs.
+//  * block order: the bands of one (image, channel group) are consecutive blocks
+//    of one XCD, so the halo rows they share are read from HBM once (L2).
+// ---------------------------------------------------------------------------
+constexpr int DW2_CB = 64;
+constexpr int DW2_LDS = 80 * 1024;
+
+template <typename T, int KS, int STRIP>
+__global__ __launch_bounds__(256) void dwconv2_nhwc(
+    const T* __restrict__ X, int64_t ldx, RowMap xm, const float* __restrict__ stats, const float* __restrict__ lg,
+    const float* __restrict__ lb, const float* __restrict__ Wt, const float* __restrict__ bias, T* __restrict__ Y,
+    int64_t ldy, RowMap ym, int B, int H, int W, int C, int band, int nband, int ncg, int pitch) {
+  constexpr int PAD = KS / 2;
+  extern __shared__ __attribute__((aligned(16))) float dsm2[];
+  const int TH = band + KS - 1;
+  float* tile = dsm2;                              // [TH][pitch][64]
+  float* wts = dsm2 + (size_t)TH * pitch * DW2_CB;  // [KS*KS][64]
+  // block -> (unit = (image, channel group), band): XCD x takes units x, x+8, ...
+  const int bx = blockIdx.x, xcd = bx & 7, k = bx >> 3;
+  const int unit = xcd + 8 * (k / nband), bnd = k - (k / nband) * nband;
+  if (unit >= B * ncg) return;
+  const int b = unit / ncg, cg = unit - b * ncg;
+  const int c0 = cg * DW2_CB, h0 = bnd * band;
+  const int hb = min(band, H - h0);
+  const int tid = threadIdx.x;
+  const int64_t img0 = (int64_t)b * H * W;
+  const int64_t xrow0 = xm(img0), yrow0 = ym(img0);
+
+  bool wdone = false;
+  // ---- stage LN(x) of rows h0-PAD .. h0+hb+PAD-1 as fp32 (8 lanes x 8 channels per pixel) ----
+  const int part = tid & 7;
+  const int c = c0 + part * 8;
+  const bool cok = c < C;  // C % 8 == 0: a part is all in or all out
+  float g8[8], b8[8];
+  const int npix = (hb + KS - 1) * pitch;
+  // all of a thread's pixel loads are issued before any is consumed (one HBM round
+  // trip per block: the staging is latency-bound otherwise)
+  constexpr int UNR = 10;  // 32 pixels per pass: (7 + 6) x 20 = 260 pixels in one pass
+  for (int base = tid >> 3; base < npix; base += 32 * UNR) {
+    float v[UNR][8];
+    float2 st[UNR];
+    bool inb[UNR];
+    // unconditional loads from clamped (valid) addresses, masked afterwards: a
+    // load under a divergent branch makes hipcc wait for it at the branch join
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int pix = base + 32 * u;
+      const int th = pix / pitch, tw = pix - th * pitch;
+      const int h = h0 - PAD + th, w = tw - PAD;
+      inb[u] = pix < npix && cok && h >= 0 && h < H && w >= 0 && w < W;
+      const int hc = min(max(h, 0), H - 1), wc = min(max(w, 0), W - 1);
+      const int64_t local = (int64_t)hc * W + wc;
+      const T* src = X + (xrow0 + local) * ldx + (cok ? c : c0);
+      if constexpr (sizeof(T) == 2) {
+        const bf16x8 r = *(const bf16x8*)src;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[u][e] = bf2f((bf16_t)r[e]);
+      } else {
+        const f32x4 r0 = *(const f32x4*)src, r1 = *(const f32x4*)(src + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[u][e] = r0[e];
+          v[u][4 + e] = r1[e];
+        }
+      }
+      st[u] = stats ? *(const float2*)(stats + 2 * (img0 + local)) : float2{0.f, 1.f};
+    }
+    if (!wdone) {  // weights and LN parameters: loaded behind the pixel loads (one round trip)
+      wdone = true;
+      for (int i = tid; i < KS * KS * DW2_CB; i += 256) {
+        const int tap = i / DW2_CB, cc = i - tap * DW2_CB;
+        wts[i] = (c0 + cc < C) ? Wt[(int64_t)(c0 + cc) * KS * KS + tap] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        g8[e] = (stats && cok) ? lg[c + e] : 1.f;
+        b8[e] = (stats && cok) ? lb[c + e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int pix = base + 32 * u;
+      f32x4 o0, o1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a0 = stats ? (v[u][e] - st[u].x) * st[u].y * g8[e] + b8[e] : v[u][e];
+        const float a1 = stats ? (v[u][4 + e] - st[u].x) * st[u].y * g8[4 + e] + b8[4 + e] : v[u][4 + e];
+        o0[e] = inb[u] ? a0 : 0.f;
+        o1[e] = inb[u] ? a1 : 0.f;
+      }
+      if (pix < npix) {
+        float* dst = tile + (size_t)pix * DW2_CB + part * 8;
+        *(f32x4*)dst = o0;
+        *(f32x4*)(dst + 4) = o1;
+      }
+    }
+  }
+  __syncthreads();
+
+  const int q = tid & 15;   // channels c0 + 4q .. +3
+  const int cg4 = c0 + q * 4;
+  const f32x4 bv = (bias && cg4 < C) ? *(const f32x4*)(bias + cg4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nstrip = (W + STRIP - 1) / STRIP;
+  for (int job = tid >> 4; job < hb * nstrip; job += 16) {
+    const int oh = job / nstrip;
+    const int w0 = (job - oh * nstrip) * STRIP;
+    f32x4 acc[STRIP];
+#pragma unroll
+    for (int o = 0; o < STRIP; ++o) acc[o] = bv;
+#pragma unroll 1
+    for (int ky = 0; ky < KS; ++ky) {
+      const float* trow = tile + ((size_t)(oh + ky) * pitch + w0) * DW2_CB + q * 4;
+      f32x4 win[STRIP + KS - 1];
+#pragma unroll
+      for (int ix = 0; ix < STRIP + KS - 1; ++ix) win[ix] = *(const f32x4*)(trow + ix * DW2_CB);
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) {
+        const f32x4 wv = *(const f32x4*)&wts[(ky * KS + kx) * DW2_CB + q * 4];
+#pragma unroll
+        for (int o = 0; o < STRIP; ++o) acc[o] += win[o + kx] * wv;
+      }
+    }
+    if (cg4 < C) {
+      const int gh = h0 + oh;
+#pragma unroll
+      for (int o = 0; o < STRIP; ++o) {
+        const int w = w0 + o;
+        if (w < W) {
+          T* dst = Y + (yrow0 + (int64_t)gh * W + w) * ldy + cg4;
+          if constexpr (sizeof(T) == 2) {
+            bf16x4 t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t[r] = (short)f2bf(acc[o][r]);
+            *(bf16x4*)dst = t;
+          } else {
+            *(f32x4*)dst = acc[o];
+          }
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int KS, int STRIP>
+static int launch_dw2(const void* X, int64_t ldx, RowMap xm, const float* stats, const float* lg, const float* lb,
+                      const float* Wt, const float* bias, void* Y, int64_t ldy, RowMap ym, int B, int H, int W, int C,
+                      hipStream_t s) {
+  const int nstrip = (W + STRIP - 1) / STRIP;
+  const int pitch = nstrip * STRIP + KS - 1;
+  const size_t row_bytes = (size_t)pitch * DW2_CB * 4;
+  const size_t wbytes = (size_t)KS * KS * DW2_CB * 4;
+  int maxband = (int)((DW2_LDS - wbytes) / row_bytes) - (KS - 1);
+  if (maxband < 1) return -1;  // caller falls back
+  const int nband = (H + maxband - 1) / maxband;
+  const int band = (H + nband - 1) / nband;
+  const size_t lds = (size_t)(band + KS - 1) * row_bytes + wbytes;
+  const int ncg = (C + DW2_CB - 1) / DW2_CB;
+  const int units = B * ncg;
+  const int grid = ((units + 7) / 8) * 8 * nband;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)dwconv2_nhwc<T, KS, STRIP>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL((dwconv2_nhwc<T, KS, STRIP>), dim3(grid), dim3(256), lds, s, (const T*)X, ldx, xm, stats, lg, lb,
+                     Wt, bias, (T*)Y, ldy, ym, B, H, W, C, band, nband, ncg, pitch);
+  return SDP_CHECK_LAUNCH();
+}
+
+template <typename T>
+static int dw2_dispatch(int k, const void* X, int64_t ldx, RowMap xm, const float* stats, const float* lg,
+                        const float* lb, const float* Wt, const float* bias, void* Y, int64_t ldy, RowMap ym, int B,
+                        int H, int W, int C, hipStream_t s) {
+#define SDP_DW2(KS) \
+  return (W % 8 == 0) ? launch_dw2<T, KS, 8>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s) \
+                      : launch_dw2<T, KS, 7>(X, ldx, xm, stats, lg, lb, Wt, bias, Y, ldy, ym, B, H, W, C, s)
+  switch (k) {
+    case 3: SDP_DW2(3);
+    case 5: SDP_DW2(5);
+    case 7: SDP_DW2(7);
+    default: return -1;
+  }
+#undef SDP_DW2
+}
+
+// 2 (default) = dwconv2_nhwc where it applies, 1 = dwconv_ln_nhwc
+static int g_dw_kernel = 2;
+extern "C" int sdp_dwconv_set_kernel(int k) {
+  const int old = g_dw_kernel;
+  if (k == 1 || k == 2) g_dw_kernel = k;
+  return old;
+}
+
 extern "C" int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
                           const float* stats, const float* ln_gamma, const float* ln_beta, const float* weight,
                           const float* bias, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int B,
@@ -512,6 +713,13 @@ extern "C" int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int6
   if ((x_grp > 0 && x_grp % (H * W)) || (y_grp > 0 && y_grp % (H * W))) return (int)hipErrorInvalidValue;
   const RowMap xm = mk_rmap(x_grp, x_gstride, x_off), ym = mk_rmap(y_grp, y_gstride, y_off);
   hipStream_t s = (hipStream_t)stream;
+  const bool v16 = ((ldx * esz) % 16 == 0) && ((uintptr_t)X % 16 == 0) && ((ldy * esz) % 16 == 0) &&
+                   ((uintptr_t)Y % 16 == 0) && (!stats || ((uintptr_t)stats % 8 == 0));
+  if (g_dw_kernel == 2 && C % 8 == 0 && v16 && (k == 3 || k == 5 || k == 7)) {
+    const int rc = dtype == 1 ? dw2_dispatch<bf16_t>(k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s)
+                              : dw2_dispatch<float>(k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s);
+    if (rc != -1) return rc;  // -1: image too wide for the dw2 LDS band -> original kernel
+  }
   if (dtype == 1) return dw_dispatch<bf16_t>(k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s);
   if (dtype == 0) return dw_dispatch<float>(k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s);
   return (int)hipErrorInvalidValue;

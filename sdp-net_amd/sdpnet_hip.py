@@ -40,6 +40,7 @@ _SIGS = {
     "sdp_rowstats": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _i32, _i32, _vp], _i32),
     "sdp_dwconv": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _i32,
                     _i32, _i32, _vp], _i32),
+    "sdp_dwconv_set_kernel": ([_i32], _i32),
     "sdp_attention": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _i64,
                        _i64, _vp], _i32),
     "sdp_attention_variant": ([_i32, _i32, _i32, _i32, _i32], _i32),
@@ -87,6 +88,9 @@ def lib():
         kern = os.environ.get("SDPNET_GEMM_KERNEL")  # A/B switch for the bf16 fast GEMM (benchmarks)
         if kern:
             L.sdp_gemm_set_fast_kernel(int(kern))
+        kern = os.environ.get("SDPNET_DW_KERNEL")  # A/B switch for the depthwise conv
+        if kern:
+            L.sdp_dwconv_set_kernel(int(kern))
         kern = os.environ.get("SDPNET_ATTN_KERNEL")  # A/B switch for the bf16 flash attention
         if kern:
             L.sdp_attention_set_kernel(int(kern))

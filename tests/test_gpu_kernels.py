@@ -167,7 +167,8 @@ def test_qk_headnorm(dtype, H, hd):
                                        (1, 20, 37, 36, 9), (2, 3, 3, 8, 1)])
 @pytest.mark.parametrize("bias", [False, True])
 @pytest.mark.parametrize("ln", [False, True])
-def test_dwconv(dtype, B, H, W, C, k, bias, ln):
+@pytest.mark.parametrize("kern", [1, 2])
+def test_dwconv(dtype, B, H, W, C, k, bias, ln, kern):
     x = rnd(B, C, H, W, dtype=dtype, seed=30, scale=2.0) + 0.5
     w = rnd(C, 1, k, k, seed=31, scale=0.2)
     b = rnd(C, seed=32) if bias else None
@@ -183,7 +184,11 @@ def test_dwconv(dtype, B, H, W, C, k, bias, ln):
         close(stats, ref_stats, torch.float32, rel=1e-5, what="rowstats")
         kw = dict(stats=stats, ln_gamma=g, ln_beta=be)
         xin = F.layer_norm(rows.float(), (C,), g, be, 1e-6).view(B, H, W, C).permute(0, 3, 1, 2)
-    sp.dwconv(sp.dense(rows), w.view(C, k * k).contiguous(), b, sp.dense(y), B, H, W, C, k, **kw)
+    old = sp.lib().sdp_dwconv_set_kernel(kern)
+    try:
+        sp.dwconv(sp.dense(rows), w.view(C, k * k).contiguous(), b, sp.dense(y), B, H, W, C, k, **kw)
+    finally:
+        sp.lib().sdp_dwconv_set_kernel(old)
     ref = F.conv2d(xin, w, b, padding="same", groups=C).permute(0, 2, 3, 1).reshape(B * H * W, C)
     close(y, ref, dtype, what="dwconv")
 

@@ -45,9 +45,12 @@ def main():
         w = torch.randn(C, 49, device=dev) * 0.1
         g, be = torch.ones(C, device=dev), torch.zeros(C, device=dev)
         y = torch.empty(B * P, C, device=dev, dtype=bf)
-        us = timeit(lambda: sp.dwconv(img, w, None, sp.dense(y), B, H, W, C, 7, stats=stats, ln_gamma=g, ln_beta=be),
-                    args.reps)
-        print(f"dwconv_ln  {us:8.1f} us  {2 * B * P * C * 2 / us / 1e3:7.1f} GB/s (read+write)")
+        for kern in (1, 2):
+            old = sp.lib().sdp_dwconv_set_kernel(kern)
+            us = timeit(lambda: sp.dwconv(img, w, None, sp.dense(y), B, H, W, C, 7, stats=stats, ln_gamma=g,
+                                          ln_beta=be), args.reps)
+            sp.lib().sdp_dwconv_set_kernel(old)
+            print(f"dwconv_ln k{kern} {us:8.1f} us  {2 * B * P * C * 2 / us / 1e3:7.1f} GB/s (read+write)")
     if "ln" in only:
         g, be = torch.ones(C, device=dev), torch.zeros(C, device=dev)
         y = torch.empty(B * N, C, device=dev, dtype=bf)
