@@ -50,6 +50,23 @@ int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride
              int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
              int64_t y_gstride, int y_off, int M, int N, int K, int act, int resid_pre,
              void* stream);
+/*
+ * sdp_gemm with a LayerNorm folded in and/or the output rows' LayerNorm
+ * statistics emitted (replaces nn.LayerNorm / channel LayerNorm + the following
+ * Linear / 1x1 conv: layers.py:12-24 -> :83-88, :280 -> :282-284, :307 -> :308).
+ *   ln_stats (float2 per logical row of X: mean, rstd) and ln_colsum ([N], 16-B
+ *   aligned) together, or both NULL: W holds W_orig * gamma (per input column),
+ *   bias holds beta . W_orig^T (+ the Linear bias), ln_colsum[n] = sum_k W[n][k];
+ *   the epilogue computes rstd * acc - rstd * mean * ln_colsum[n] + bias[n]
+ *   before activation / residual.
+ *   part != NULL: part[(phys_out_row * ceil(N/64) + c) * 2 + {0,1}] = {mean, M2}
+ *   of the stored output row's columns [64c, 64c+64) (combine with sdp_ln_stats).
+ */
+int sdp_gemm_ln(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+                int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
+                int64_t y_gstride, int y_off, int M, int N, int K, int act, int resid_pre,
+                const float* ln_stats, const float* ln_colsum, float* part, void* stream);
 /* Which kernel sdp_gemm picks for a shape: 1 = 256x256 MFMA, 0 = generic. */
 int sdp_gemm_variant(int dtype, int M, int N, int K);
 /* Test hook: force the generic kernel (returns the previous setting). */
@@ -63,6 +80,17 @@ int sdp_gemm_force_generic(int on);
  * no-store timing probes of 3 / 9 (benchmarks only: wrong results).  Any other
  * value leaves the selection unchanged.  Returns the previous selection. */
 int sdp_gemm_set_fast_kernel(int k);
+
+/*
+ * LayerNorm statistics by parts: sdp_row_partials writes {mean, M2} of every
+ * 64-column chunk of the logical rows of X to part[(phys_row * ceil(C/64) + c) * 2];
+ * sdp_ln_stats combines a row's chunks exactly (pairwise mean / M2 update) into
+ * stats[m] = (mean, 1 / sqrt(M2 / C + eps)) for logical row m of the given map.
+ */
+int sdp_row_partials(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                     int M, int C, float* part, void* stream);
+int sdp_ln_stats(const float* part, int x_grp, int64_t x_gstride, int x_off, int M, int C, float eps,
+                 float* stats, void* stream);
 
 /*
  * Row LayerNorm over C contiguous channels, fp32 statistics, biased variance.
@@ -169,6 +197,12 @@ int sdp_rows_to_nchw(int dtype_in, const void* X, int64_t ldx, int x_grp, int64_
 
 /* Element cast fp32 <-> bf16 (weight cache preparation, output conversion). */
 int sdp_cast(int dtype_in, const void* X, int dtype_out, void* Y, int64_t n, void* stream);
+/* LayerNorm folding of the Linear that consumes LN(x) (weight preparation for
+ * sdp_gemm_ln): Wf[n][k] = W[n][k] * gamma[k] (dtype_out), colsum[n] = sum_k Wf[n][k],
+ * cvec[n] = sum_k beta[k] * W[n][k] + bias[n] (bias may be NULL).  W, gamma, beta,
+ * bias fp32; W [N][K] row-major. */
+int sdp_fold_ln_weight(const float* W, const float* gamma, const float* beta, const float* bias, int N,
+                       int K, int dtype_out, void* Wf, float* colsum, float* cvec, void* stream);
 
 #ifdef __cplusplus
 }

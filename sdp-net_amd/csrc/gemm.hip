@@ -42,14 +42,30 @@ struct Epi {
   RowMap cmap;
   int act;
   int resid_pre;
+  // LayerNorm folded into this GEMM (W = W_orig * gamma, bias = beta . W_orig^T + b):
+  // v = rstd_m * acc - rstd_m * mean_m * lnsum[n] + bias[n], (mean, rstd) = lnst[m]
+  const float* lnst;   // float2 per logical row, or null
+  const float* lnsum;  // [N] column sums of the folded weight
+  // Per-row partial statistics of the stored outputs, 64-column chunks:
+  // part[(cmap(m) * (N/64) + n/64) * 2 + {0,1}] = {mean, M2} (whole-line epilogue only)
+  float* part;
 };
+
+// fold: v = r * acc + (b - r * mu * s) for one element (generic paths)
+SDP_DEV float ln_fold(float acc, float r, float rmu, float s, float b) { return fmaf(r, acc, fmaf(-rmu, s, b)); }
 
 // Apply the epilogue to 4 consecutive columns n..n+3 of logical row m.
 template <typename T>
 SDP_DEV void epi_store4(const Epi<T>& e, int64_t m, int n, int N, f32x4 acc) {
   float v[4] = {acc[0], acc[1], acc[2], acc[3]};
   const bool full = (n + 3 < N);
-  if (e.bias) {
+  if (e.lnst) {
+    const float2 st = *(const float2*)(e.lnst + 2 * m);
+    const float rmu = st.y * st.x;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (full || n + r < N) v[r] = ln_fold(v[r], st.y, rmu, e.lnsum[n + r], e.bias ? e.bias[n + r] : 0.f);
+  } else if (e.bias) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] += (full || n + r < N) ? e.bias[n + r] : 0.f;
   }
@@ -163,16 +179,23 @@ SDP_DEV void tile_epilogue(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, i
     }
     return;
   }
-  f32x4 bv[4];
+  f32x4 bv[4], sv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int n = n0 + wn * 64 + i * 16 + fq * 4;
     bv[i] = epi.bias ? *(const f32x4*)(epi.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    sv[i] = epi.lnst ? *(const f32x4*)(epi.lnsum + n) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int m = m0 + wm * 128 + j * 16 + fr;
     if (m >= M) continue;
+    float lr = 1.f, lrmu = 0.f;
+    if (epi.lnst) {
+      const float2 st = *(const float2*)(epi.lnst + 2 * (int64_t)m);
+      lr = st.y;
+      lrmu = st.y * st.x;
+    }
     const int nb = n0 + wn * 64 + fq * 4;
     bf16x4 rr[4];
     if (epi.resid) {
@@ -186,7 +209,7 @@ SDP_DEV void tile_epilogue(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, i
       bf16x4 o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = acc[i][j][r] + bv[i][r];
+        float v = epi.lnst ? ln_fold(acc[i][j][r], lr, lrmu, sv[i][r], bv[i][r]) : acc[i][j][r] + bv[i][r];
         if (epi.resid && epi.resid_pre) v += bf2f((bf16_t)rr[i][r]);
         v = epi_act<ACT>(epi.act, v);
         if (epi.resid && !epi.resid_pre) v += bf2f((bf16_t)rr[i][r]);
@@ -213,7 +236,7 @@ SDP_DEV void tile_epilogue16(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0,
     return;
   }
   const int cbase = n0 + wn * 64 + pair_col0(fq);
-  f32x4 bv[2][2];
+  f32x4 bv[2][2], sv[2][2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     if (epi.bias) {
@@ -221,6 +244,12 @@ SDP_DEV void tile_epilogue16(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0,
       bv[p][1] = *(const f32x4*)(epi.bias + cbase + 32 * p + 4);
     } else {
       bv[p][0] = bv[p][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (epi.lnst) {
+      sv[p][0] = *(const f32x4*)(epi.lnsum + cbase + 32 * p);
+      sv[p][1] = *(const f32x4*)(epi.lnsum + cbase + 32 * p + 4);
+    } else {
+      sv[p][0] = sv[p][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
   // Residual loads are issued JB row groups at a time (one 16-B load per lane per
@@ -246,6 +275,12 @@ SDP_DEV void tile_epilogue16(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0,
       if (!FULL && m >= M) continue;
       const bf16x8* rr = rres[jj];
       bf16_t* op = epi.out + epi.cmap(m) * epi.ldc + cbase;
+      float lr = 1.f, lrmu = 0.f;
+      if (epi.lnst) {
+        const float2 st = *(const float2*)(epi.lnst + 2 * (int64_t)m);
+        lr = st.y;
+        lrmu = st.y * st.x;
+      }
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         float v[8];
@@ -259,7 +294,8 @@ SDP_DEV void tile_epilogue16(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0,
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float x = v[e] + bv[p][e >> 2][e & 3];
+          float x = epi.lnst ? ln_fold(v[e], lr, lrmu, sv[p][e >> 2][e & 3], bv[p][e >> 2][e & 3])
+                             : v[e] + bv[p][e >> 2][e & 3];
           if (epi.resid && epi.resid_pre) x += bf2f((bf16_t)rr[p][e]);
           x = epi_act<ACT>(epi.act, x);
           if (epi.resid && !epi.resid_pre) x += bf2f((bf16_t)rr[p][e]);
@@ -287,15 +323,21 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
   // (host guarantees N % 8 == 0 and 16-B aligned rows), so a row's result never
   // depends on where the tile boundaries fall (batch invariance).
   const int cbase = n0 + wn * 64 + pair_col0(fq);
-  f32x4 bv[2][2];
+  f32x4 bv[2][2], sv[2][2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
+    const int c0 = min(cbase + 32 * p, N - 8);
     if (epi.bias) {
-      const int c0 = min(cbase + 32 * p, N - 8);
       bv[p][0] = *(const f32x4*)(epi.bias + c0);
       bv[p][1] = *(const f32x4*)(epi.bias + c0 + 4);
     } else {
       bv[p][0] = bv[p][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (epi.lnst) {
+      sv[p][0] = *(const f32x4*)(epi.lnsum + c0);
+      sv[p][1] = *(const f32x4*)(epi.lnsum + c0 + 4);
+    } else {
+      sv[p][0] = sv[p][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
   const int rlo = lane >> 3, ch = lane & 7;
@@ -318,6 +360,13 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
 #pragma unroll
     for (int jj = 0; jj < JB; ++jj) {
       const int j = j0 + jj;
+      f32x2 lr2 = {1.f, 1.f}, lm2 = {0.f, 0.f};  // rstd, -rstd * mean of this lane's row (MFMA layout)
+      if (epi.lnst) {
+        const int mrow = min(m0 + wm * 128 + j * 16 + fr, M - 1);
+        const float2 st = *(const float2*)(epi.lnst + 2 * (int64_t)mrow);
+        lr2 = f32x2{st.y, st.y};
+        lm2 = f32x2{-st.y * st.x, -st.y * st.x};
+      }
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         float v[8];
@@ -331,7 +380,14 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
-          f32x2 x2 = f32x2{v[e], v[e + 1]} + f32x2{bv[p][e >> 2][e & 3], bv[p][e >> 2][(e & 3) + 1]};
+          const f32x2 b2 = {bv[p][e >> 2][e & 3], bv[p][e >> 2][(e & 3) + 1]};
+          f32x2 x2;
+          if (epi.lnst) {  // r * acc + (b - r * mean * s)
+            const f32x2 s2 = {sv[p][e >> 2][e & 3], sv[p][e >> 2][(e & 3) + 1]};
+            x2 = f32x2{v[e], v[e + 1]} * lr2 + (s2 * lm2 + b2);
+          } else {
+            x2 = f32x2{v[e], v[e + 1]} + b2;
+          }
           if constexpr (ACT == ACT_GELU) {
             x2 = gelu_fast2(x2);
           } else {
@@ -353,6 +409,26 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
         }
         const int m = m0 + wm * 128 + j * 16 + r;
         if (m < M && col_ok) *(bf16x8*)(epi.out + epi.cmap(m) * epi.ldc + col) = o;
+        if (epi.part) {  // {mean, M2} of the row's 64 stored columns (8 lanes x 8)
+          float f[8], sum = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            f[e] = bf2f((bf16_t)o[e]);
+            sum += f[e];
+          }
+          sum += __shfl_xor(sum, 1, 64);
+          sum += __shfl_xor(sum, 2, 64);
+          sum += __shfl_xor(sum, 4, 64);
+          const float mean = sum * (1.0f / 64.0f);
+          float m2 = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m2 = fmaf(f[e] - mean, f[e] - mean, m2);
+          m2 += __shfl_xor(m2, 1, 64);
+          m2 += __shfl_xor(m2, 2, 64);
+          m2 += __shfl_xor(m2, 4, 64);
+          if (ch == 0 && m < M && col_ok)
+            *(float2*)(epi.part + (epi.cmap(m) * (N >> 6) + ((n0 + wn * 64) >> 6)) * 2) = float2{mean, m2};
+        }
       }
     }
   }
@@ -1203,19 +1279,53 @@ static int num_cus() {
   return n;
 }
 
+int sdp_row_partials(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, int M, int C,
+                     float* part, void* stream);
+
+static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                     const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+                     int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
+                     int64_t y_gstride, int y_off, int M, int N, int K, int act, int resid_pre,
+                     const float* ln_stats, const float* ln_colsum, float* part, bool* part_done, void* stream);
+
 extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
                         const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
                         int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
                         int64_t y_gstride, int y_off, int M, int N, int K, int act, int resid_pre,
                         void* stream) {
+  return gemm_impl(dtype, X, ldx, x_grp, x_gstride, x_off, W, ldw, bias, R, ldr, r_grp, r_gstride, r_off, Y, ldy,
+                   y_grp, y_gstride, y_off, M, N, K, act, resid_pre, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int sdp_gemm_ln(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                           const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+                           int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
+                           int64_t y_gstride, int y_off, int M, int N, int K, int act, int resid_pre,
+                           const float* ln_stats, const float* ln_colsum, float* part, void* stream) {
+  if ((ln_stats != nullptr) != (ln_colsum != nullptr)) return (int)hipErrorInvalidValue;
+  bool done = false;
+  const int rc = gemm_impl(dtype, X, ldx, x_grp, x_gstride, x_off, W, ldw, bias, R, ldr, r_grp, r_gstride, r_off, Y,
+                           ldy, y_grp, y_gstride, y_off, M, N, K, act, resid_pre, ln_stats, ln_colsum, part, &done,
+                           stream);
+  if (rc || !part || done || M == 0) return rc;
+  // the kernel taken could not emit the partials: compute them from the stored rows
+  return sdp_row_partials(dtype, Y, ldy, y_grp, y_gstride, y_off, M, N, part, stream);
+}
+
+static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                     const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+                     int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
+                     int64_t y_gstride, int y_off, int M, int N, int K, int act, int resid_pre,
+                     const float* ln_stats, const float* ln_colsum, float* part, bool* part_done, void* stream) {
   if (M < 0 || N <= 0 || K <= 0 || !X || !W || !Y) return (int)hipErrorInvalidValue;
   if (M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const RowMap xm = mk_map(x_grp, x_gstride, x_off);
   const RowMap rm = mk_map(r_grp, r_gstride, r_off);
   const RowMap ym = mk_map(y_grp, y_gstride, y_off);
+  if (ln_colsum && (uintptr_t)ln_colsum % 16) return (int)hipErrorInvalidValue;
   if (dtype == 1) {
-    Epi<bf16_t> e{bias, (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, act, resid_pre};
+    Epi<bf16_t> e{bias, (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, act, resid_pre, ln_stats, ln_colsum, nullptr};
     const bool aligned = (ldy % 4 == 0) && ((uintptr_t)Y % 8 == 0) && (!R || ((ldr % 4 == 0) && ((uintptr_t)R % 8 == 0))) &&
                          (!bias || ((uintptr_t)bias % 16 == 0)) && (ldx % 8 == 0) && ((uintptr_t)X % 16 == 0) &&
                          (ldw % 8 == 0) && ((uintptr_t)W % 16 == 0);
@@ -1266,6 +1376,10 @@ extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_
         return SDP_CHECK_LAUNCH();
       }
       if (fk == 12) {
+        if (part && N % 64 == 0) {  // the whole-line epilogue emits the row partial statistics
+          e.part = part;
+          if (part_done) *part_done = true;
+        }
 #define SDP_8PH(A) hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, 3>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
         if (act == ACT_NONE) SDP_8PH(ACT_NONE); else if (act == ACT_GELU) SDP_8PH(ACT_GELU); else SDP_8PH(-1);
@@ -1301,7 +1415,7 @@ extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_
                          (const bf16_t*)W, ldw, e, M, N, K);
     }
   } else if (dtype == 0) {
-    Epi<float> e{bias, (const float*)R, ldr, rm, (float*)Y, ldy, ym, act, resid_pre};
+    Epi<float> e{bias, (const float*)R, ldr, rm, (float*)Y, ldy, ym, act, resid_pre, ln_stats, ln_colsum, nullptr};
     dim3 grid((M + gen::BM - 1) / gen::BM, (N + gen::BN - 1) / gen::BN);
     hipLaunchKernelGGL(gen::gemm_generic<float>, grid, dim3(256), 0, s, (const float*)X, ldx, xm,
                        (const float*)W, ldw, e, M, N, K);

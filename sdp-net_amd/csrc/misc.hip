@@ -305,3 +305,52 @@ extern "C" int sdp_act(int dtype, const void* X, void* Y, int64_t n, int act, vo
 }
 
 extern "C" const char* sdp_version(void) { return "sdpnet-hip gfx950 r1"; }
+
+// ---------------------------------------------------------------------------
+// LayerNorm folding of a Linear / 1x1 conv that consumes LN(x) (layers.py:83-88
+// after :102-103's layer_norm_2, :282-284 after norm1, :308 after norm2):
+//   LN(x) . W^T + b = rstd * (x . (W*gamma)^T) - rstd * mean * colsum + (beta . W^T + b)
+// One workgroup per output row n: Wf[n][k] = cast(W[n][k] * gamma[k]),
+// colsum[n] = sum_k Wf[n][k] (of the stored, rounded values), cvec[n] = sum_k beta[k] W[n][k]
+// (+ bias[n]).  W, gamma, beta, bias fp32.  Run once per weight version.
+// ---------------------------------------------------------------------------
+template <typename TO>
+__global__ __launch_bounds__(256) void fold_ln_k(const float* __restrict__ W, const float* __restrict__ g,
+                                                 const float* __restrict__ be, const float* __restrict__ bias,
+                                                 TO* __restrict__ Wf, float* __restrict__ colsum,
+                                                 float* __restrict__ cvec, int K) {
+  const int n = blockIdx.x;
+  const float* w = W + (int64_t)n * K;
+  float s = 0.f, c = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const TO v = from_f<TO>(w[k] * g[k]);
+    Wf[(int64_t)n * K + k] = v;
+    s += to_f<TO>(v);
+    c = fmaf(be[k], w[k], c);
+  }
+  __shared__ float red[2][4];
+  s = wave_sum(s);
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s;
+    red[1][threadIdx.x >> 6] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    colsum[n] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    cvec[n] = red[1][0] + red[1][1] + red[1][2] + red[1][3] + (bias ? bias[n] : 0.f);
+  }
+}
+
+extern "C" int sdp_fold_ln_weight(const float* W, const float* gamma, const float* beta, const float* bias, int N,
+                                  int K, int dtype_out, void* Wf, float* colsum, float* cvec, void* stream) {
+  if (!W || !gamma || !beta || !Wf || !colsum || !cvec || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_out == 1)
+    hipLaunchKernelGGL(fold_ln_k<bf16_t>, dim3(N), dim3(256), 0, s, W, gamma, beta, bias, (bf16_t*)Wf, colsum, cvec, K);
+  else if (dtype_out == 0)
+    hipLaunchKernelGGL(fold_ln_k<float>, dim3(N), dim3(256), 0, s, W, gamma, beta, bias, (float*)Wf, colsum, cvec, K);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}

@@ -284,6 +284,92 @@ extern "C" int sdp_rowstats(int dtype, const void* X, int64_t ldx, int x_grp, in
 }
 
 // ---------------------------------------------------------------------------
+// LayerNorm statistics by parts.  A token row's LN statistics are carried as
+// per-64-column partials {mean, M2} (written by the producing GEMM's whole-line
+// epilogue, or by sdp_row_partials), combined exactly (Chan et al. pairwise
+// formula) by sdp_ln_stats into (mean, rstd) for the consumer: the LN-folded GEMM
+// or the depthwise conv.  Replaces the separate LayerNorm / row-statistics passes
+// over the token buffer (layers.py:12-24, :252-253).
+//   part[(phys_row * nch + c) * 2 + {0,1}] = {mean, M2} of columns [64c, 64c+64)
+//   (the last chunk may be shorter when C % 64 != 0), nch = ceil(C / 64).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void row_partials_k(const T* __restrict__ X, int64_t ldx, RowMap xm, int M, int C,
+                                                      float* __restrict__ part) {
+  // 8 lanes per 64-column chunk, 8 columns per lane
+  const int64_t g = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);  // (row, chunk) index
+  const int nch = (C + 63) / 64;
+  const int64_t row = g / nch;
+  const int c = (int)(g - row * nch);
+  const int sub = threadIdx.x & 7;
+  const bool ok = row < M;
+  const int64_t pr = ok ? xm(row) : 0;
+  const int col = c * 64 + sub * 8;
+  const int n = min(64, C - c * 64);
+  float f[8], sum = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    f[e] = (ok && col + e < C) ? to_f<T>(X[pr * ldx + col + e]) : 0.f;
+    sum += f[e];
+  }
+  sum += __shfl_xor(sum, 1, 64);
+  sum += __shfl_xor(sum, 2, 64);
+  sum += __shfl_xor(sum, 4, 64);
+  const float mean = sum / (float)n;
+  float m2 = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (col + e < C) m2 = fmaf(f[e] - mean, f[e] - mean, m2);
+  m2 += __shfl_xor(m2, 1, 64);
+  m2 += __shfl_xor(m2, 2, 64);
+  m2 += __shfl_xor(m2, 4, 64);
+  if (ok && sub == 0) *(float2*)(part + (pr * nch + c) * 2) = float2{mean, m2};
+}
+
+extern "C" int sdp_row_partials(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, int M,
+                                int C, float* part, void* stream) {
+  if (!X || !part || M < 0 || C <= 0) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  const RowMap xm = mk_rmap(x_grp, x_gstride, x_off);
+  const int64_t units = (int64_t)M * ((C + 63) / 64);
+  dim3 grid((unsigned)((units + 31) / 32)), blk(256);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 1) hipLaunchKernelGGL(row_partials_k<bf16_t>, grid, blk, 0, s, (const bf16_t*)X, ldx, xm, M, C, part);
+  else if (dtype == 0) hipLaunchKernelGGL(row_partials_k<float>, grid, blk, 0, s, (const float*)X, ldx, xm, M, C, part);
+  else return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// one thread per logical row: combine the nch partials of physical row xm(m)
+__global__ __launch_bounds__(256) void ln_stats_k(const float* __restrict__ part, RowMap xm, int M, int C, float eps,
+                                                  float* __restrict__ stats) {
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  const int nch = (C + 63) / 64;
+  const float* p = part + xm(m) * nch * 2;
+  float na = 0.f, mean = 0.f, m2 = 0.f;
+  for (int c = 0; c < nch; ++c) {
+    const float2 q = *(const float2*)(p + 2 * c);
+    const float nb = (float)min(64, C - c * 64);
+    const float n = na + nb;
+    const float d = q.x - mean;
+    mean = fmaf(d, nb / n, mean);
+    m2 += q.y + d * d * (na * nb / n);
+    na = n;
+  }
+  *(float2*)(stats + 2 * m) = float2{mean, rsqrtf(m2 / (float)C + eps)};
+}
+
+extern "C" int sdp_ln_stats(const float* part, int x_grp, int64_t x_gstride, int x_off, int M, int C, float eps,
+                            float* stats, void* stream) {
+  if (!part || !stats || M < 0 || C <= 0) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  const RowMap xm = mk_rmap(x_grp, x_gstride, x_off);
+  hipLaunchKernelGGL(ln_stats_k, dim3((M + 255) / 256), dim3(256), 0, (hipStream_t)stream, part, xm, M, C, eps, stats);
+  return SDP_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
 // Depthwise conv, NHWC token rows, with the channel LayerNorm applied on load.
 // X: pixel (b, h, w) at physical row xm(b*H*W + h*W + w).  Y: same with ym.
 // If stats != null the conv input is LN(x) = (x - mean) * rstd * g + be (the

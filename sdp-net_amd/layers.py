@@ -14,6 +14,7 @@ Module construction mirrors the reference order exactly, so the same
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional, Tuple
 
 import torch
@@ -30,6 +31,31 @@ Rows = sp.Rows
 
 def _dense(t: torch.Tensor) -> Rows:
     return Rows(t, t.shape[-1])
+
+
+# A/B switch (benchmarks): SDPNET_LN_FOLD=0 runs the LayerNorms as separate row-LN
+# kernels feeding unfolded GEMMs (the statistics still come from the partials).
+_LN_FOLD = os.environ.get("SDPNET_LN_FOLD", "1") != "0"
+
+
+def new_partials(rows: int, C: int, device) -> torch.Tensor:
+    """LayerNorm statistics by parts of a token buffer: [rows, ceil(C/64), 2] fp32
+    {mean, M2} per 64-column chunk of each physical row (sdp_row_partials /
+    sdp_gemm_ln write them, sdp_ln_stats combines them)."""
+    return torch.empty(rows, (C + 63) // 64, 2, dtype=torch.float32, device=device)
+
+
+def _ln_stats(part: torch.Tensor, rows: Rows, M: int, C: int, eps: float) -> torch.Tensor:
+    st = torch.empty(M, 2, dtype=torch.float32, device=part.device)
+    sp.ln_stats(part, rows, M, C, eps, st)
+    return st
+
+
+def _fold(w: torch.Tensor, ln: nn.Module, bias: Optional[torch.Tensor], dt):
+    """(W*gamma in dt, colsum, beta.W^T + b) of a Linear consuming LN(x)."""
+    g = ln.gamma if hasattr(ln, "gamma") else ln.weight
+    b = ln.beta if hasattr(ln, "beta") else ln.bias
+    return sp.fold_ln_weight(f32(w), f32(g), f32(b), f32(bias), dt)
 
 
 class LayerNorm(nn.Module):
@@ -92,8 +118,10 @@ class ConvPatcher(nn.Module):
             return wp
         return cached(self, "w", [self.conv.weight], dt, build)
 
-    def _run(self, img: torch.Tensor, dt, y: Rows, resid: Optional[Rows] = None, act: int = 0):
-        """img [B,3,Hi,Wi] -> y rows (logical row = b*P + ph*Wp + pw)."""
+    def _run(self, img: torch.Tensor, dt, y: Rows, resid: Optional[Rows] = None, act: int = 0,
+             part: Optional[torch.Tensor] = None):
+        """img [B,3,Hi,Wi] -> y rows (logical row = b*P + ph*Wp + pw); ``part``: token
+        LN partial statistics the output rows' are written to."""
         B, _, Hi, Wi = img.shape
         p = self.patch_size
         P = (Hi // p) * (Wi // p)
@@ -101,7 +129,7 @@ class ConvPatcher(nn.Module):
         patches = torch.empty(B * P, kp, dtype=dt, device=img.device)
         sp.patchify(img.contiguous(), patches, p, kp)
         w = self._weight(dt)
-        sp.gemm(_dense(patches), w, y, B * P, w.shape[0], kp, resid=resid, act=act, resid_pre=True)
+        sp.gemm(_dense(patches), w, y, B * P, w.shape[0], kp, resid=resid, act=act, resid_pre=True, part=part)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         dt = compute_dtype(x, self)
@@ -140,39 +168,54 @@ class ConvMixer(nn.Module):
 
     def _prep(self, dt):
         dw, cc, up, dn = self.conv2d[0], self.conv2d[1], self.conv1d[0], self.conv1d[2]
-        params = [dw.weight, dw.bias, cc.weight, cc.bias, up.weight, up.bias, dn.weight, dn.bias]
+        ln2 = self.layer_norm_2
+        params = [dw.weight, dw.bias, cc.weight, cc.bias, up.weight, up.bias, dn.weight, dn.bias,
+                  ln2.gamma, ln2.beta]
 
         def build():
             C = cc.out_channels
+            # layer_norm_2 folded into the up projection (sdp_gemm_ln)
+            up_w, up_s, up_c = _fold(up.weight.reshape(4 * C, C), ln2, up.bias, dt)
+            if not _LN_FOLD:
+                up_w, up_s, up_c = as_dtype(up.weight.reshape(4 * C, C), dt), None, f32(up.bias)
             return dict(
                 k=dw.kernel_size[0],
                 dw_w=f32(dw.weight.reshape(C, -1)), dw_b=f32(dw.bias),
                 cc_w=as_dtype(cc.weight.reshape(C, C), dt), cc_b=f32(cc.bias),
-                up_w=as_dtype(up.weight.reshape(4 * C, C), dt), up_b=f32(up.bias),
+                up_w=up_w, up_s=up_s, up_c=up_c,
                 dn_w=as_dtype(dn.weight.reshape(C, 4 * C), dt), dn_b=f32(dn.bias))
         return cached(self, "w", params, dt, build)
 
-    def _run_tokens(self, img: Rows, B: int, H: int, W: int, dt):
-        """In-place on the image rows ``img`` (logical row b*H*W + h*W + w)."""
+    def _run_tokens(self, img: Rows, B: int, H: int, W: int, dt, part: Optional[torch.Tensor] = None):
+        """In-place on the image rows ``img`` (logical row b*H*W + h*W + w).  ``part``:
+        the token buffer's LN partial statistics (current for these rows; kept
+        current on return); computed here when not given."""
         C = self.conv2d[1].out_channels
         M = B * H * W
         w = self._prep(dt)
         a = act_code(self.activation)
         dev = img.t.device
-        # LN1 fused into the depthwise conv: row stats, then normalise-on-load (layers.py:102)
-        stats = torch.empty(M, 2, dtype=torch.float32, device=dev)
-        sp.rowstats(img, self.layer_norm_1.eps, stats, M, C)
+        if part is None:
+            part = new_partials(img.t.shape[0], C, dev)
+            sp.row_partials(img, M, C, part)
+        # LN1 fused into the depthwise conv: (mean, rstd) from the partials, normalise-on-load (layers.py:102)
+        stats = _ln_stats(part, img, M, C, self.layer_norm_1.eps)
         g1, b1 = self.layer_norm_1._params()
         dwo = torch.empty(M, C, dtype=dt, device=dev)
         sp.dwconv(img, w["dw_w"], w["dw_b"], _dense(dwo), B, H, W, C, w["k"], stats=stats, ln_gamma=g1, ln_beta=b1)
-        ln = torch.empty(M, C, dtype=dt, device=dev)
-        # x_ = act(PW(DW(LN1 x)) + b) + x      (layers.py:102)
-        sp.gemm(_dense(dwo), w["cc_w"], img, M, C, C, bias=w["cc_b"], resid=img, act=a)
-        self.layer_norm_2._run_rows(img, _dense(ln), M)
+        # x_ = act(PW(DW(LN1 x)) + b) + x      (layers.py:102); emits x_'s LN partials
+        sp.gemm(_dense(dwo), w["cc_w"], img, M, C, C, bias=w["cc_b"], resid=img, act=a, part=part)
+        # hid = act(PW_up(LN2 x_) + b) with LN2 folded into the GEMM (layers.py:103)
         hid = torch.empty(M, 4 * C, dtype=dt, device=dev)
-        sp.gemm(_dense(ln), w["up_w"], _dense(hid), M, 4 * C, C, bias=w["up_b"], act=a)
-        # x = PW_down(hid) + b + x_             (layers.py:103)
-        sp.gemm(_dense(hid), w["dn_w"], img, M, C, 4 * C, bias=w["dn_b"], resid=img)
+        if _LN_FOLD:
+            stats2 = _ln_stats(part, img, M, C, self.layer_norm_2.eps)
+            sp.gemm(img, w["up_w"], _dense(hid), M, 4 * C, C, bias=w["up_c"], act=a, ln=(stats2, w["up_s"]))
+        else:
+            ln = torch.empty(M, C, dtype=dt, device=dev)
+            self.layer_norm_2._run_rows(img, _dense(ln), M)
+            sp.gemm(_dense(ln), w["up_w"], _dense(hid), M, 4 * C, C, bias=w["up_c"], act=a)
+        # x = PW_down(hid) + b + x_             (layers.py:103); emits x's LN partials
+        sp.gemm(_dense(hid), w["dn_w"], img, M, C, 4 * C, bias=w["dn_b"], resid=img, part=part)
 
     def forward(self, x: torch.Tensor):
         check_eval(self)
@@ -337,13 +380,19 @@ class EncoderLayer(nn.Module):
             params += [self.q_norm.weight, self.q_norm.bias, self.k_norm.weight, self.k_norm.bias]
 
         def build():
-            wqkv = torch.cat([as_dtype(self.q_proj.weight, dt), as_dtype(self.k_proj.weight, dt),
-                              as_dtype(self.v_proj.weight, dt)], 0).contiguous()
-            d = dict(wqkv=wqkv, wo=as_dtype(self.o_proj.weight, dt),
-                     w1=as_dtype(self.ff_linear1.weight, dt), b1=f32(self.ff_linear1.bias),
+            # norm1 folded into the fused QKV projection, norm2 into ff_linear1 (sdp_gemm_ln)
+            wqkv32 = torch.cat([f32(self.q_proj.weight), f32(self.k_proj.weight), f32(self.v_proj.weight)], 0)
+            wqkv, sqkv, cqkv = _fold(wqkv32.contiguous(), self.norm1, None, dt)
+            w1, s1, c1 = _fold(self.ff_linear1.weight, self.norm2, self.ff_linear1.bias, dt)
+            if not _LN_FOLD:
+                wqkv, sqkv, cqkv = as_dtype(wqkv32.contiguous(), dt), None, None
+                w1, s1, c1 = as_dtype(self.ff_linear1.weight, dt), None, f32(self.ff_linear1.bias)
+            d = dict(wqkv=wqkv, sqkv=sqkv, cqkv=cqkv, wo=as_dtype(self.o_proj.weight, dt),
+                     n1g=f32(self.norm1.weight), n1b=f32(self.norm1.bias),
+                     n2g=f32(self.norm2.weight), n2b=f32(self.norm2.bias),
+                     w1=w1, s1=s1, c1=c1,
                      w2=as_dtype(self.ff_linear2.weight, dt), b2=f32(self.ff_linear2.bias),
-                     n1g=f32(self.norm1.weight), n1b=f32(self.norm1.bias), n1e=self.norm1.eps,
-                     n2g=f32(self.norm2.weight), n2b=f32(self.norm2.bias), n2e=self.norm2.eps)
+                     n1e=self.norm1.eps, n2e=self.norm2.eps)
             if qn:
                 d.update(qg=f32(self.q_norm.weight), qb=f32(self.q_norm.bias), kg=f32(self.k_norm.weight),
                          kb=f32(self.k_norm.bias), qe=self.q_norm.eps)
@@ -366,16 +415,26 @@ class EncoderLayer(nn.Module):
             add = add.contiguous()
         return add, add.stride(0), add.stride(1)
 
-    def _run_tokens(self, tok: torch.Tensor, B: int, N: int, dt, mask: Optional[torch.Tensor] = None):
-        """In place on the dense token buffer ``tok`` [B*N, C] (registers first)."""
+    def _run_tokens(self, tok: torch.Tensor, B: int, N: int, dt, mask: Optional[torch.Tensor] = None,
+                    part: Optional[torch.Tensor] = None):
+        """In place on the dense token buffer ``tok`` [B*N, C] (registers first).
+        ``part``: its LN partial statistics (computed here when not given)."""
         C, Hn, hd = self.embedding_dim, self.n_head, self.head_dim
         T = B * N
         w = self._prep(dt)
         dev = tok.device
-        h = torch.empty(T, C, dtype=dt, device=dev)
-        sp.layernorm(_dense(tok), w["n1g"], w["n1b"], w["n1e"], _dense(h), T, C)            # :280
+        if part is None:
+            part = new_partials(T, C, dev)
+            sp.row_partials(_dense(tok), T, C, part)
+        # LN1 (:280) folded into the fused QKV projection (:282-284)
         qkv = torch.empty(T, 3 * C, dtype=dt, device=dev)
-        sp.gemm(_dense(h), w["wqkv"], _dense(qkv), T, 3 * C, C)                            # :282-284
+        if _LN_FOLD:
+            st1 = _ln_stats(part, _dense(tok), T, C, w["n1e"])
+            sp.gemm(_dense(tok), w["wqkv"], _dense(qkv), T, 3 * C, C, bias=w["cqkv"], ln=(st1, w["sqkv"]))
+        else:
+            h = torch.empty(T, C, dtype=dt, device=dev)
+            sp.layernorm(_dense(tok), w["n1g"], w["n1b"], w["n1e"], _dense(h), T, C)
+            sp.gemm(_dense(h), w["wqkv"], _dense(qkv), T, 3 * C, C)
         qkn = (w["qg"], w["qb"], w["kg"], w["kb"]) if "qg" in w else None                  # :286 (fused)
         att = torch.empty(T, C, dtype=dt, device=dev)
         if mask is not None:
@@ -383,12 +442,19 @@ class EncoderLayer(nn.Module):
             sp.attention(qkv, att, B, N, Hn, hd, mb, sb, sh, qk_norm=qkn, eps=w.get("qe", 1e-5))  # :289-298
         else:
             sp.attention(qkv, att, B, N, Hn, hd, qk_norm=qkn, eps=w.get("qe", 1e-5))
-        sp.gemm(_dense(att), w["wo"], _dense(tok), T, C, C, resid=_dense(tok))             # :300-303
-        sp.layernorm(_dense(tok), w["n2g"], w["n2b"], w["n2e"], _dense(h), T, C)            # :307
+        sp.gemm(_dense(att), w["wo"], _dense(tok), T, C, C, resid=_dense(tok), part=part)  # :300-303
+        # LN2 (:307) folded into ff_linear1 (:308)
         F_ = w["w1"].shape[0]
         f = torch.empty(T, F_, dtype=dt, device=dev)
-        sp.gemm(_dense(h), w["w1"], _dense(f), T, F_, C, bias=w["b1"], act=act_code(self.activation))
-        sp.gemm(_dense(f), w["w2"], _dense(tok), T, C, F_, bias=w["b2"], resid=_dense(tok))  # :308-309
+        if _LN_FOLD:
+            st2 = _ln_stats(part, _dense(tok), T, C, w["n2e"])
+            sp.gemm(_dense(tok), w["w1"], _dense(f), T, F_, C, bias=w["c1"], act=act_code(self.activation),
+                    ln=(st2, w["s1"]))
+        else:
+            h = torch.empty(T, C, dtype=dt, device=dev)
+            sp.layernorm(_dense(tok), w["n2g"], w["n2b"], w["n2e"], _dense(h), T, C)
+            sp.gemm(_dense(h), w["w1"], _dense(f), T, F_, C, bias=w["c1"], act=act_code(self.activation))
+        sp.gemm(_dense(f), w["w2"], _dense(tok), T, C, F_, bias=w["b2"], resid=_dense(tok), part=part)  # :308-309
 
     def forward(self, x: torch.Tensor, register: torch.Tensor, mask: torch.Tensor = None):
         check_eval(self)
@@ -442,17 +508,22 @@ class Block(nn.Module):
                                            for _ in range(conv_block_num)])
         self.conv_first = conv_first
 
-    def _run_tokens(self, tok: torch.Tensor, B: int, R: int, H: int, W: int, dt, mask=None):
+    def _run_tokens(self, tok: torch.Tensor, B: int, R: int, H: int, W: int, dt, mask=None,
+                    part: Optional[torch.Tensor] = None):
         N = R + H * W
-        img = Rows(tok, tok.shape[-1], H * W, N, R)
+        C = tok.shape[-1]
+        img = Rows(tok, C, H * W, N, R)
+        if part is None:
+            part = new_partials(B * N, C, tok.device)
+            sp.row_partials(_dense(tok), B * N, C, part)
         if not self.conv_first:
-            self.t_block._run_tokens(tok, B, N, dt, mask)
+            self.t_block._run_tokens(tok, B, N, dt, mask, part=part)
             for m in self.conv_blocks:
-                m._run_tokens(img, B, H, W, dt)
+                m._run_tokens(img, B, H, W, dt, part=part)
             return
         for m in self.conv_blocks:
-            m._run_tokens(img, B, H, W, dt)
-        self.t_block._run_tokens(tok, B, N, dt, mask)
+            m._run_tokens(img, B, H, W, dt, part=part)
+        self.t_block._run_tokens(tok, B, N, dt, mask, part=part)
 
     def forward(self, x: torch.Tensor, register: torch.Tensor, mask: torch.Tensor = None):
         check_eval(self)
@@ -481,8 +552,8 @@ class FinalBlock(nn.Module):
                                     multiplication_factor=multiplication_factor, ff_dropout=ff_dropout,
                                     att_dropout=att_dropout, normalize_qv=normalize_qv, drop_p=drop_p)
 
-    def _run_tokens(self, tok, B, R, H, W, dt, mask=None):
-        self.t_block._run_tokens(tok, B, R + H * W, dt, mask)
+    def _run_tokens(self, tok, B, R, H, W, dt, mask=None, part: Optional[torch.Tensor] = None):
+        self.t_block._run_tokens(tok, B, R + H * W, dt, mask, part=part)
 
     def forward(self, x: torch.Tensor, register: torch.Tensor, mask: torch.Tensor = None):
         return self.t_block(x, register, mask)

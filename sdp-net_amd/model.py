@@ -28,6 +28,7 @@ from numpy import arccos, cos
 import sdpnet_hip as sp
 from layers import ConvMixer, EmbeddingLayer, ConvPatcher, Block, FinalBlock, ClassificationHead, ConvEmbedding  # noqa: F401
 from utility_layers import SdPModel, StochasticDepth  # noqa: F401
+from layers import new_partials  # token-buffer plumbing of the fused path
 from sdpnet_engine import act_code, as_dtype, cached, check_eval, compute_dtype, hooked as _hooked
 from training_utilities import KeLu
 
@@ -188,13 +189,15 @@ class MainModel(SdPModel):
         img = Rows(tok, C, P, N, R)
         # patch GEMM + positional table (+ embedding activation) into the image rows
         # (layers.py:40-42, :157-168 / :205)
+        part = new_partials(B * N, C, x.device)  # LN statistics by parts of every token row
         self.conv_init._run(x, dt, img, resid=Rows(self._pos_rows(Hp, Wp, dt), C, P, 0, 0),
-                            act=act_code(emb.activation))
+                            act=act_code(emb.activation), part=part)
         if R:
             sp.copy_rows(table.contiguous(), C, 0, tok, C, N * C, B, R, C)
+            sp.row_partials(Rows(tok, C, R, N, 0), B * R, C, part)
         for block in self.blocks:                                     # model.py:139-140
-            block._run_tokens(tok, B, R, Hp, Wp, dt)
-        self.final_block._run_tokens(tok, B, R, Hp, Wp, dt)           # model.py:143
+            block._run_tokens(tok, B, R, Hp, Wp, dt, part=part)
+        self.final_block._run_tokens(tok, B, R, Hp, Wp, dt, part=part)  # model.py:143
         head = self.output_head                                       # model.py:146
         if head.from_register:
             head._run(Rows(tok, C, R, N, 0), B, R, C, dt, out=logits)

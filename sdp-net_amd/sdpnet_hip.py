@@ -14,7 +14,7 @@ from __future__ import annotations
 import ctypes
 import os
 from dataclasses import dataclass
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
@@ -32,12 +32,16 @@ _SIGS = {
     "sdp_version": ([], ctypes.c_char_p),
     "sdp_gemm": ([_i32, _vp, _i64, *_ROWMAP, _vp, _i64, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP,
                   _i32, _i32, _i32, _i32, _i32, _vp], _i32),
+    "sdp_gemm_ln": ([_i32, _vp, _i64, *_ROWMAP, _vp, _i64, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP,
+                     _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp], _i32),
     "sdp_gemm_variant": ([_i32, _i32, _i32, _i32], _i32),
     "sdp_gemm_force_generic": ([_i32], _i32),
     "sdp_gemm_set_fast_kernel": ([_i32], _i32),
     "sdp_layernorm": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _f32, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_qk_headnorm": ([_i32, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp], _i32),
     "sdp_rowstats": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _i32, _i32, _vp], _i32),
+    "sdp_row_partials": ([_i32, _vp, _i64, *_ROWMAP, _i32, _i32, _vp, _vp], _i32),
+    "sdp_ln_stats": ([_vp, *_ROWMAP, _i32, _i32, _f32, _vp, _vp], _i32),
     "sdp_dwconv": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _i32,
                     _i32, _i32, _vp], _i32),
     "sdp_dwconv_set_kernel": ([_i32], _i32),
@@ -55,6 +59,7 @@ _SIGS = {
     "sdp_nchw_to_rows": ([_i32, _vp, _i32, _vp, _i64, *_ROWMAP, _i32, _i32, _i32, _vp], _i32),
     "sdp_rows_to_nchw": ([_i32, _vp, _i64, *_ROWMAP, _i32, _vp, _i32, _i32, _i32, _vp], _i32),
     "sdp_cast": ([_i32, _vp, _i32, _vp, _i64, _vp], _i32),
+    "sdp_fold_ln_weight": ([_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp], _i32),
 }
 
 _lib = None
@@ -154,7 +159,12 @@ def dense(t: torch.Tensor) -> Rows:
 
 # ---------------------------------------------------------------------------
 def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Optional[torch.Tensor] = None,
-         resid: Optional[Rows] = None, act: int = 0, resid_pre: bool = False):
+         resid: Optional[Rows] = None, act: int = 0, resid_pre: bool = False,
+         ln: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, part: Optional[torch.Tensor] = None):
+    """y = epilogue(x . w^T).  ln = (stats [M,2] (mean, rstd) per logical row of x,
+    colsum [N] of the LN-folded weight): LayerNorm folded into the GEMM
+    (w = W * gamma, bias = beta . W^T + b).  part: token-row partial statistics
+    buffer [rows, ceil(N/64), 2] the output rows' {mean, M2} are written to."""
     _need_cuda(x.t, w, y.t, bias)
     dt = dcode(x.t.dtype)
     assert w.dtype == x.t.dtype == y.t.dtype and w.is_contiguous() and w.shape[0] >= N
@@ -168,8 +178,16 @@ def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Option
     if timer is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-    rc = lib().sdp_gemm(dt, *x.args(), w.data_ptr(), w.stride(0), _ptr(bias), *r, *y.args(), M, N, K, act,
-                        int(bool(resid_pre)), _stream(y.t))
+    if ln is None and part is None:
+        rc = lib().sdp_gemm(dt, *x.args(), w.data_ptr(), w.stride(0), _ptr(bias), *r, *y.args(), M, N, K, act,
+                            int(bool(resid_pre)), _stream(y.t))
+    else:
+        if ln is not None:
+            assert ln[0].dtype == ln[1].dtype == torch.float32 and ln[0].numel() >= 2 * M and ln[1].numel() >= N
+        assert part is None or part.dtype == torch.float32
+        rc = lib().sdp_gemm_ln(dt, *x.args(), w.data_ptr(), w.stride(0), _ptr(bias), *r, *y.args(), M, N, K, act,
+                               int(bool(resid_pre)), _ptr(ln[0]) if ln else None, _ptr(ln[1]) if ln else None,
+                               _ptr(part), _stream(y.t))
     _check(rc, "gemm")
     if timer is not None:
         e1.record()
@@ -192,6 +210,22 @@ def qk_headnorm(qkv: torch.Tensor, rows: int, n_head: int, head_dim: int, gq, bq
     rc = lib().sdp_qk_headnorm(dcode(qkv.dtype), qkv.data_ptr(), qkv.stride(0), rows, n_head, head_dim,
                                gq.data_ptr(), bq.data_ptr(), gk.data_ptr(), bk.data_ptr(), float(eps), _stream(qkv))
     _check(rc, "qk_headnorm")
+
+
+def row_partials(x: Rows, M: int, C: int, part: torch.Tensor):
+    """part[phys_row] = per-64-column {mean, M2} of the rows of x (LN statistics by parts)."""
+    _need_cuda(x.t, part)
+    assert part.dtype == torch.float32
+    rc = lib().sdp_row_partials(dcode(x.t.dtype), *x.args(), M, C, part.data_ptr(), _stream(part))
+    _check(rc, "row_partials")
+
+
+def ln_stats(part: torch.Tensor, rows: Rows, M: int, C: int, eps: float, stats: torch.Tensor):
+    """stats[m] = (mean, rstd) of logical row m of ``rows`` (its map over ``part``'s physical rows)."""
+    _need_cuda(part, stats)
+    assert part.dtype == stats.dtype == torch.float32 and stats.numel() >= 2 * M
+    rc = lib().sdp_ln_stats(part.data_ptr(), *rows.map(), M, C, float(eps), stats.data_ptr(), _stream(stats))
+    _check(rc, "ln_stats")
 
 
 def rowstats(x: Rows, eps: float, stats: torch.Tensor, M: int, C: int):
@@ -313,3 +347,20 @@ def gemm_variant(dtype: torch.dtype, M: int, N: int, K: int) -> int:
 
 def attention_variant(dtype: torch.dtype, N: int, n_head: int, head_dim: int, has_mask: bool = False) -> int:
     return lib().sdp_attention_variant(dcode(dtype), N, n_head, head_dim, int(has_mask))
+
+
+def fold_ln_weight(w: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, bias: Optional[torch.Tensor],
+                   dtype: torch.dtype):
+    """(W * gamma cast to dtype, colsum [N] fp32, beta . W^T + bias [N] fp32) for sdp_gemm_ln."""
+    _need_cuda(w, gamma, beta, bias)
+    assert w.dtype == gamma.dtype == beta.dtype == torch.float32 and w.is_contiguous() and w.dim() == 2
+    assert bias is None or (bias.dtype == torch.float32 and bias.is_contiguous())
+    N, K = w.shape
+    wf = torch.empty(N, K, dtype=dtype, device=w.device)
+    colsum = torch.empty(N, dtype=torch.float32, device=w.device)
+    cvec = torch.empty(N, dtype=torch.float32, device=w.device)
+    rc = lib().sdp_fold_ln_weight(w.data_ptr(), gamma.contiguous().data_ptr(), beta.contiguous().data_ptr(),
+                                  _ptr(bias), N, K, dcode(dtype), wf.data_ptr(), colsum.data_ptr(), cvec.data_ptr(),
+                                  _stream(w))
+    _check(rc, "fold_ln_weight")
+    return wf, colsum, cvec

@@ -371,3 +371,82 @@ def test_gemm_fast_kernel_variants(kern, M, N, K, act, res):
         sp.lib().sdp_gemm_set_fast_kernel(old)
     ref = ACTS[act](x.float() @ w.float().t() + b) + (r.float() if res else 0)
     close(y, ref, BF, what=f"kernel {kern}")
+
+
+# ------------------------------------------------- LayerNorm by parts / folded into the GEMM
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("M,C", [(300, 768), (77, 128), (5, 96), (1, 64), (130, 200)])
+def test_row_partials_and_ln_stats(dtype, M, C):
+    x = (rnd(M, C, seed=60, scale=1.5) + rnd(M, 1, seed=61, scale=3.0)).to(dtype)
+    nch = (C + 63) // 64
+    part = torch.full((M, nch, 2), float("nan"), device=DEV)
+    sp.row_partials(sp.dense(x), M, C, part)
+    xf = x.float()
+    for c in range(nch):
+        blk = xf[:, 64 * c: 64 * c + 64]
+        mu = blk.mean(1)
+        close(part[:, c, 0], mu, torch.float32, rel=1e-5, what="chunk mean")
+        close(part[:, c, 1], ((blk - mu[:, None]) ** 2).sum(1), torch.float32, rel=1e-5, what="chunk M2")
+    st = torch.empty(M, 2, device=DEV)
+    sp.ln_stats(part, sp.dense(x), M, C, 1e-6, st)
+    close(st[:, 0], xf.mean(1), torch.float32, rel=1e-5, what="mean")
+    close(st[:, 1], 1 / torch.sqrt(xf.var(1, unbiased=False) + 1e-6), torch.float32, rel=1e-4, what="rstd")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("kern", [9, 12])
+@pytest.mark.parametrize("M,N,K,act,has_b", [(600, 3072, 768, 1, False), (700, 768, 768, 0, True),
+                                             (513, 2304, 768, 0, False), (100, 200, 128, 1, True)])
+def test_gemm_ln_fold(dtype, kern, M, N, K, act, has_b):
+    """LN(x) . W^T + b computed as the folded GEMM (sdp_fold_ln_weight + sdp_gemm_ln)."""
+    x = (rnd(M, K, seed=62, scale=1.3) + rnd(M, 1, seed=63, scale=2.0)).to(dtype)
+    w = rnd(N, K, seed=64, scale=0.05)
+    g, be = rnd(K, seed=65) * 0.2 + 1, rnd(K, seed=66) * 0.2
+    b = rnd(N, seed=67) if has_b else None
+    part = torch.empty(M, (K + 63) // 64, 2, device=DEV)
+    sp.row_partials(sp.dense(x), M, K, part)
+    st = torch.empty(M, 2, device=DEV)
+    sp.ln_stats(part, sp.dense(x), M, K, 1e-5, st)
+    wf, colsum, cvec = sp.fold_ln_weight(w, g, be, b, dtype)
+    y = torch.empty(M, N, dtype=dtype, device=DEV)
+    old = sp.lib().sdp_gemm_set_fast_kernel(kern)
+    try:
+        sp.gemm(sp.dense(x), wf, sp.dense(y), M, N, K, bias=cvec, act=act, ln=(st, colsum))
+    finally:
+        sp.lib().sdp_gemm_set_fast_kernel(old)
+    ln = F.layer_norm(x.float(), (K,), g, be, 1e-5)
+    if dtype == BF:
+        ln = ln.to(BF).float()
+        w = w.to(BF).float()
+    ref = ACTS[act](ln @ w.t() + (b if b is not None else 0))
+    close(y, ref, dtype, rel=2e-5 if dtype == torch.float32 else 2e-2, what=f"ln-folded gemm kern {kern}")
+
+
+@pytest.mark.parametrize("kern", [9, 12])
+@pytest.mark.parametrize("M,N,K", [(600, 768, 768), (257, 768, 3072), (90, 128, 256), (70, 100, 64)])
+def test_gemm_emits_row_partials(kern, M, N, K):
+    """The residual GEMM's whole-line epilogue writes the output rows' LN partials
+    (other kernels: the library computes them after the GEMM), on a row-mapped output."""
+    B_, R = 2, 4
+    P = (M + B_ - 1) // B_
+    Mt = B_ * P
+    Nt = R + P
+    x = rnd(Mt, K, dtype=BF, seed=68)
+    w = rnd(N, K, dtype=BF, seed=69, scale=0.05)
+    tok = rnd(B_ * Nt, N, dtype=BF, seed=70)
+    img = sp.Rows(tok, N, P, Nt, R)
+    nch = (N + 63) // 64
+    part = torch.full((B_ * Nt, nch, 2), float("nan"), device=DEV)
+    old = sp.lib().sdp_gemm_set_fast_kernel(kern)
+    try:
+        sp.gemm(sp.dense(x), w, img, Mt, N, K, resid=img, act=1, part=part)
+    finally:
+        sp.lib().sdp_gemm_set_fast_kernel(old)
+    rows = tok.view(B_, Nt, N)[:, R:, :].reshape(Mt, N).float()
+    pr = part.view(B_, Nt, nch, 2)[:, R:].reshape(Mt, nch, 2)
+    for c in range(nch):
+        blk = rows[:, 64 * c: 64 * c + 64]
+        mu = blk.mean(1)
+        close(pr[:, c, 0], mu, torch.float32, rel=1e-5, what="emitted chunk mean")
+        close(pr[:, c, 1], ((blk - mu[:, None]) ** 2).sum(1), torch.float32, rel=1e-4, what="emitted chunk M2")
+    assert torch.isnan(part.view(B_, Nt, nch, 2)[:, :R]).all()  # register rows untouched
