@@ -777,11 +777,240 @@ static int dw2_dispatch(int k, const void* X, int64_t ldx, RowMap xm, const floa
 #undef SDP_DW2
 }
 
-// 2 (default) = dwconv2_nhwc where it applies, 1 = dwconv_ln_nhwc
-static int g_dw_kernel = 2;
+// ---------------------------------------------------------------------------
+// dwconv3_mfma — depthwise conv on the matrix cores (bf16, H, W <= 16,
+// W + KS - 1 <= 32, C % 32 == 0).  Per (image, channel) the conv is 16x16 D
+// tile (rows h, cols w) = sum over ky of A_ky (16 x 32) . B_ky (32 x 16):
+//   A_ky[h][q] = LN(x)[h + ky - PAD][q - PAD] (zero padded; q = padded column),
+//   B_ky[q][w] = W[c][ky][q - w] for 0 <= q - w < KS, else 0 (a Toeplitz band),
+// i.e. KS v_mfma_f32_16x16x32_bf16 per (image, channel).  B depends only on the
+// channel: each wave owns 2 channels and keeps their KS B fragments in registers
+// for all the images its persistent workgroup walks.
+// Workgroup = 32 channels (one 64-B half line per pixel; the other half is the
+// neighbouring workgroup on the same XCD, same image order) x a chunk of images,
+// 16 waves.  Per image: the 32 channel planes [22 rows][32 cols] bf16 are written
+// to LDS transposed from the NHWC rows (LN applied; the zero padding is written
+// once), the waves run their MFMAs, the D tiles go through an LDS [pixel][32]
+// image back to NHWC 64-B row stores.  The next image's loads are in flight
+// (registers) while the current one computes.
+// ---------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+SDP_DEV uint32_t pack_bf16x2(float a, float b) {
+  const bf16x2v v = __builtin_convertvector((f32x2){a, b}, bf16x2v);
+  return __builtin_bit_cast(uint32_t, v);
+}
+constexpr int DW3_CB = 32, DW3_ROWS = 22, DW3_RS = 32;
+constexpr int DW3_PLANE = DW3_ROWS * DW3_RS;  // elements per channel plane
+
+
+template <int KS, int NT, bool LN, int PF>
+__global__ __launch_bounds__(NT) void dwconv3_mfma(
+    const bf16_t* __restrict__ X, int64_t ldx, RowMap xm, const float* __restrict__ stats,
+    const float* __restrict__ lg, const float* __restrict__ lb, const float* __restrict__ Wt,
+    const float* __restrict__ bias, bf16_t* __restrict__ Y, int64_t ldy, RowMap ym, int B, int H, int W, int C,
+    int ncg, int ipb, int nunits) {
+  constexpr int PAD = KS / 2;
+  constexpr int CPW = DW3_CB / (NT / 64);  // channels per wave
+  constexpr int NIT = 1024 / NT;            // staging items per thread (256 pixels x 4 parts)
+  // channel plane cl at cl * DW3_PLANE + 16 * (cl >> 3): the +32 B skew per group of 8
+  // puts the 4 planes a staging instruction writes (channels 8q + e) on distinct banks
+  __shared__ __attribute__((aligned(16))) bf16_t planes[DW3_CB * DW3_PLANE + 48];  // 45,152 B
+  __shared__ __attribute__((aligned(16))) bf16_t outs[256 * DW3_CB];          // [pixel][32]  16,384 B
+  __shared__ __attribute__((aligned(16))) float lnp[2 * DW3_CB];              // gamma | beta of the block's channels
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // block -> (unit, half): blocks x and x+8 (same XCD) take the two 32-channel
+  // halves of one 64-channel group for the same images
+  const int xb = blockIdx.x, xcd = xb & 7, k = xb >> 3;
+  const int unit = xcd + 8 * (k >> 1), half = k & 1;
+  if (unit >= nunits) return;
+  const int cgp = unit % ((ncg + 1) / 2), chunk = unit / ((ncg + 1) / 2);
+  const int cg = 2 * cgp + half;
+  if (cg >= ncg) return;
+  const int c0 = cg * DW3_CB;
+  const int b0 = chunk * ipb, b1 = min(B, b0 + ipb);
+  if (b0 >= b1) return;
+  const int P = H * W;
+
+  // zero the planes once: the padding ring is never written again; the block's
+  // weights (bf16, zero-padded rows [KS][32] per channel) go to the outs buffer
+  for (int i = tid; i < (DW3_CB * DW3_PLANE + 48) / 8; i += NT) ((bf16x8*)planes)[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  if (LN && tid < 2 * DW3_CB) lnp[tid] = tid < DW3_CB ? lg[c0 + tid] : lb[c0 + tid - DW3_CB];
+  bf16_t* wl = outs;  // [32 ch][KS][32], tap kx at column kx + 16
+  for (int i = tid; i < DW3_CB * KS * 32; i += NT) {
+    const int cl = i / (KS * 32), r = i - cl * KS * 32, ky = r >> 5, col = r & 31;
+    const int kx = col - 16;
+    wl[i] = (kx >= 0 && kx < KS) ? f2bf(Wt[(int64_t)(c0 + cl) * KS * KS + ky * KS + kx]) : (bf16_t)0;
+  }
+  __syncthreads();
+  // B fragments of this wave's channels: lane (n = lane % 16, j = lane / 16) holds
+  // B_ky[8j + i][n] = W[c][ky][8j + i - n], i = 0..7 = row ky of the padded weights
+  // from column 8j - n + 16 (2-byte granular: assembled from halfword LDS reads)
+  const int n = lane & 15, j = lane >> 4;
+  bf16x8 bfr[CPW][KS];
+#pragma unroll
+  for (int cc = 0; cc < CPW; ++cc) {
+    const int cl = CPW * wave + cc;
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky) {
+      // padded row: tap t at column 16 + t, columns outside [16, 16+KS) hold zeros,
+      // so the window 16 + 8j - n + i (in [1, 47]) needs no masking: clamp into the row
+      const bf16_t* row = wl + (cl * KS + ky) * 32;
+      u32x4 o;
+#pragma unroll
+      for (int i = 0; i < 8; i += 2) {
+        const int c0i = min(16 + 8 * j - n + i, 31), c1i = min(16 + 8 * j - n + i + 1, 31);
+        o[i >> 1] = (uint32_t)row[c0i] | ((uint32_t)row[c1i] << 16);
+      }
+      bfr[cc][ky] = __builtin_bit_cast(bf16x8, o);
+      asm volatile("" : "+v"(bfr[cc][ky]));  // build the fragments one at a time
+    }
+  }
+  __syncthreads();  // weights consumed before outs is reused
+
+  // staging role: item t (2 per thread) -> pixel t / 4 (of up to 256), channels 8 * (t & 3) .. +7
+  auto load = [&](int b, int it, bf16x8& v, float2& st) {
+    const int t = tid + NT * it, pix = t >> 2, q = t & 3;
+    const int64_t local = (int64_t)b * P + (pix < P ? pix : 0);
+    v = *(const bf16x8*)(X + xm(local) * ldx + c0 + 8 * q);
+    if constexpr (LN) st = *(const float2*)(stats + 2 * local);
+  };
+  auto put = [&](int it, const bf16x8& v, const float2& st) {  // LN + transpose into the planes
+    const int t = tid + NT * it, pix = t >> 2, q = t & 3;
+    if (pix >= P) return;
+    const int h = pix / W, w = pix - (pix / W) * W;
+    bf16_t* dst = planes + (size_t)(8 * q) * DW3_PLANE + 16 * q + (h + PAD) * DW3_RS + (w + PAD);
+    if constexpr (LN) {  // gamma / beta from LDS (a global load here would drain the prefetch ring)
+      const f32x4 g0 = *(const f32x4*)(lnp + 8 * q), g1 = *(const f32x4*)(lnp + 8 * q + 4);
+      const f32x4 e0 = *(const f32x4*)(lnp + DW3_CB + 8 * q), e1 = *(const f32x4*)(lnp + DW3_CB + 8 * q + 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = (bf2f((bf16_t)v[e]) - st.x) * st.y;
+        dst[e * DW3_PLANE] = f2bf(e < 4 ? fmaf(x, g0[e], e0[e]) : fmaf(x, g1[e - 4], e1[e - 4]));
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dst[e * DW3_PLANE] = (bf16_t)v[e];
+    }
+  };
+  // PF images of loads in flight (HBM latency x bandwidth needs tens of KiB per CU):
+  // slot u of the register ring holds image b0 + u (mod PF); the loop is unrolled by
+  // PF so the ring index is static
+  float bch[CPW];
+#pragma unroll
+  for (int cc = 0; cc < CPW; ++cc) bch[cc] = bias ? bias[c0 + CPW * wave + cc] : 0.f;
+  bf16x8 pv[PF][NIT];
+  float2 ps[PF][NIT];
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) load(min(b0 + u, b1 - 1), it, pv[u][it], ps[u][it]);
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) put(it, pv[0][it], ps[0][it]);
+  for (int bb = b0; bb < b1; bb += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int b = bb + u;
+      if (b >= b1) break;  // uniform
+      __syncthreads();  // planes of image b complete
+      // slot u is free (image b is in the planes): refill it with image b + PF
+      // (unconditional, clamped to the last image: a static count of loads in flight lets
+      //  the compiler wait for exactly the slot it needs)
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) load(min(b + PF, b1 - 1), it, pv[u][it], ps[u][it]);
+#pragma unroll
+      for (int pp = 0; pp < CPW / 2; ++pp) {  // channel pairs: one packed dword per output pixel
+        f32x4 d[2];
+#pragma unroll
+        for (int c2 = 0; c2 < 2; ++c2) {
+          const int cc = 2 * pp + c2, cl = CPW * wave + cc;
+          const bf16_t* pl = planes + (size_t)cl * DW3_PLANE + 16 * (cl >> 3);
+          d[c2] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ky = 0; ky < KS; ++ky) {
+            const bf16x8 a = *(const bf16x8*)(pl + (n + ky) * DW3_RS + 8 * j);  // A_ky[h = n][8j ..]
+            d[c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[cc][ky], d[c2], 0, 0, 0);
+          }
+        }
+        // D[h = 4j + i][w = n] -> outs[pixel][32], 16-B chunk c of pixel p at c ^ ((p >> 2) & 3)
+        const int cl0 = CPW * wave + 2 * pp;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int h = 4 * j + i;
+          if (h < H && n < W) {
+            const int p = h * W + n;
+            *(uint32_t*)(outs + p * DW3_CB + (((cl0 >> 3) ^ ((p >> 2) & 3)) << 3) + (cl0 & 7)) =
+                pack_bf16x2(d[0][i] + bch[2 * pp], d[1][i] + bch[2 * pp + 1]);
+          }
+        }
+        asm volatile("" ::: "memory");  // one channel pair's A fragments live at a time
+      }
+      __syncthreads();  // outs complete; everyone done reading the planes
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int t = tid + NT * it, pix = t >> 2, q = t & 3;
+        if (pix < P) {
+          const int64_t local = (int64_t)b * P + pix;
+          *(bf16x8*)(Y + ym(local) * ldy + c0 + 8 * q) =
+              *(const bf16x8*)(outs + pix * DW3_CB + ((q ^ ((pix >> 2) & 3)) << 3));
+        }
+      }
+      if (b + 1 < b1) {
+        const int un = (u + 1) % PF;  // static after unrolling
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) put(it, pv[un][it], ps[un][it]);
+      }
+    }
+  }
+}
+
+static int launch_dw3(int variant, int k, const void* X, int64_t ldx, RowMap xm, const float* stats, const float* lg,
+                      const float* lb, const float* Wt, const float* bias, void* Y, int64_t ldy, RowMap ym, int B,
+                      int H, int W, int C, hipStream_t s) {
+  const int ncg = C / DW3_CB;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  const int npairs = (ncg + 1) / 2;
+  int nchunk = (ncu + ncg - 1) / ncg;  // about one workgroup per CU
+  if (nchunk > B) nchunk = B;
+  const int ipb = (B + nchunk - 1) / nchunk;
+  nchunk = (B + ipb - 1) / ipb;
+  const int nunits = npairs * nchunk;
+  const int grid = ((nunits + 7) / 8) * 16;
+#define SDP_DW3(KS, NT, PF)                                                                                    \
+  if (stats)                                                                                                     \
+    hipLaunchKernelGGL((dwconv3_mfma<KS, NT, true, PF>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx, xm,  \
+                       stats, lg, lb, Wt, bias, (bf16_t*)Y, ldy, ym, B, H, W, C, ncg, ipb, nunits);             \
+  else                                                                                                           \
+    hipLaunchKernelGGL((dwconv3_mfma<KS, NT, false, PF>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx, xm, \
+                       stats, lg, lb, Wt, bias, (bf16_t*)Y, ldy, ym, B, H, W, C, ncg, ipb, nunits)
+  // 16 waves x 2 channels, 3 images in flight (variant 3) or 8 waves x 4 channels, 4 in flight (4)
+  if (variant == 4) {
+    switch (k) {
+      case 3: SDP_DW3(3, 512, 4); break;
+      case 5: SDP_DW3(5, 512, 4); break;
+      case 7: SDP_DW3(7, 512, 4); break;
+      default: return -1;
+    }
+  } else {
+    switch (k) {
+      case 3: SDP_DW3(3, 1024, 3); break;
+      case 5: SDP_DW3(5, 1024, 3); break;
+      case 7: SDP_DW3(7, 1024, 3); break;
+      default: return -1;
+    }
+  }
+#undef SDP_DW3
+  return SDP_CHECK_LAUNCH();
+}
+
+// 3 (default) / 4 = dwconv3_mfma (16 waves x 2 channels / 8 waves x 4 channels) where it
+// applies, 2 = dwconv2_nhwc, 1 = dwconv_ln_nhwc
+static int g_dw_kernel = 3;
 extern "C" int sdp_dwconv_set_kernel(int k) {
   const int old = g_dw_kernel;
-  if (k == 1 || k == 2) g_dw_kernel = k;
+  if (k >= 1 && k <= 4) g_dw_kernel = k;
   return old;
 }
 
@@ -801,7 +1030,12 @@ extern "C" int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int6
   hipStream_t s = (hipStream_t)stream;
   const bool v16 = ((ldx * esz) % 16 == 0) && ((uintptr_t)X % 16 == 0) && ((ldy * esz) % 16 == 0) &&
                    ((uintptr_t)Y % 16 == 0) && (!stats || ((uintptr_t)stats % 8 == 0));
-  if (g_dw_kernel == 2 && C % 8 == 0 && v16 && (k == 3 || k == 5 || k == 7)) {
+  if (g_dw_kernel >= 3 && dtype == 1 && C % 32 == 0 && H <= 16 && W <= 16 && v16 && (k == 3 || k == 5 || k == 7) &&
+      ((uintptr_t)weight % 4 == 0)) {
+    const int rc = launch_dw3(g_dw_kernel, k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s);
+    if (rc != -1) return rc;
+  }
+  if (g_dw_kernel >= 2 && C % 8 == 0 && v16 && (k == 3 || k == 5 || k == 7)) {
     const int rc = dtype == 1 ? dw2_dispatch<bf16_t>(k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s)
                               : dw2_dispatch<float>(k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s);
     if (rc != -1) return rc;  // -1: image too wide for the dw2 LDS band -> original kernel

@@ -167,7 +167,7 @@ def test_qk_headnorm(dtype, H, hd):
                                        (1, 20, 37, 36, 9), (2, 3, 3, 8, 1)])
 @pytest.mark.parametrize("bias", [False, True])
 @pytest.mark.parametrize("ln", [False, True])
-@pytest.mark.parametrize("kern", [1, 2])
+@pytest.mark.parametrize("kern", [1, 2, 3, 4])
 def test_dwconv(dtype, B, H, W, C, k, bias, ln, kern):
     x = rnd(B, C, H, W, dtype=dtype, seed=30, scale=2.0) + 0.5
     w = rnd(C, 1, k, k, seed=31, scale=0.2)

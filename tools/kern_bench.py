@@ -45,7 +45,7 @@ def main():
         w = torch.randn(C, 49, device=dev) * 0.1
         g, be = torch.ones(C, device=dev), torch.zeros(C, device=dev)
         y = torch.empty(B * P, C, device=dev, dtype=bf)
-        for kern in (1, 2):
+        for kern in (1, 2, 3, 4):
             old = sp.lib().sdp_dwconv_set_kernel(kern)
             us = timeit(lambda: sp.dwconv(img, w, None, sp.dense(y), B, H, W, C, 7, stats=stats, ln_gamma=g,
                                           ln_beta=be), args.reps)
