@@ -81,6 +81,12 @@ int sdp_gemm_force_generic(int on);
  * value leaves the selection unchanged.  Returns the previous selection. */
 int sdp_gemm_set_fast_kernel(int k);
 
+/* First-round stagger of the 8-phase GEMM: in the first wave of blocks (one per CU),
+ * every other block of an XCD sleeps d x s_sleep(127) (~8k cycles each) before its
+ * prologue, so the CUs' epilogue store bursts stop coinciding.  0 = off.  Returns
+ * the previous value. */
+int sdp_gemm_set_desync(int d);
+
 /*
  * LayerNorm statistics by parts: sdp_row_partials writes {mean, M2} of every
  * 64-column chunk of the logical rows of X to part[(phys_row * ceil(C/64) + c) * 2];

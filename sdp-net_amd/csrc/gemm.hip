@@ -49,6 +49,10 @@ struct Epi {
   // Per-row partial statistics of the stored outputs, 64-column chunks:
   // part[(cmap(m) * (N/64) + n/64) * 2 + {0,1}] = {mean, M2} (whole-line epilogue only)
   float* part;
+  // first-round stagger (sdp_gemm_set_desync): blocks b < delay_blocks with (b >> 3) odd
+  // sleep `delay` x s_sleep(127) before their prologue
+  int delay = 0;
+  int delay_blocks = 0;
 };
 
 // fold: v = r * acc + (b - r * mu * s) for one element (generic paths)
@@ -619,6 +623,9 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   const int wm = wave >> 2, wn = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
   const int nk = K / BK;
+  if (epi.delay > 0 && b < epi.delay_blocks && ((b >> 3) & 1)) {
+    for (int i = 0; i < epi.delay; ++i) __builtin_amdgcn_s_sleep(127);
+  }
 
   // The wave's 8 DMA pieces per K-tile (8 rows x 128 B each): [0,1] S1-X,
   // [2,3] S1-W, [4,5] S2-W, [6,7] S3-X.  Source pointers advance by BK per tile.
@@ -1269,6 +1276,13 @@ extern "C" int sdp_gemm_set_fast_kernel(int k) {
   return old;
 }
 
+static int g_desync = 0;
+extern "C" int sdp_gemm_set_desync(int d) {
+  int old = g_desync;
+  g_desync = d < 0 ? 0 : d;
+  return old;
+}
+
 static int num_cus() {
   static int n = 0;
   if (n == 0) {
@@ -1326,6 +1340,8 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
   if (ln_colsum && (uintptr_t)ln_colsum % 16) return (int)hipErrorInvalidValue;
   if (dtype == 1) {
     Epi<bf16_t> e{bias, (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, act, resid_pre, ln_stats, ln_colsum, nullptr};
+    e.delay = g_desync;
+    e.delay_blocks = num_cus();
     const bool aligned = (ldy % 4 == 0) && ((uintptr_t)Y % 8 == 0) && (!R || ((ldr % 4 == 0) && ((uintptr_t)R % 8 == 0))) &&
                          (!bias || ((uintptr_t)bias % 16 == 0)) && (ldx % 8 == 0) && ((uintptr_t)X % 16 == 0) &&
                          (ldw % 8 == 0) && ((uintptr_t)W % 16 == 0);

@@ -26,6 +26,7 @@ from torch.nn import functional as F
 from numpy import arccos, cos
 
 import sdpnet_hip as sp
+import sdpnet_ops
 from layers import ConvMixer, EmbeddingLayer, ConvPatcher, Block, FinalBlock, ClassificationHead, ConvEmbedding  # noqa: F401
 from utility_layers import SdPModel, StochasticDepth  # noqa: F401
 from layers import new_partials  # token-buffer plumbing of the fused path
@@ -107,6 +108,12 @@ class MainModel(SdPModel):
                                               from_register=head_output_from_register,
                                               simple_output=simple_mlp_output, bias=output_head_bias)
         self.__init_weights__()
+        self._sdp_handle = sdpnet_ops.register(self)
+
+    def __setstate__(self, state):
+        # deep copies / unpickled models get their own custom-op handle
+        super().__setstate__(state)
+        self._sdp_handle = sdpnet_ops.register(self)
 
     def __init_weights__(self):
         for m in self.modules():
@@ -145,9 +152,18 @@ class MainModel(SdPModel):
 
     def forward(self, x: torch.Tensor, num_registers: int = 3, return_raw_outputs: bool = False):
         check_eval(self)
+        if torch.compiler.is_compiling():
+            # torch.compile (model_test.py:64, cifar100_test.py:93 fullgraph=True): the whole
+            # fused forward is one opaque custom op with a shape-only fake (sdpnet_ops.py)
+            code = sdpnet_ops.DTYPE_CODES[compute_dtype(x, self)]
+            if return_raw_outputs:
+                return torch.ops.sdpnet.main_forward_raw(x, self._sdp_handle, num_registers, code)
+            return torch.ops.sdpnet.main_forward(x, self._sdp_handle, num_registers, code)
         if _hooked(self):
             return self._forward_modules(x, num_registers, return_raw_outputs)
-        dt = compute_dtype(x, self)
+        return self._fused_forward(x, num_registers, compute_dtype(x, self), return_raw_outputs)
+
+    def _fused_forward(self, x: torch.Tensor, num_registers: int, dt, return_raw_outputs: bool):
         with torch.no_grad():
             B, _, Hi, Wi = x.shape
             p = self.conv_init.patch_size

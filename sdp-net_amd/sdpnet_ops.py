@@ -1,0 +1,89 @@
+"""torch.library registration of the fused MainModel forward.
+
+The reference's harnesses wrap the model in ``torch.compile`` -- ``model_test.py:64``,
+``training_tools.py:39`` (``dynamic=True``) and ``cifar100_test.py:93``
+(``fullgraph=True``).  The fused forward is a chain of ctypes launches into
+libsdpnet_hip.so that Dynamo cannot trace, so under compilation ``MainModel.forward``
+emits ONE opaque custom op per call instead:
+
+    sdpnet::main_forward(Tensor x, int handle, int num_registers, int dtype_code) -> Tensor
+    sdpnet::main_forward_raw(...) -> (Tensor logits, Tensor x_nchw, Tensor registers)
+
+``handle`` names the live MainModel in a process-local registry (weak references;
+a deep copy or unpickled copy registers itself anew, ``MainModel.__setstate__``).
+The fake (meta) implementations give the output shapes from the module structure
+alone, so ``fullgraph=True`` and ``dynamic=True`` trace with 0 graph breaks.  The
+real implementation is registered for the CUDA (ROCm) device type only: a CPU
+tensor reaching it raises instead of silently running some other path.
+"""
+from __future__ import annotations
+
+import itertools
+import weakref
+from typing import Tuple
+
+import torch
+from torch import Tensor
+
+from sdpnet_engine import num_reg_rows
+
+_MODELS: "dict[int, weakref.ref]" = {}
+_NEXT = itertools.count(1)
+
+DTYPE_CODES = {torch.float32: 0, torch.bfloat16: 1}
+_DTYPES = {v: k for k, v in DTYPE_CODES.items()}
+
+
+def register(model) -> int:
+    """Give ``model`` a fresh handle (called from MainModel.__init__ / __setstate__)."""
+    h = next(_NEXT)
+    _MODELS[h] = weakref.ref(model, lambda _r, h=h: _MODELS.pop(h, None))
+    return h
+
+
+def lookup(handle: int):
+    ref = _MODELS.get(int(handle))
+    model = ref() if ref is not None else None
+    if model is None:
+        raise RuntimeError(f"sdpnet: model handle {handle} is not live (the MainModel was freed)")
+    return model
+
+
+def _register_rows(model, num_registers: int) -> int:
+    emb = model.embedding_layer
+    n = emb.register.shape[0] if hasattr(emb, "register") else emb.max_num_registers
+    return num_reg_rows(n, num_registers)
+
+
+def _shapes(model, x: Tensor, num_registers: int):
+    B, _, Hi, Wi = x.shape
+    p = model.conv_init.patch_size
+    C = model.conv_init.conv.out_channels
+    lins = [m for m in model.output_head.output_head if isinstance(m, torch.nn.Linear)]
+    ncls = lins[-1].out_features
+    return B, C, Hi // p, Wi // p, ncls, _register_rows(model, num_registers)
+
+
+@torch.library.custom_op("sdpnet::main_forward", mutates_args=(), device_types="cuda")
+def main_forward(x: Tensor, handle: int, num_registers: int, dtype_code: int) -> Tensor:
+    return lookup(handle)._fused_forward(x, num_registers, _DTYPES[dtype_code], False)
+
+
+@main_forward.register_fake
+def _main_forward_fake(x, handle, num_registers, dtype_code):
+    B, C, Hp, Wp, ncls, R = _shapes(lookup(handle), x, num_registers)
+    return x.new_empty((B, ncls), dtype=_DTYPES[dtype_code])
+
+
+@torch.library.custom_op("sdpnet::main_forward_raw", mutates_args=(), device_types="cuda")
+def main_forward_raw(x: Tensor, handle: int, num_registers: int, dtype_code: int) -> Tuple[Tensor, Tensor, Tensor]:
+    logits, xo, regs = lookup(handle)._fused_forward(x, num_registers, _DTYPES[dtype_code], True)
+    return logits, xo, regs
+
+
+@main_forward_raw.register_fake
+def _main_forward_raw_fake(x, handle, num_registers, dtype_code):
+    B, C, Hp, Wp, ncls, R = _shapes(lookup(handle), x, num_registers)
+    dt = _DTYPES[dtype_code]
+    return (x.new_empty((B, ncls), dtype=dt), x.new_empty((B, C, Hp, Wp), dtype=dt),
+            x.new_empty((B, R, C), dtype=dt))

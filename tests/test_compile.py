@@ -1,0 +1,123 @@
+"""torch.compile surface of the drop-in MainModel (SURVEY.md §8(b) "harness
+behaviours to survive"): ``model_test.py:64`` compiles the model,
+``training_tools.py:39`` with ``dynamic=True``, ``cifar100_test.py:93`` with
+``fullgraph=True``.  Under compilation the fused forward is one custom op
+(``sdpnet::main_forward``, sdpnet_ops.py) with a shape-only fake.
+
+CPU tests trace with fake CUDA tensors (FakeTensorMode; no GPU or kernel runs):
+one graph, zero graph breaks, correct output shapes/dtypes.  The GPU test
+compiles for real and compares with the eager fused forward.
+"""
+import copy
+
+import pytest
+import torch
+from torch._subclasses.fake_tensor import FakeTensorMode
+
+import model as ours
+import sdpnet_ops
+
+XXS = dict(embedding_dim=64, num_blocks=2, n_head=4, patch_size=16, conv_kernel_size=7,
+           head_output_from_register=True, output_classes=10)
+
+
+def _model(**kw):
+    cfg = dict(XXS)
+    cfg.update(kw)
+    return ours.MainModel(**cfg).eval()
+
+
+def _export(m, x, **kw):
+    gm, _ = torch._dynamo.export(m, **kw)(x)
+    return gm
+
+
+def _sdp_nodes(gm):
+    return [n for n in gm.graph.nodes if n.op == "call_function" and "sdpnet" in str(n.target)]
+
+
+def test_fullgraph_single_custom_op():
+    m = _model()
+    with FakeTensorMode(allow_non_fake_inputs=True):
+        x = torch.empty(2, 3, 224, 224, device="cuda")
+        gm = _export(m, x)
+    nodes = _sdp_nodes(gm)
+    assert len(nodes) == 1 and nodes[0].target in (torch.ops.sdpnet.main_forward, torch.ops.sdpnet.main_forward.default)
+    calls = [n for n in gm.graph.nodes if n.op == "call_function"]
+    assert calls == nodes  # nothing else traced: the whole forward is the op
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_compiled_fake_shapes(dt):
+    torch._dynamo.reset()
+    m = _model()
+    graphs = []
+
+    def backend(gm, example_inputs):
+        graphs.append(gm)
+        return gm.forward
+
+    cm = torch.compile(m, fullgraph=True, dynamic=True, backend=backend)
+    with FakeTensorMode(allow_non_fake_inputs=True):
+        for B in (2, 5):
+            x = torch.empty(B, 3, 224, 224, device="cuda", dtype=dt)
+            y = cm(x)
+            assert tuple(y.shape) == (B, 10) and y.dtype == dt and y.is_cuda
+            logits, xo, regs = cm(x, return_raw_outputs=True)
+            assert tuple(logits.shape) == (B, 10)
+            assert tuple(xo.shape) == (B, 64, 14, 14) and xo.dtype == dt
+            assert tuple(regs.shape) == (B, 4, 64)  # num_registers=3 -> 4 rows (layers.py:157)
+            _, _, regs1 = cm(x, num_registers=1, return_raw_outputs=True)
+            assert tuple(regs1.shape) == (B, 2, 64)
+    # dynamic=True: one graph per (return_raw_outputs, num_registers) variant, reused across B
+    assert 1 <= len(graphs) <= 3
+    for gm in graphs:
+        assert len(_sdp_nodes(gm)) == 1
+
+
+@pytest.mark.gpu  # torch.autocast("cuda") disables itself without a device
+def test_autocast_selects_bf16_op():
+    m = _model()
+    with FakeTensorMode(allow_non_fake_inputs=True):
+        x = torch.empty(2, 3, 224, 224, device="cuda")
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            gm = _export(m, x)
+    (node,) = _sdp_nodes(gm)
+    assert node.args[3] == sdpnet_ops.DTYPE_CODES[torch.bfloat16]
+
+
+def test_handles_follow_copies():
+    m = _model()
+    m2 = copy.deepcopy(m)
+    assert m2._sdp_handle != m._sdp_handle
+    assert sdpnet_ops.lookup(m._sdp_handle) is m
+    assert sdpnet_ops.lookup(m2._sdp_handle) is m2
+    h = m2._sdp_handle
+    del m2
+    import gc
+    gc.collect()
+    with pytest.raises(RuntimeError, match="not live"):
+        sdpnet_ops.lookup(h)
+
+
+def test_op_has_no_cpu_kernel():
+    m = _model()
+    x = torch.zeros(1, 3, 224, 224)
+    with pytest.raises(NotImplementedError):
+        torch.ops.sdpnet.main_forward(x, m._sdp_handle, 3, 0)
+
+
+@pytest.mark.gpu
+def test_compiled_equals_eager_on_gpu():
+    torch.manual_seed(0)
+    m = _model().to("cuda")
+    x = torch.randn(3, 3, 224, 224, device="cuda")
+    ref = m(x)
+    torch._dynamo.reset()
+    cm = torch.compile(m, fullgraph=True)
+    y = cm(x)
+    torch.testing.assert_close(y, ref, rtol=0, atol=0)
+    ref_raw = m(x.bfloat16(), return_raw_outputs=True)
+    y_raw = cm(x.bfloat16(), return_raw_outputs=True)
+    for a, b in zip(y_raw, ref_raw):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
