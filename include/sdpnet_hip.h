@@ -211,6 +211,36 @@ int sdp_cast(int dtype_in, const void* X, int dtype_out, void* Y, int64_t n, voi
 int sdp_fold_ln_weight(const float* W, const float* gamma, const float* beta, const float* bias, int N,
                        int K, int dtype_out, void* Wf, float* colsum, float* cvec, void* stream);
 
+/* ---- Evaluation: either side of the forward path ---- */
+
+/* Validation transform of hf_dataset_generator.py:27-41 (val_transforms, used by
+ * model_test.py:50-52): RGB -> Resize((RH, RW), BICUBIC) -> CenterCrop((CH, CW)) ->
+ * ToDtype(float32, scale=True) -> Normalize(mean3, std3), on B decoded uint8 RGB HWC
+ * images of any sizes, bit-exact to Pillow 12.2.0's 8-bit resampler (the PIL path the
+ * reference's torchvision transforms take) up to the uint8 crop.
+ *   pix, offs[B] (int64 byte offsets), hw[B][2] (H, W): device; image b is
+ *   pix[offs[b] .. + H*W*3).  top/left: the crop origin inside the RH x RW resize
+ *   (torchvision: round((RH - CH) / 2), round((RW - CW) / 2)).
+ *   KMAX: the largest tap count over the batch, ceil(2 * max(1, In / Out)) * 2 + 1 over
+ *   both axes of every image (<= 160).  ws: B * (CW + CH) * (2 + KMAX) int32 of
+ *   device workspace; tmp: B * tmp_stride bytes, tmp_stride >= max_H * CW * 3.
+ *   out: [B][3][CH][CW] fp32 (dtype_out 0) or bf16 (1); out_u8 (optional, may be NULL):
+ *   the cropped uint8 HWC image [B][CH][CW][3].  mean3 / std3: host arrays. */
+int sdp_val_preprocess(const uint8_t* pix, const int64_t* offs, const int* hw, int B, int RH, int RW,
+                       int top, int left, int CH, int CW, int KMAX, const float* mean3, const float* std3,
+                       void* ws, uint8_t* tmp, int64_t tmp_stride, int dtype_out, void* out,
+                       uint8_t* out_u8, void* stream);
+
+/* Per-row evaluation metrics of run_test (model_test.py:69-82): for logits X [B][C]
+ * (row stride ld, fp32 or bf16) and int64 labels [B]:
+ *   out[3b] = logsumexp(X[b]) - X[b][label]     (nn.CrossEntropyLoss before the mean)
+ *   out[3b+1] = sum_j BCE-with-logits(X[b][j], onehot * (1 - ls) + ls / C)
+ *               (training_utilities.py:95-107 before the mean over B*C)
+ *   out[3b+2] = 1 if the first maximal index equals the label (outputs.argmax(1) == labels)
+ * A label outside [0, C) gives NaN. */
+int sdp_logits_metrics(int dtype, const void* X, int64_t ld, const int64_t* labels, int B, int C,
+                       float label_smoothing, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

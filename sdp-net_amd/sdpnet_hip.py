@@ -61,6 +61,9 @@ _SIGS = {
     "sdp_rows_to_nchw": ([_i32, _vp, _i64, *_ROWMAP, _i32, _vp, _i32, _i32, _i32, _vp], _i32),
     "sdp_cast": ([_i32, _vp, _i32, _vp, _i64, _vp], _i32),
     "sdp_fold_ln_weight": ([_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp], _i32),
+    "sdp_val_preprocess": ([_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
+                            _vp, _vp, _i64, _i32, _vp, _vp, _vp], _i32),
+    "sdp_logits_metrics": ([_i32, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp], _i32),
 }
 
 _lib = None
@@ -368,3 +371,37 @@ def fold_ln_weight(w: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, bia
                                   _stream(w))
     _check(rc, "fold_ln_weight")
     return wf, colsum, cvec
+
+
+def val_preprocess(pix: torch.Tensor, offs: torch.Tensor, hw: torch.Tensor, resize, crop, top: int, left: int,
+                   kmax: int, mean, std, tmp_stride: int, dtype: torch.dtype, want_u8: bool = False):
+    """Batched validation transform (sdp_val_preprocess); returns (out NCHW, out_u8 or None)."""
+    _need_cuda(pix, offs, hw)
+    assert pix.dtype == torch.uint8 and offs.dtype == torch.int64 and hw.dtype == torch.int32
+    B = hw.shape[0]
+    (RH, RW), (CH, CW) = resize, crop
+    dev = pix.device
+    ws = torch.empty(B * (CW + CH) * (2 + kmax), dtype=torch.int32, device=dev)
+    tmp = torch.empty(max(1, B * tmp_stride), dtype=torch.uint8, device=dev)
+    out = torch.empty(B, 3, CH, CW, dtype=dtype, device=dev)
+    u8 = torch.empty(B, CH, CW, 3, dtype=torch.uint8, device=dev) if want_u8 else None
+    m3 = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    s3 = (ctypes.c_float * 3)(*[float(v) for v in std])
+    rc = lib().sdp_val_preprocess(pix.data_ptr(), offs.data_ptr(), hw.data_ptr(), B, RH, RW, top, left, CH, CW,
+                                  kmax, m3, s3, ws.data_ptr(), tmp.data_ptr(), tmp_stride, dcode(dtype),
+                                  out.data_ptr(), _ptr(u8), _stream(out))
+    _check(rc, "val_preprocess")
+    return out, u8
+
+
+def logits_metrics(logits: torch.Tensor, labels: torch.Tensor, label_smoothing: float = 0.0) -> torch.Tensor:
+    """[B, 3] fp32: per-row cross-entropy, BCE-with-logits row sum, top-1 hit."""
+    _need_cuda(logits, labels)
+    assert logits.dim() == 2 and logits.stride(1) == 1 and labels.dtype == torch.int64
+    B, C = logits.shape
+    labels = labels.contiguous()
+    out = torch.empty(B, 3, dtype=torch.float32, device=logits.device)
+    rc = lib().sdp_logits_metrics(dcode(logits.dtype), logits.data_ptr(), logits.stride(0), labels.data_ptr(), B, C,
+                                  float(label_smoothing), out.data_ptr(), _stream(out))
+    _check(rc, "logits_metrics")
+    return out
