@@ -40,6 +40,17 @@ M_CFG = dict(embedding_dim=768, num_blocks=12, n_head=8, activation="gelu", embe
              conv_embedding=False, conv_embedding_kernel_size=5)
 
 
+# BASELINE.json configs[2]: SdP-Net-XL (17 blocks, d=768, patch 14, 256 patches + 4 registers)
+XL_CFG = dict(M_CFG, num_blocks=17, patch_size=14)
+CONFIGS = {
+    "m": dict(cfg=M_CFG, batch=256, name="SdP-Net-M", metric=METRIC,
+              desc="SdP-Net-M eval forward (12 blocks, d=768, patch 16, 200 tokens)"),
+    "xl": dict(cfg=XL_CFG, batch=512, name="SdP-Net-XL",
+               metric="images/sec fwd SdP-Net-XL 224×224 bs=512 @1 GPU (BASELINE.json configs[2])",
+               desc="SdP-Net-XL eval forward (17 blocks, d=768, patch 14, 260 tokens)"),
+}
+
+
 def flops_per_image(cfg, img=224, num_registers=3):
     """2*MAC over every conv (incl. depthwise), GEMM and attention QK^T + PV
     (M = 88.933 GF)."""
@@ -73,7 +84,7 @@ def measured_traffic(kernel):
     return None, None
 
 
-def cpu_baseline(model_cpu_sd, cfg, seconds=12.0):
+def cpu_baseline(model_cpu_sd, cfg, seconds=12.0, name="SdP-Net-M"):
     import torch
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import sdpnet_oracle as orc
@@ -91,7 +102,7 @@ def cpu_baseline(model_cpu_sd, cfg, seconds=12.0):
             break
     dt = time.perf_counter() - t0
     return {"value": round(n / dt, 3), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"SdP-Net-M fp32 eval forward, {n} images in batches of {bs}, {dt:.1f} s, "
+            "sample": f"{name} fp32 eval forward, {n} images in batches of {bs}, {dt:.1f} s, "
                       f"oracle/sdpnet_oracle.py (reference math, stock torch CPU ops)"}
 
 
@@ -100,12 +111,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="m",
+                    help="m = the BASELINE metric's workload (default); xl = configs[2]")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = the config's: M 256, XL 512)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prof-steps", type=int, default=2)
     ap.add_argument("--streams", type=int, default=0, help="sub-batch streams per GPU (0 = model default)")
     args = ap.parse_args()
+    C = CONFIGS[args.config]
+    cfg = C["cfg"]
+    if args.batch <= 0:
+        args.batch = C["batch"]
 
     import torch
     import torch.distributed as dist
@@ -123,7 +140,7 @@ def main():
     import sharding
 
     torch.manual_seed(231424314)  # model_train.py:61
-    m = sdp.MainModel.from_dict(**M_CFG).eval()
+    m = sdp.MainModel.from_dict(**cfg).eval()
     if args.streams > 0:
         m.num_streams = args.streams
     cpu_sd = {k: v.detach().clone() for k, v in m.state_dict().items()} if rank == 0 else None
@@ -204,12 +221,13 @@ def main():
             fast_n += len(lst)
     achieved = fast_fl / (fast_ms * 1e-3) / 1e12 if fast_ms else 0.0
     kname = FAST_GEMM_NAMES.get(sp.lib().sdp_gemm_set_fast_kernel(0), "?")
-    traffic, traffic_src = measured_traffic(kname)
+    traffic, traffic_src = measured_traffic(kname) if args.config == "m" else (None, None)
 
-    gf = flops_per_image(M_CFG) / 1e9
+    gf = flops_per_image(cfg) / 1e9
+    tokens = (224 // cfg["patch_size"]) ** 2 + min(4, cfg["max_num_registers"])
     value = total_imgs / el
     out = {
-        "metric": METRIC,
+        "metric": C["metric"],
         "value": round(value, 2),
         "unit": "images/sec",
         "n_gpus": world,
@@ -221,10 +239,9 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic N(0,1) 224x224 images resident in HBM; random-init weights (reference init)",
-        "config": {"workload": "SdP-Net-M eval forward (12 blocks, d=768, patch 16, 200 tokens), "
-                               "bf16 storage / fp32 accumulate, HIP-graph replay",
+        "config": {"workload": C["desc"] + ", bf16 storage / fp32 accumulate, HIP-graph replay",
                    "streams_per_gpu": m._num_streams(B),
-                   "global_batch": args.batch * world, "per_gpu_batch": B, "image": 224, "tokens": 200,
+                   "global_batch": args.batch * world, "per_gpu_batch": B, "image": 224, "tokens": tokens,
                    "parallelism": f"dp{world} independent batch shards (no collective)"},
         "model_flops_per_image_gf": round(gf, 3),
         "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
@@ -240,7 +257,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cpu_sd, M_CFG)
+        out["cpu_baseline"] = cpu_baseline(cpu_sd, cfg, name=C["name"])
         cb = out["cpu_baseline"]["value"]
         out["gpu_over_cpu"] = round(value / cb, 1) if cb else None
     if rank == 0:
