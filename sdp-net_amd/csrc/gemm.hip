@@ -684,13 +684,15 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) wf[i * 2 + ks] = lds_frag(wt, wn * 64 + in * 32 + i * 16 + fr, ks * 4 + fq);
   };
+  // ks outermost: the two K-halves of one accumulator are 8 MFMAs apart, so no MFMA
+  // waits on its predecessor's result (ks innermost made 8 dependent back-to-back pairs)
   auto quad = [&](int jm, int in, const bf16x8(&wf)[4]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
+        for (int j = 0; j < 4; ++j)
           acc[in * 2 + i][jm * 4 + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i * 2 + ks], xf[j * 2 + ks], acc[in * 2 + i][jm * 4 + j], 0, 0, 0);
   };
@@ -858,13 +860,15 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8php(const bf16_t* __restr
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) wf[i * 2 + ks] = lds_frag(wt, wn * 64 + in * 32 + i * 16 + fr, ks * 4 + fq);
   };
+  // ks outermost: the two K-halves of one accumulator are 8 MFMAs apart, so no MFMA
+  // waits on its predecessor's result (ks innermost made 8 dependent back-to-back pairs)
   auto quad = [&](int jm, int in, const bf16x8(&wf)[4]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
+        for (int j = 0; j < 4; ++j)
           acc[in * 2 + i][jm * 4 + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i * 2 + ks], xf[j * 2 + ks], acc[in * 2 + i][jm * 4 + j], 0, 0, 0);
   };

@@ -16,6 +16,17 @@ DEV = "cuda"
 BF = torch.bfloat16
 
 
+@pytest.fixture(autouse=True)
+def _full_precision_references():
+    """Importing model.py sets float32 matmul precision 'high' (reference model.py:9), which
+    lets torch's fp32 references use reduced-precision matmuls; the fp32 tolerances here
+    assume exact fp32 references, whatever test module imported model first."""
+    old = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    yield
+    torch.set_float32_matmul_precision(old)
+
+
 def rnd(*shape, dtype=torch.float32, seed=0, scale=1.0):
     g = torch.Generator(device="cpu").manual_seed(seed)
     return (torch.randn(*shape, generator=g) * scale).to(dtype).to(DEV)

@@ -16,6 +16,7 @@ for s in "$@"; do
   case $s in
     kern) step kern 900 python -m pytest tests/test_gpu_kernels.py -q -p no:cacheprovider -rf ;;
     model) step model 1200 python -m pytest tests/test_gpu_model.py -q -p no:cacheprovider -rf ;;
+    all) step all 1500 python -u -m pytest tests/ -m gpu -q -p no:cacheprovider -rf --timeout 240 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) step benchq 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
