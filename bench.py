@@ -30,7 +30,8 @@ sys.path.insert(0, os.path.join(REPO, "sdp-net_amd"))
 METRIC = "images/sec fwd SdP-Net-M 224×224 bs=256 @1 GPU; scaling 1/2/4/8"
 MFMA_BF16_PEAK_TFLOPS = 2516.6   # 256 CU x 2.4 GHz x 4096 FLOP/clk/CU (dense)
 FAST_GEMM_NAMES = {1: "gemm_bf16_256x256", 3: "gemm_bf16_256x256", 5: "gemm_bf16_deepx", 7: "gemm_bf16_256x128",
-                   8: "gemm_bf16_256x128i", 9: "gemm_bf16_8ph", 11: "gemm_bf16_8php", 12: "gemm_bf16_8ph", 13: "gemm_bf16_8php"}
+                   8: "gemm_bf16_256x128i", 9: "gemm_bf16_8ph", 11: "gemm_bf16_8php", 12: "gemm_bf16_8ph", 13: "gemm_bf16_8php",
+                   14: "gemm_bf16_8ph"}
 
 M_CFG = dict(embedding_dim=768, num_blocks=12, n_head=8, activation="gelu", embedding_activation="none",
              conv_kernel_size=7, patch_size=16, ffn_dropout=0.2, attn_dropout=0.2, output_classes=1000,

@@ -71,8 +71,9 @@ int sdp_gemm_ln(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstr
 int sdp_gemm_variant(int dtype, int M, int N, int K);
 /* Test hook: force the generic kernel (returns the previous setting). */
 int sdp_gemm_force_generic(int on);
-/* Select the bf16 fast kernel: 12 = 8-phase ping-pong 256x256x64 with the
- * whole-line (LDS-staged) epilogue (default); 9 = same with the direct epilogue;
+/* Select the bf16 fast kernel: 14 = 8-phase ping-pong 256x256x64 with the
+ * whole-line (LDS-staged) epilogue, all row groups staged before the first store
+ * (default); 12 = same staging one row group at a time; 9 = direct epilogue;
  * 11 / 13 = persistent forms of 9 / 12;
  * 1 = 256x256 tiles, 2-stage LDS ring, 8-byte stores; 3 = same with
  * permlane-paired 16-byte stores; 5 = 256x256, deep X ring (3 slots); 7 = 256x128
@@ -86,6 +87,10 @@ int sdp_gemm_set_fast_kernel(int k);
  * prologue, so the CUs' epilogue store bursts stop coinciding.  0 = off.  Returns
  * the previous value. */
 int sdp_gemm_set_desync(int d);
+
+/* Output store policy of the whole-line GEMM epilogue: 1 = non-temporal (streaming)
+ * stores, 0 = default.  Returns the previous value. */
+int sdp_gemm_set_store_policy(int nt);
 
 /*
  * LayerNorm statistics by parts: sdp_row_partials writes {mean, M2} of every

@@ -13,8 +13,8 @@
 // covers  act(conv)+x  (ConvMixer), x + FFN (+bias) (Encoder), pos-emb add +
 // embedding activation (EmbeddingLayer), Tanh (head).
 //
-// Kernels (bf16 fast path selected by sdp_gemm_set_fast_kernel, default 12):
-//  * gemm_bf16_8ph (9; 12 with tile_epilogue_rows) — the hot kernel: 256x256x64 tiles, 8 waves (2 along M x
+// Kernels (bf16 fast path selected by sdp_gemm_set_fast_kernel, default 14):
+//  * gemm_bf16_8ph (9; 12 / 14 with tile_epilogue_rows) — the hot kernel: 256x256x64 tiles, 8 waves (2 along M x
 //    4 along N, 128x64 per wave), v_mfma_f32_16x16x32_bf16, both operands staged
 //    HBM->LDS by global_load_lds_dwordx4 into an XOR-swizzled [row][64] image
 //    (conflict-free ds_read_b128), 4 phases per K-tile with the two wave groups
@@ -53,6 +53,7 @@ struct Epi {
   // sleep `delay` x s_sleep(127) before their prologue
   int delay = 0;
   int delay_blocks = 0;
+  int nt_store = 0;  // whole-line epilogue: non-temporal (streaming) output stores
 };
 
 // fold: v = r * acc + (b - r * mu * s) for one element (generic paths)
@@ -320,7 +321,7 @@ SDP_DEV void tile_epilogue16(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0,
 // (v = bf16(act(acc + b)) + R, rounded again), i.e. resid_pre = 0 semantics; the
 // caller routes resid_pre with an activation elsewhere.  Same-wave LDS accesses
 // execute in order, so the slot needs no barrier.
-template <int ACT, int JB = 4>
+template <int ACT, int JB = 4, bool ALL = false>
 SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int M, int N, int wm,
                                 int wn, int lane, int fr, int fq, char* stg) {
   // Ragged tiles take the same arithmetic with masked rows / 8-column chunks
@@ -349,6 +350,96 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
   const bool col_ok = col < N;
   const int lcol = col_ok ? col : N - 8;
   const int wchunk0 = ((fq & 1) << 1) | (fq >> 1);  // 16-B chunk of pair 0 (pair 1: +4)
+  // stage(j): row group j through the permlane pairing, bias / LN fold / activation, bf16
+  // pack, into its LDS slot; drain(j, rr): read the slot back in whole-line order, add the
+  // residual, store, emit the row partials.  ALL: every row group gets its own 2 KiB
+  // slot (stg spans 16 KiB per wave), all eight are staged before the first drain, so the
+  // wave pays one LDS round trip instead of eight and issues its 16 stores back to back.
+  auto slot = [&](int j) { return ALL ? stg + j * 2048 : stg; };
+  auto stage = [&](int j) {
+    char* sl = slot(j);
+    f32x2 lr2 = {1.f, 1.f}, lm2 = {0.f, 0.f};  // rstd, -rstd * mean of this lane's row (MFMA layout)
+    if (epi.lnst) {
+      const int mrow = min(m0 + wm * 128 + j * 16 + fr, M - 1);
+      const float2 st = *(const float2*)(epi.lnst + 2 * (int64_t)mrow);
+      lr2 = f32x2{st.y, st.y};
+      lm2 = f32x2{-st.y * st.x, -st.y * st.x};
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                   __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[4 + r] = __uint_as_float(sw[1]);
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const f32x2 b2 = {bv[p][e >> 2][e & 3], bv[p][e >> 2][(e & 3) + 1]};
+        f32x2 x2;
+        if (epi.lnst) {  // r * acc + (b - r * mean * s)
+          const f32x2 s2 = {sv[p][e >> 2][e & 3], sv[p][e >> 2][(e & 3) + 1]};
+          x2 = f32x2{v[e], v[e + 1]} * lr2 + (s2 * lm2 + b2);
+        } else {
+          x2 = f32x2{v[e], v[e + 1]} + b2;
+        }
+        if constexpr (ACT == ACT_GELU) {
+          x2 = gelu_fast2(x2);
+        } else {
+          x2.x = epi_act<ACT>(epi.act, x2.x);
+          x2.y = epi_act<ACT>(epi.act, x2.y);
+        }
+        o[e] = (short)f2bf(x2.x);
+        o[e + 1] = (short)f2bf(x2.y);
+      }
+      *(bf16x8*)(sl + fr * 128 + (((4 * p + wchunk0) ^ (fr & 7)) << 4)) = o;
+    }
+  };
+  auto drain = [&](int j, const bf16x8(&rr)[2]) {
+    const char* sl = slot(j);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = rlo + 8 * q;
+      bf16x8 o = *(const bf16x8*)(sl + r * 128 + ((ch ^ (r & 7)) << 4));
+      if (epi.resid) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(bf2f((bf16_t)o[e]) + bf2f((bf16_t)rr[q][e]));
+      }
+      const int m = m0 + wm * 128 + j * 16 + r;
+      if (m < M && col_ok) {
+        bf16x8* dst = (bf16x8*)(epi.out + epi.cmap(m) * epi.ldc + col);
+        if (epi.nt_store) __builtin_nontemporal_store(o, dst);
+        else *dst = o;
+      }
+      if (epi.part) {  // {mean, M2} of the row's 64 stored columns (8 lanes x 8)
+        float f[8], sum = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          f[e] = bf2f((bf16_t)o[e]);
+          sum += f[e];
+        }
+        sum += __shfl_xor(sum, 1, 64);
+        sum += __shfl_xor(sum, 2, 64);
+        sum += __shfl_xor(sum, 4, 64);
+        const float mean = sum * (1.0f / 64.0f);
+        float m2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m2 = fmaf(f[e] - mean, f[e] - mean, m2);
+        m2 += __shfl_xor(m2, 1, 64);
+        m2 += __shfl_xor(m2, 2, 64);
+        m2 += __shfl_xor(m2, 4, 64);
+        if (ch == 0 && m < M && col_ok)
+          *(float2*)(epi.part + (epi.cmap(m) * (N >> 6) + ((n0 + wn * 64) >> 6)) * 2) = float2{mean, m2};
+      }
+    }
+  };
+  if constexpr (ALL) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) stage(j);
+  }
 #pragma unroll
   for (int j0 = 0; j0 < 8; j0 += JB) {
     bf16x8 rres[JB][2];
@@ -363,77 +454,8 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
     }
 #pragma unroll
     for (int jj = 0; jj < JB; ++jj) {
-      const int j = j0 + jj;
-      f32x2 lr2 = {1.f, 1.f}, lm2 = {0.f, 0.f};  // rstd, -rstd * mean of this lane's row (MFMA layout)
-      if (epi.lnst) {
-        const int mrow = min(m0 + wm * 128 + j * 16 + fr, M - 1);
-        const float2 st = *(const float2*)(epi.lnst + 2 * (int64_t)mrow);
-        lr2 = f32x2{st.y, st.y};
-        lm2 = f32x2{-st.y * st.x, -st.y * st.x};
-      }
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        float v[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
-                                                     __float_as_uint(acc[2 * p + 1][j][r]), false, false);
-          v[r] = __uint_as_float(sw[0]);
-          v[4 + r] = __uint_as_float(sw[1]);
-        }
-        bf16x8 o;
-#pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-          const f32x2 b2 = {bv[p][e >> 2][e & 3], bv[p][e >> 2][(e & 3) + 1]};
-          f32x2 x2;
-          if (epi.lnst) {  // r * acc + (b - r * mean * s)
-            const f32x2 s2 = {sv[p][e >> 2][e & 3], sv[p][e >> 2][(e & 3) + 1]};
-            x2 = f32x2{v[e], v[e + 1]} * lr2 + (s2 * lm2 + b2);
-          } else {
-            x2 = f32x2{v[e], v[e + 1]} + b2;
-          }
-          if constexpr (ACT == ACT_GELU) {
-            x2 = gelu_fast2(x2);
-          } else {
-            x2.x = epi_act<ACT>(epi.act, x2.x);
-            x2.y = epi_act<ACT>(epi.act, x2.y);
-          }
-          o[e] = (short)f2bf(x2.x);
-          o[e + 1] = (short)f2bf(x2.y);
-        }
-        *(bf16x8*)(stg + fr * 128 + (((4 * p + wchunk0) ^ (fr & 7)) << 4)) = o;
-      }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int r = rlo + 8 * q;
-        bf16x8 o = *(const bf16x8*)(stg + r * 128 + ((ch ^ (r & 7)) << 4));
-        if (epi.resid) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(bf2f((bf16_t)o[e]) + bf2f((bf16_t)rres[jj][q][e]));
-        }
-        const int m = m0 + wm * 128 + j * 16 + r;
-        if (m < M && col_ok) *(bf16x8*)(epi.out + epi.cmap(m) * epi.ldc + col) = o;
-        if (epi.part) {  // {mean, M2} of the row's 64 stored columns (8 lanes x 8)
-          float f[8], sum = 0.f;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            f[e] = bf2f((bf16_t)o[e]);
-            sum += f[e];
-          }
-          sum += __shfl_xor(sum, 1, 64);
-          sum += __shfl_xor(sum, 2, 64);
-          sum += __shfl_xor(sum, 4, 64);
-          const float mean = sum * (1.0f / 64.0f);
-          float m2 = 0.f;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) m2 = fmaf(f[e] - mean, f[e] - mean, m2);
-          m2 += __shfl_xor(m2, 1, 64);
-          m2 += __shfl_xor(m2, 2, 64);
-          m2 += __shfl_xor(m2, 4, 64);
-          if (ch == 0 && m < M && col_ok)
-            *(float2*)(epi.part + (epi.cmap(m) * (N >> 6) + ((n0 + wn * 64) >> 6)) * 2) = float2{mean, m2};
-        }
-      }
+      if constexpr (!ALL) stage(j0 + jj);
+      drain(j0 + jj, rres[jj]);
     }
   }
 }
@@ -743,6 +765,11 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   if constexpr (EPI == 3) {  // whole-line epilogue through the (drained) LDS buffers; the
     // host routes resid_pre-with-activation and unaligned calls to EPI 1
     tile_epilogue_rows<ACT>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + wave * 2048);
+    return;
+  }
+  if constexpr (EPI == 4) {  // same, all eight row groups staged first (16 KiB per wave:
+    // both K buffers, free once the balancing barrier above has passed)
+    tile_epilogue_rows<ACT, 4, true>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + wave * 16384);
     return;
   }
   if constexpr (EPI == 2) {
@@ -1269,14 +1296,23 @@ extern "C" int sdp_gemm_force_generic(int on) {
 // bf16 fast-kernel selection: 1 = 2-stage ring + 8-B stores, 3 = 2-stage ring + paired
 // 16-B stores, 5 = deep-X ring (3 X slots, 2 W slots, counted vmcnt) + 16-B stores,
 // 7 = 256x128 tiles, 3-slot ring, two blocks per CU, 8 = same with interleaved DMA,
-// 9 = 8-phase ping-pong 256x256, 11 = persistent form of 9, 12 (default) / 13 = 9 / 11
+// 9 = 8-phase ping-pong 256x256, 11 = persistent form of 9, 12 / 13 = 9 / 11
 // with the whole-line LDS-staged epilogue,
+// 14 (default) = 12 with every row group staged before the first store (one LDS round
+// trip per wave; 9 % less single-stream GEMM time, equal in the two-stream model),
 // 4 / 10 = no-store timing probes of 3 / 9
 // (wrong results; benchmarks only).
-static int g_fast_kernel = 12;
+static int g_fast_kernel = 14;
 extern "C" int sdp_gemm_set_fast_kernel(int k) {
   int old = g_fast_kernel;
-  if (k == 1 || k == 3 || k == 4 || k == 5 || (k >= 7 && k <= 13)) g_fast_kernel = k;
+  if (k == 1 || k == 3 || k == 4 || k == 5 || (k >= 7 && k <= 14)) g_fast_kernel = k;
+  return old;
+}
+
+static int g_nt_store = 0;
+extern "C" int sdp_gemm_set_store_policy(int nt) {
+  int old = g_nt_store;
+  g_nt_store = nt ? 1 : 0;
   return old;
 }
 
@@ -1345,6 +1381,7 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
   if (dtype == 1) {
     Epi<bf16_t> e{bias, (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, act, resid_pre, ln_stats, ln_colsum, nullptr};
     e.delay = g_desync;
+    e.nt_store = g_nt_store;
     e.delay_blocks = num_cus();
     const bool aligned = (ldy % 4 == 0) && ((uintptr_t)Y % 8 == 0) && (!R || ((ldr % 4 == 0) && ((uintptr_t)R % 8 == 0))) &&
                          (!bias || ((uintptr_t)bias % 16 == 0)) && (ldx % 8 == 0) && ((uintptr_t)X % 16 == 0) &&
@@ -1378,7 +1415,8 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
       // and implements resid_pre only without an activation
       const bool rows_ok = (N % 8 == 0) && (ldy % 8 == 0) && ((uintptr_t)Y % 16 == 0) &&
                            (!R || ((ldr % 8 == 0) && ((uintptr_t)R % 16 == 0))) && !(R && resid_pre && act != ACT_NONE);
-      const int fk = (!rows_ok && g_fast_kernel == 12) ? 9 : (!rows_ok && g_fast_kernel == 13) ? 11 : g_fast_kernel;
+      const int fk = (!rows_ok && (g_fast_kernel == 12 || g_fast_kernel == 14)) ? 9
+                     : (!rows_ok && g_fast_kernel == 13) ? 11 : g_fast_kernel;
       // persistent form: epilogues GELU / none only (the runtime-activation variant
       // spills), 32-bit element offsets must cover both operands
       if ((fk == 11 || fk == 13) && (act == ACT_NONE || act == ACT_GELU) &&
@@ -1395,14 +1433,18 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
 #undef SDP_8PHP
         return SDP_CHECK_LAUNCH();
       }
-      if (fk == 12) {
+      if (fk == 12 || fk == 14) {
         if (part && N % 64 == 0) {  // the whole-line epilogue emits the row partial statistics
           e.part = part;
           if (part_done) *part_done = true;
         }
-#define SDP_8PH(A) hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, 3>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
-                                      (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
-        if (act == ACT_NONE) SDP_8PH(ACT_NONE); else if (act == ACT_GELU) SDP_8PH(ACT_GELU); else SDP_8PH(-1);
+#define SDP_8PH(A, E) hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
+                                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
+        if (fk == 14) {
+          if (act == ACT_NONE) SDP_8PH(ACT_NONE, 4); else if (act == ACT_GELU) SDP_8PH(ACT_GELU, 4); else SDP_8PH(-1, 4);
+        } else {
+          if (act == ACT_NONE) SDP_8PH(ACT_NONE, 3); else if (act == ACT_GELU) SDP_8PH(ACT_GELU, 3); else SDP_8PH(-1, 3);
+        }
 #undef SDP_8PH
         return SDP_CHECK_LAUNCH();
       }
