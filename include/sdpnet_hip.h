@@ -228,13 +228,15 @@ int sdp_fold_ln_weight(const float* W, const float* gamma, const float* beta, co
  *   (torchvision: round((RH - CH) / 2), round((RW - CW) / 2)).
  *   KMAX: the largest tap count over the batch, ceil(2 * max(1, In / Out)) * 2 + 1 over
  *   both axes of every image (<= 160).  ws: B * (CW + CH) * (2 + KMAX) int32 of
- *   device workspace; tmp: B * tmp_stride bytes, tmp_stride >= max_H * CW * 3.
+ *   device workspace; tmp: B * tmp_stride bytes, tmp_stride >= max_H * CW * 4 (the
+ *   horizontal pass's RGBX words).  max_w: the widest image of the batch (<= 40960; its
+ *   RGBX row is staged in LDS).
  *   out: [B][3][CH][CW] fp32 (dtype_out 0) or bf16 (1); out_u8 (optional, may be NULL):
  *   the cropped uint8 HWC image [B][CH][CW][3].  mean3 / std3: host arrays. */
 int sdp_val_preprocess(const uint8_t* pix, const int64_t* offs, const int* hw, int B, int RH, int RW,
                        int top, int left, int CH, int CW, int KMAX, const float* mean3, const float* std3,
-                       void* ws, uint8_t* tmp, int64_t tmp_stride, int dtype_out, void* out,
-                       uint8_t* out_u8, void* stream);
+                       void* ws, uint8_t* tmp, int64_t tmp_stride, int max_w, int dtype_out,
+                       void* out, uint8_t* out_u8, void* stream);
 
 /* Per-row evaluation metrics of run_test (model_test.py:69-82): for logits X [B][C]
  * (row stride ld, fp32 or bf16) and int64 labels [B]:

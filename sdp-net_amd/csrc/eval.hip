@@ -30,11 +30,15 @@ __device__ double bicubic(double x) {
 }
 
 // Workspace per image: for the CW cropped output columns then the CH cropped output
-// rows: bounds {first tap, tap count} and KMAX fixed-point taps.
+// rows: bounds {first tap, tap count} and KMAX fixed-point taps, tap-major so that the
+// lanes of a wave (consecutive output columns) read one tap with one coalesced load.
 struct Tab {
   int* bounds;  // [B][CW + CH][2]
-  int* coef;    // [B][CW + CH][KMAX]
+  int* coef;    // [B][KMAX][CW + CH]
 };
+SDP_DEV int64_t tap_at(int b, int x, int t, int CW, int CH, int KMAX) {
+  return ((int64_t)b * KMAX + x) * (CW + CH) + t;
+}
 
 __global__ void coef_k(const int* __restrict__ hw, int B, int RH, int RW, int top, int left, int CH, int CW, int KMAX,
                        Tab tab) {
@@ -59,7 +63,6 @@ __global__ void coef_k(const int* __restrict__ hw, int B, int RH, int RW, int to
   if (xmax > inSize) xmax = inSize;
   xmax -= xmin;
   if (xmax > KMAX) xmax = KMAX;  // host sizes KMAX to the largest ksize: never taken
-  int* kk = tab.coef + ((int64_t)b * (CW + CH) + t) * KMAX;
   const int n = xmax;
   double ww = 0.0;
   for (int x = 0; x < n; ++x) ww += bicubic((x + xmin - center + 0.5) * ss);
@@ -67,9 +70,9 @@ __global__ void coef_k(const int* __restrict__ hw, int B, int RH, int RW, int to
     double v = bicubic((x + xmin - center + 0.5) * ss);
     if (ww != 0.0) v /= ww;
     // normalize_coeffs_8bpc
-    kk[x] = v < 0 ? (int)(-0.5 + v * (1 << PREC)) : (int)(0.5 + v * (1 << PREC));
+    tab.coef[tap_at(b, x, t, CW, CH, KMAX)] = v < 0 ? (int)(-0.5 + v * (1 << PREC)) : (int)(0.5 + v * (1 << PREC));
   }
-  for (int x = n; x < KMAX; ++x) kk[x] = 0;
+  for (int x = n; x < KMAX; ++x) tab.coef[tap_at(b, x, t, CW, CH, KMAX)] = 0;
   int* bd = tab.bounds + ((int64_t)b * (CW + CH) + t) * 2;
   bd[0] = xmin;
   bd[1] = n;
@@ -92,44 +95,51 @@ SDP_DEV void rows_needed(const Tab& tab, int b, int CH, int CW, bool need_v, int
   y1 = bd[2 * (CW + CH - 1)] + bd[2 * (CW + CH - 1) + 1];
 }
 
-// Horizontal pass over the needed source rows, cropped columns only:
-// tmp[b][y][j][c], row stride CW * 3, image stride tmp_stride bytes.
-__global__ void hpass_k(const uint8_t* __restrict__ pix, const int64_t* __restrict__ offs, const int* __restrict__ hw,
-                        int RH, int RW, int top, int left, int CH, int CW, int KMAX, Tab tab, uint8_t* __restrict__ tmp,
-                        int64_t tmp_stride) {
+// Horizontal pass over the needed source rows, cropped columns only.  Each wave owns
+// one source row at a time: it stages the packed RGB row into its private LDS slot as
+// RGBX words (coalesced byte loads, ds_write_b8 into the padded slot; no workgroup
+// barrier, a wave's LDS accesses execute in order), then every output column reads
+// its taps as one 32-bit word each.  Output: tmp[b][y][j] RGBX uint32 (row stride CW
+// words, image stride tmp_stride bytes).
+__global__ __launch_bounds__(256) void hpass_k(const uint8_t* __restrict__ pix, const int64_t* __restrict__ offs,
+                                               const int* __restrict__ hw, int RH, int RW, int top, int left, int CH,
+                                               int CW, int KMAX, Tab tab, uint8_t* __restrict__ tmp,
+                                               int64_t tmp_stride, int max_w) {
+  extern __shared__ uint32_t lds_rows[];  // [waves][max_w] RGBX
   const int b = blockIdx.y;
   const int H = hw[2 * b], W = hw[2 * b + 1];
   const bool need_h = W != RW, need_v = H != RH;
   int y0, y1;
   rows_needed(tab, b, CH, CW, need_v, top, y0, y1);
   const uint8_t* img = pix + offs[b];
-  uint8_t* out = tmp + (int64_t)b * tmp_stride;
-  const int64_t total = (int64_t)(y1 - y0) * CW;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int y = y0 + (int)(idx / CW), j = (int)(idx % CW);
+  uint32_t* out = (uint32_t*)(tmp + (int64_t)b * tmp_stride);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t* srow = lds_rows + (int64_t)wave * max_w;
+  for (int y = y0 + blockIdx.x * nw + wave; y < y1; y += gridDim.x * nw) {
     const uint8_t* row = img + (int64_t)y * W * 3;
-    uint8_t* o = out + ((int64_t)y * CW + j) * 3;
-    if (!need_h) {
-      o[0] = row[(left + j) * 3 + 0];
-      o[1] = row[(left + j) * 3 + 1];
-      o[2] = row[(left + j) * 3 + 2];
-      continue;
+    __builtin_amdgcn_wave_barrier();  // previous row's tap reads precede the overwrite
+    for (int i = lane; i < W * 3; i += 64) ((uint8_t*)srow)[(i / 3) * 4 + (i % 3)] = row[i];
+    __builtin_amdgcn_wave_barrier();
+    for (int j = lane; j < CW; j += 64) {
+      uint32_t o;
+      if (!need_h) {
+        o = srow[left + j] & 0x00ffffffu;
+      } else {
+        const int* bd = tab.bounds + ((int64_t)b * (CW + CH) + j) * 2;
+        const int* k = tab.coef + tap_at(b, 0, j, CW, CH, KMAX);
+        const int xmin = bd[0], n = bd[1];
+        int s0 = 1 << (PREC - 1), s1 = s0, s2 = s0;
+        for (int x = 0; x < n; ++x) {
+          const int w = k[(int64_t)x * (CW + CH)];
+          const uint32_t px = srow[xmin + x];
+          s0 += (int)(px & 0xff) * w;
+          s1 += (int)((px >> 8) & 0xff) * w;
+          s2 += (int)((px >> 16) & 0xff) * w;
+        }
+        o = (uint32_t)clip8(s0) | ((uint32_t)clip8(s1) << 8) | ((uint32_t)clip8(s2) << 16);
+      }
+      out[(int64_t)y * CW + j] = o;
     }
-    const int* bd = tab.bounds + ((int64_t)b * (CW + CH) + j) * 2;
-    const int* k = tab.coef + ((int64_t)b * (CW + CH) + j) * KMAX;
-    const int xmin = bd[0], n = bd[1];
-    int s0 = 1 << (PREC - 1), s1 = s0, s2 = s0;
-    const uint8_t* p = row + xmin * 3;
-    for (int x = 0; x < n; ++x) {
-      const int w = k[x];
-      s0 += (int)p[3 * x + 0] * w;
-      s1 += (int)p[3 * x + 1] * w;
-      s2 += (int)p[3 * x + 2] * w;
-    }
-    o[0] = clip8(s0);
-    o[1] = clip8(s1);
-    o[2] = clip8(s2);
   }
 }
 
@@ -145,29 +155,29 @@ __global__ void vpass_k(const int* __restrict__ hw, int RH, int top, int CH, int
   const int b = blockIdx.y;
   const int H = hw[2 * b];
   const bool need_v = H != RH;
-  const uint8_t* src = tmp + (int64_t)b * tmp_stride;
+  const uint32_t* src = (const uint32_t*)(tmp + (int64_t)b * tmp_stride);
   const int64_t total = (int64_t)CH * CW;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int i = (int)(idx / CW), j = (int)(idx % CW);
     uint8_t u[3];
     if (!need_v) {
-      const uint8_t* p = src + ((int64_t)(top + i) * CW + j) * 3;
-      u[0] = p[0];
-      u[1] = p[1];
-      u[2] = p[2];
+      const uint32_t px = src[(int64_t)(top + i) * CW + j];
+      u[0] = px & 0xff;
+      u[1] = (px >> 8) & 0xff;
+      u[2] = (px >> 16) & 0xff;
     } else {
       const int* bd = tab.bounds + ((int64_t)b * (CW + CH) + CW + i) * 2;
-      const int* k = tab.coef + ((int64_t)b * (CW + CH) + CW + i) * KMAX;
+      const int* k = tab.coef + tap_at(b, 0, CW + i, CW, CH, KMAX);
       const int ymin = bd[0], n = bd[1];
       int s0 = 1 << (PREC - 1), s1 = s0, s2 = s0;
-      const uint8_t* p = src + ((int64_t)ymin * CW + j) * 3;
+      const uint32_t* p = src + (int64_t)ymin * CW + j;
       for (int y = 0; y < n; ++y) {
-        const int w = k[y];
-        const uint8_t* q = p + (int64_t)y * CW * 3;
-        s0 += (int)q[0] * w;
-        s1 += (int)q[1] * w;
-        s2 += (int)q[2] * w;
+        const int w = k[(int64_t)y * (CW + CH)];
+        const uint32_t px = p[(int64_t)y * CW];
+        s0 += (int)(px & 0xff) * w;
+        s1 += (int)((px >> 8) & 0xff) * w;
+        s2 += (int)((px >> 16) & 0xff) * w;
       }
       u[0] = clip8(s0);
       u[1] = clip8(s1);
@@ -190,10 +200,10 @@ __global__ void vpass_k(const int* __restrict__ hw, int RH, int top, int CH, int
 
 extern "C" int sdp_val_preprocess(const uint8_t* pix, const int64_t* offs, const int* hw, int B, int RH, int RW,
                                   int top, int left, int CH, int CW, int KMAX, const float* mean3, const float* std3,
-                                  void* ws, uint8_t* tmp, int64_t tmp_stride, int dtype_out, void* out,
-                                  uint8_t* out_u8, void* stream) {
+                                  void* ws, uint8_t* tmp, int64_t tmp_stride, int max_w, int dtype_out,
+                                  void* out, uint8_t* out_u8, void* stream) {
   if (B < 0 || RH <= 0 || RW <= 0 || CH <= 0 || CW <= 0 || top < 0 || left < 0 || top + CH > RH ||
-      left + CW > RW || KMAX <= 0 || KMAX > 160 || !mean3 || !std3)
+      left + CW > RW || KMAX <= 0 || KMAX > 160 || !mean3 || !std3 || max_w <= 0 || max_w > 40960)
     return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
   if (!pix || !offs || !hw || !ws || !tmp || !out) return (int)hipErrorInvalidValue;
@@ -206,8 +216,19 @@ extern "C" int sdp_val_preprocess(const uint8_t* pix, const int64_t* offs, const
   }
   hipLaunchKernelGGL(pre::coef_k, dim3((CW + CH + 63) / 64, B), dim3(64), 0, s, hw, B, RH, RW, top, left, CH, CW,
                      KMAX, tab);
-  hipLaunchKernelGGL(pre::hpass_k, dim3(64, B), dim3(256), 0, s, pix, offs, hw, RH, RW, top, left, CH, CW, KMAX, tab,
-                     tmp, tmp_stride);
+  // one RGBX source row per wave in LDS: 4 waves per block while they fit in 64 KiB
+  int nw = 4;
+  while (nw > 1 && (size_t)nw * max_w * 4 > 65536) nw >>= 1;
+  const size_t lds = (size_t)nw * max_w * 4;
+  if (lds > 65536) {
+    static bool raised = false;
+    if (!raised) {
+      (void)hipFuncSetAttribute((const void*)pre::hpass_k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      raised = true;
+    }
+  }
+  hipLaunchKernelGGL(pre::hpass_k, dim3(64, B), dim3(64 * nw), lds, s, pix, offs, hw, RH, RW, top, left, CH, CW,
+                     KMAX, tab, tmp, tmp_stride, max_w);
   if (dtype_out == 0)
     hipLaunchKernelGGL(pre::vpass_k<float>, dim3(64, B), dim3(256), 0, s, hw, RH, top, CH, CW, KMAX, tab,
                        (const uint8_t*)tmp, tmp_stride, nm, (float*)out, out_u8);

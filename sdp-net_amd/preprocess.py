@@ -76,7 +76,7 @@ class ValTransform:
             out = torch.empty(0, 3, *self.crop_size, dtype=self.dtype, device=self.device)
             u8 = torch.empty(0, *self.crop_size, 3, dtype=torch.uint8, device=self.device)
             return (out, u8) if return_u8 else out
-        kmax, hmax = 1, 1
+        kmax, hmax, wmax = 1, 1, 1
         for a in arrs:
             H, W = a.shape[:2]
             if H == 0 or W == 0:
@@ -85,6 +85,7 @@ class ValTransform:
                 raise NotImplementedError(f"image {H}x{W}: aspect ratio above 100 (Pillow reorders its passes there)")
             kmax = max(kmax, _taps(W, RW), _taps(H, RH))
             hmax = max(hmax, H)
+            wmax = max(wmax, W)
         if kmax > MAX_TAPS:
             raise NotImplementedError(f"downscale factor too large ({kmax} taps > {MAX_TAPS})")
         sizes = [a.shape[0] * a.shape[1] * 3 for a in arrs]
@@ -98,9 +99,9 @@ class ValTransform:
         pix = host.to(self.device, non_blocking=True)
         offs_d = torch.from_numpy(offs).to(self.device)
         hw_d = hw.to(self.device)
-        tmp_stride = hmax * self.crop_size[1] * 3
+        tmp_stride = hmax * self.crop_size[1] * 4  # RGBX words of the horizontal pass
         out, u8 = sp.val_preprocess(pix, offs_d, hw_d, self.image_size, self.crop_size, self.top, self.left, kmax,
-                                    self.mean, self.std, tmp_stride, self.dtype, want_u8=return_u8)
+                                    self.mean, self.std, tmp_stride, self.dtype, want_u8=return_u8, max_w=wmax)
         return (out, u8) if return_u8 else out
 
 

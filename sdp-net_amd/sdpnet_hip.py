@@ -63,7 +63,7 @@ _SIGS = {
     "sdp_cast": ([_i32, _vp, _i32, _vp, _i64, _vp], _i32),
     "sdp_fold_ln_weight": ([_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp], _i32),
     "sdp_val_preprocess": ([_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
-                            _vp, _vp, _i64, _i32, _vp, _vp, _vp], _i32),
+                            _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp], _i32),
     "sdp_logits_metrics": ([_i32, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp], _i32),
 }
 
@@ -378,7 +378,8 @@ def fold_ln_weight(w: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, bia
 
 
 def val_preprocess(pix: torch.Tensor, offs: torch.Tensor, hw: torch.Tensor, resize, crop, top: int, left: int,
-                   kmax: int, mean, std, tmp_stride: int, dtype: torch.dtype, want_u8: bool = False):
+                   kmax: int, mean, std, tmp_stride: int, dtype: torch.dtype, want_u8: bool = False,
+                   max_w: int = 0):
     """Batched validation transform (sdp_val_preprocess); returns (out NCHW, out_u8 or None)."""
     _need_cuda(pix, offs, hw)
     assert pix.dtype == torch.uint8 and offs.dtype == torch.int64 and hw.dtype == torch.int32
@@ -392,7 +393,7 @@ def val_preprocess(pix: torch.Tensor, offs: torch.Tensor, hw: torch.Tensor, resi
     m3 = (ctypes.c_float * 3)(*[float(v) for v in mean])
     s3 = (ctypes.c_float * 3)(*[float(v) for v in std])
     rc = lib().sdp_val_preprocess(pix.data_ptr(), offs.data_ptr(), hw.data_ptr(), B, RH, RW, top, left, CH, CW,
-                                  kmax, m3, s3, ws.data_ptr(), tmp.data_ptr(), tmp_stride, dcode(dtype),
+                                  kmax, m3, s3, ws.data_ptr(), tmp.data_ptr(), tmp_stride, max_w, dcode(dtype),
                                   out.data_ptr(), _ptr(u8), _stream(out))
     _check(rc, "val_preprocess")
     return out, u8

@@ -49,7 +49,7 @@ def main():
 
     def run():
         return sp.val_preprocess(pix, offs, hw, (320, 320), (224, 224), t.top, t.left, kmax, t.mean, t.std,
-                                 H * 224 * 3, torch.float32)[0]
+                                 H * 224 * 4, torch.float32, max_w=W)[0]
 
     for _ in range(3):
         run()
