@@ -1299,7 +1299,7 @@ extern "C" int sdp_gemm_force_generic(int on) {
 // 9 = 8-phase ping-pong 256x256, 11 = persistent form of 9, 12 / 13 = 9 / 11
 // with the whole-line LDS-staged epilogue,
 // 14 (default) = 12 with every row group staged before the first store (one LDS round
-// trip per wave; 9 % less single-stream GEMM time, equal in the two-stream model),
+// trip per wave; bit-identical to 12 and within +-2 % of it, order-balanced),
 // 4 / 10 = no-store timing probes of 3 / 9
 // (wrong results; benchmarks only).
 static int g_fast_kernel = 14;

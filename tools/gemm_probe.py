@@ -35,6 +35,19 @@ for kern, dist in [(int(k), d) for k in os.environ.get("PROBE_KERNELS", "10,12")
             e1.record()
             torch.cuda.synchronize()
             res[name] = 1e3 * e0.elapsed_time(e1) / 20
+        if os.environ.get("PROBE_TORCH"):  # vendor yardstick: torch F.linear (hipBLASLt), same timing loop
+            f = lambda: torch.nn.functional.linear(x, w)  # noqa: E731
+            for _ in range(3):
+                f()
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(20):
+                f()
+            e1.record()
+            torch.cuda.synchronize()
+            res["hipBLASLt"] = 1e3 * e0.elapsed_time(e1) / 20
         tf = {k: 2.0 * M * N * K / (v * 1e-6) / 1e12 for k, v in res.items()}
         print(f"kern={kern} {dist:7s} {M}x{N}x{K}: dense {res['dense']:.1f} us ({tf['dense']:.0f} TF/s)  "
-              f"hotX {res['hotX']:.1f} us ({tf['hotX']:.0f} TF/s)", flush=True)
+              f"hotX {res['hotX']:.1f} us ({tf['hotX']:.0f} TF/s)"
+              + (f"  hipBLASLt {res['hipBLASLt']:.1f} us ({tf['hipBLASLt']:.0f} TF/s)" if "hipBLASLt" in res else ""),
+              flush=True)
