@@ -92,6 +92,11 @@ int sdp_gemm_set_desync(int d);
  * stores, 0 = default.  Returns the previous value. */
 int sdp_gemm_set_store_policy(int nt);
 
+/* Tile raster of the 8-phase GEMM: M-blocks per group (consecutive blocks walk a group of
+ * gm M-blocks before the next N-tile).  1 = row-major, -1 = auto (4 when N spans >= 8
+ * tiles, else 1).  Results do not depend on it.  Returns the previous value. */
+int sdp_gemm_set_group_m(int gm);
+
 /*
  * LayerNorm statistics by parts: sdp_row_partials writes {mean, M2} of every
  * 64-column chunk of the logical rows of X to part[(phys_row * ceil(C/64) + c) * 2];

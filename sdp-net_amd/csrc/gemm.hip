@@ -54,6 +54,7 @@ struct Epi {
   int delay = 0;
   int delay_blocks = 0;
   int nt_store = 0;  // whole-line epilogue: non-temporal (streaming) output stores
+  int group_m = 1;   // 8ph tile raster: M-blocks per group (1 = row-major tiles)
 };
 
 // fold: v = r * acc + (b - r * mu * s) for one element (generic paths)
@@ -639,7 +640,21 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   const int b = blockIdx.x;
   const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
   const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
-  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
+  // grouped raster (epi.group_m > 1): wgids run down a group of group_m M-blocks before
+  // moving to the next N-tile, so the 32 concurrent tiles of an XCD span ~group_m
+  // X blocks x 32/group_m W slices instead of 32/tiles_n X blocks x every W slice
+  int tm, tn;
+  if (epi.group_m > 1) {
+    const int gsz_full = epi.group_m * tiles_n;
+    const int g = wgid / gsz_full, r = wgid - g * gsz_full;
+    const int first = g * epi.group_m;
+    const int gm = min(tiles_m - first, epi.group_m);
+    tm = first + r % gm;
+    tn = r / gm;
+  } else {
+    tm = wgid / tiles_n;
+    tn = wgid % tiles_n;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -1309,6 +1324,13 @@ extern "C" int sdp_gemm_set_fast_kernel(int k) {
   return old;
 }
 
+static int g_group_m = -1;  // -1 = auto
+extern "C" int sdp_gemm_set_group_m(int gm) {
+  int old = g_group_m;
+  g_group_m = gm;
+  return old;
+}
+
 static int g_nt_store = 0;
 extern "C" int sdp_gemm_set_store_policy(int nt) {
   int old = g_nt_store;
@@ -1382,6 +1404,10 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
     Epi<bf16_t> e{bias, (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, act, resid_pre, ln_stats, ln_colsum, nullptr};
     e.delay = g_desync;
     e.nt_store = g_nt_store;
+    {
+      const int tiles_n_ = (N + fast::BN - 1) / fast::BN;
+      e.group_m = g_group_m >= 1 ? g_group_m : (tiles_n_ >= 8 ? 4 : 1);
+    }
     e.delay_blocks = num_cus();
     const bool aligned = (ldy % 4 == 0) && ((uintptr_t)Y % 8 == 0) && (!R || ((ldr % 4 == 0) && ((uintptr_t)R % 8 == 0))) &&
                          (!bias || ((uintptr_t)bias % 16 == 0)) && (ldx % 8 == 0) && ((uintptr_t)X % 16 == 0) &&

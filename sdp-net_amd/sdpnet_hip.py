@@ -39,6 +39,7 @@ _SIGS = {
     "sdp_gemm_set_fast_kernel": ([_i32], _i32),
     "sdp_gemm_set_desync": ([_i32], _i32),
     "sdp_gemm_set_store_policy": ([_i32], _i32),
+    "sdp_gemm_set_group_m": ([_i32], _i32),
     "sdp_layernorm": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _f32, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_qk_headnorm": ([_i32, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp], _i32),
     "sdp_rowstats": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _i32, _i32, _vp], _i32),
@@ -104,6 +105,9 @@ def lib():
         kern = os.environ.get("SDPNET_GEMM_NT_STORE")  # streaming output stores in the GEMM epilogue
         if kern:
             L.sdp_gemm_set_store_policy(int(kern))
+        kern = os.environ.get("SDPNET_GEMM_GROUP_M")  # tile raster of the 8-phase GEMM (-1 auto, 1 row-major)
+        if kern:
+            L.sdp_gemm_set_group_m(int(kern))
         kern = os.environ.get("SDPNET_DW_KERNEL")  # A/B switch for the depthwise conv
         if kern:
             L.sdp_dwconv_set_kernel(int(kern))
