@@ -589,7 +589,18 @@ class ClassificationHead(nn.Module):
             params += [m.weight, m.bias]
 
         def build():
-            d = dict(lin=[(as_dtype(m.weight, dt), f32(m.bias)) for m in lins])
+            lin = [(as_dtype(m.weight, dt), f32(m.bias)) for m in lins]
+            pad = -lin[0][0].shape[0] % 64
+            if len(lin) == 2 and dt == torch.bfloat16 and pad:
+                # The bf16 MFMA GEMM needs K % 64 == 0. Zero-pad the hidden width (1000 -> 1024):
+                # the extra hidden units have zero weights and bias, so tanh(0) = 0, and they
+                # meet zero K columns of the second weight. The logits are unchanged and both
+                # GEMMs take the fast path instead of gemm_generic.
+                (w1, b1), (w2, b2) = lin
+                w1 = F.pad(w1, (0, 0, 0, pad))
+                b1 = None if b1 is None else F.pad(b1, (0, pad))
+                lin = [(w1, b1), (F.pad(w2, (0, pad)).contiguous(), b2)]
+            d = dict(lin=lin)
             if lns:
                 d["ln"] = (f32(lns[0].weight), f32(lns[0].bias), lns[0].eps)
             return d
