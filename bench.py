@@ -1,6 +1,13 @@
 """SdP-Net forward benchmark on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N --steps K --warmup W]       (N>1: under torch.distributed.run)
+  python bench.py [--gpus N --steps K --warmup W] [--config m|xl]
+
+--gpus N > 1 started outside torch.distributed.run re-launches itself as a CHILD
+`python -m torch.distributed.run --nproc-per-node N ... bench.py ...` (before any
+GPU call in the parent) and exits with its code; under torch.distributed.run each
+rank checks WORLD_SIZE == --gpus and rank 0 reports the RCCL world size and the
+per-rank devices.  --dry-run runs the same launch / barrier / max-over-ranks
+timing path on CPU with gloo and a trivial step (launcher test; no model).
 
 Workload (BASELINE.json configs[1]): SdP-Net-M (12 blocks, d=768, patch 16,
 canonical config SURVEY.md §0) bf16 eval forward, batch 256 synthetic N(0,1)
@@ -29,9 +36,7 @@ sys.path.insert(0, os.path.join(REPO, "sdp-net_amd"))
 
 METRIC = "images/sec fwd SdP-Net-M 224×224 bs=256 @1 GPU; scaling 1/2/4/8"
 MFMA_BF16_PEAK_TFLOPS = 2516.6   # 256 CU x 2.4 GHz x 4096 FLOP/clk/CU (dense)
-FAST_GEMM_NAMES = {1: "gemm_bf16_256x256", 3: "gemm_bf16_256x256", 5: "gemm_bf16_deepx", 7: "gemm_bf16_256x128",
-                   8: "gemm_bf16_256x128i", 9: "gemm_bf16_8ph", 11: "gemm_bf16_8php", 12: "gemm_bf16_8ph", 13: "gemm_bf16_8php",
-                   14: "gemm_bf16_8ph"}
+FAST_GEMM_NAMES = {9: "gemm_bf16_8ph", 14: "gemm_bf16_8ph"}
 
 M_CFG = dict(embedding_dim=768, num_blocks=12, n_head=8, activation="gelu", embedding_activation="none",
              conv_kernel_size=7, patch_size=16, ffn_dropout=0.2, attn_dropout=0.2, output_classes=1000,
@@ -107,6 +112,65 @@ def cpu_baseline(model_cpu_sd, cfg, seconds=12.0, name="SdP-Net-M"):
                       f"oracle/sdpnet_oracle.py (reference math, stock torch CPU ops)"}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """Parent side of --gpus N: run N ranks under torch.distributed.run as a child
+    process (model_train.py:33-42 is the reference's rank setup: one process per GPU,
+    LOCAL_RANK from the launcher).  No GPU call happens in this process."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, world, rank):
+    """CPU/gloo rehearsal of the multi-rank timing path (no model, no GPU)."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(REPO, "sdp-net_amd"))
+    import sharding
+    if world > 1:
+        dist.init_process_group("gloo")
+    lo, hi = sharding.shard_bounds(args.batch * world, world, rank)
+    x = torch.randn(hi - lo, 64)
+    w = torch.randn(64, 64)
+    for _ in range(args.warmup):
+        x @ w
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x @ w
+    if world > 1:
+        dist.barrier()
+    el = sharding.max_over_ranks(time.perf_counter() - t0)
+    total = int(sharding.sum_over_ranks((hi - lo) * args.steps))
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid(), "shard": [lo, hi]})
+    else:
+        ranks = [{"rank": 0, "pid": os.getpid(), "shard": [lo, hi]}]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "steps": args.steps, "value": round(total / el, 2),
+                          "comm_world": dist.get_world_size() if world > 1 else 1,
+                          "backend": dist.get_backend() if world > 1 else None,
+                          "global_batch": args.batch * world, "ranks": ranks}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,22 +183,38 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prof-steps", type=int, default=2)
     ap.add_argument("--streams", type=int, default=0, help="sub-batch streams per GPU (0 = model default)")
+    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of the launch + timing path")
     args = ap.parse_args()
     C = CONFIGS[args.config]
     cfg = C["cfg"]
     if args.batch <= 0:
         args.batch = C["batch"]
 
-    import torch
-    import torch.distributed as dist
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch N ranks with --gpus N")
+    if args.dry_run:
+        return dry_run(args, world, rank)
+
+    import torch
+    import torch.distributed as dist
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    comm_world = dist.get_world_size() if world > 1 else 1
+    if comm_world != world:
+        raise SystemExit(f"bench.py: RCCL world size {comm_world} != {world}")
+    if world > 1:
+        devs = [None] * world
+        dist.all_gather_object(devs, f"rank{rank}:cuda:{local}:{torch.cuda.get_device_name(dev)}")
+    else:
+        devs = [f"rank0:cuda:{local}:{torch.cuda.get_device_name(dev)}"]
 
     import model as sdp
     import sdpnet_hip as sp
@@ -215,7 +295,7 @@ def main():
         per_shape[f"{key[0]}x{key[1]}x{key[2]}"] = dict(launches=len(lst), avg_us=round(1e3 * ms / len(lst), 2),
                                                         tflops=round(fl / (ms * 1e-3) / 1e12, 1),
                                                         kernel="fast" if key[3] == 1 else "gemm_generic")
-        if key[3] == 1:
+        if key[3] == 1 and key[0] >= 1024:  # the head's batch-row GEMMs stay in per_shape only
             fast_fl += fl
             fast_ms += ms
             fast_by += by
@@ -240,10 +320,13 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic N(0,1) 224x224 images resident in HBM; random-init weights (reference init)",
-        "config": {"workload": C["desc"] + ", bf16 storage / fp32 accumulate, HIP-graph replay",
+        "config": {"workload": C["desc"] + ", bf16 storage / fp32 accumulate"
+                                + (", eager launches" if args.no_graph else ", HIP-graph replay"),
                    "streams_per_gpu": m._num_streams(B),
                    "global_batch": args.batch * world, "per_gpu_batch": B, "image": 224, "tokens": tokens,
-                   "parallelism": f"dp{world} independent batch shards (no collective)"},
+                   "parallelism": f"dp{world} independent batch shards (no collective)",
+                   "comm_world": comm_world, "comm_backend": "nccl (RCCL)" if world > 1 else None,
+                   "devices": devs},
         "model_flops_per_image_gf": round(gf, 3),
         "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
         "roofline": {"bound": "mfma", "kernel": kname,

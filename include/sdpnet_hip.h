@@ -18,9 +18,13 @@
  *     stride `ld` (in elements).  grp <= 0 means "dense" (physical = logical).
  *     This addresses the image rows of the persistent [B, R+P, C] token buffer
  *     (grp = P, gstride = R+P, off = R) without gather/scatter copies.
- *   - Activation codes: 0 none, 1 gelu (exact erf), 2 relu, 3 tanh, 4 sigmoid,
+ *   - Activation codes: 0 none, 1 gelu, 2 relu, 3 tanh, 4 sigmoid,
  *     5 leaky_relu (0.01), 6 selu, 7 kelu (model.py:13-24,
- *     training_utilities.py:91-92).
+ *     training_utilities.py:91-92).  GELU is the exact erf form everywhere except
+ *     the bf16 fast-GEMM epilogue, which uses the tanh form
+ *     x * sigmoid(sqrt(2/pi) (x + 0.044715 x^3)) (|diff| <= 4.7e-4, about one bf16
+ *     rounding of the output; a DECLARED deviation from nn.GELU(), model.py:15) unless
+ *     sdp_gemm_set_exact_gelu(1) is set.
  */
 #ifndef SDPNET_HIP_H
 #define SDPNET_HIP_H
@@ -73,20 +77,10 @@ int sdp_gemm_variant(int dtype, int M, int N, int K);
 int sdp_gemm_force_generic(int on);
 /* Select the bf16 fast kernel: 14 = 8-phase ping-pong 256x256x64 with the
  * whole-line (LDS-staged) epilogue, all row groups staged before the first store
- * (default); 12 = same staging one row group at a time; 9 = direct epilogue;
- * 11 / 13 = persistent forms of 9 / 12;
- * 1 = 256x256 tiles, 2-stage LDS ring, 8-byte stores; 3 = same with
- * permlane-paired 16-byte stores; 5 = 256x256, deep X ring (3 slots); 7 = 256x128
- * tiles, 3-slot ring, two blocks per CU; 8 = 7 with interleaved DMA; 4 / 10 =
- * no-store timing probes of 3 / 9 (benchmarks only: wrong results).  Any other
+ * (default); 9 = same main loop, permlane-paired 16-B register epilogue (also the
+ * automatic fallback for unaligned rows and resid_pre with an activation).  Any other
  * value leaves the selection unchanged.  Returns the previous selection. */
 int sdp_gemm_set_fast_kernel(int k);
-
-/* First-round stagger of the 8-phase GEMM: in the first wave of blocks (one per CU),
- * every other block of an XCD sleeps d x s_sleep(127) (~8k cycles each) before its
- * prologue, so the CUs' epilogue store bursts stop coinciding.  0 = off.  Returns
- * the previous value. */
-int sdp_gemm_set_desync(int d);
 
 /* Output store policy of the whole-line GEMM epilogue: 1 = non-temporal (streaming)
  * stores, 0 = default.  Returns the previous value. */
@@ -96,6 +90,11 @@ int sdp_gemm_set_store_policy(int nt);
  * gm M-blocks before the next N-tile).  1 = row-major, -1 = auto (4 when N spans >= 8
  * tiles, else 1).  Results do not depend on it.  Returns the previous value. */
 int sdp_gemm_set_group_m(int gm);
+
+/* GELU form of the bf16 fast-GEMM epilogue: 0 = tanh form (default, one v_exp + one
+ * v_rcp per element), 1 = exact erf (nn.GELU(), model.py:15; runtime-activation epilogue).
+ * Used to bound the tanh form's share of the bf16 logits error.  Returns the previous value. */
+int sdp_gemm_set_exact_gelu(int on);
 
 /*
  * LayerNorm statistics by parts: sdp_row_partials writes {mean, M2} of every

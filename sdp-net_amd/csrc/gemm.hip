@@ -14,14 +14,13 @@
 // embedding activation (EmbeddingLayer), Tanh (head).
 //
 // Kernels (bf16 fast path selected by sdp_gemm_set_fast_kernel, default 14):
-//  * gemm_bf16_8ph (9; 12 / 14 with tile_epilogue_rows) — the hot kernel: 256x256x64 tiles, 8 waves (2 along M x
+//  * gemm_bf16_8ph — the hot kernel: 256x256x64 tiles, 8 waves (2 along M x
 //    4 along N, 128x64 per wave), v_mfma_f32_16x16x32_bf16, both operands staged
 //    HBM->LDS by global_load_lds_dwordx4 into an XOR-swizzled [row][64] image
 //    (conflict-free ds_read_b128), 4 phases per K-tile with the two wave groups
-//    ping-ponging MFMA against LDS traffic, XCD-aware tile order.
+//    ping-ponging MFMA against LDS traffic, XCD-aware tile order.  Epilogue 14 =
+//    whole-line LDS-staged stores (default), 9 = register epilogue (fallback).
 //    Requires K % 64 == 0; any M, N (clamped loads, masked stores).
-//  * gemm_bf16_256x256 (1/3/4), gemm_bf16_deepx (5), half::gemm_bf16_256x128[i]
-//    (7/8) — earlier schedules kept for A/B measurement.
 //  * gemm_generic<T> — correctness path for fp32 (exact f32 MFMA
 //    v_mfma_f32_16x16x4_f32) and for odd bf16 shapes; fully masked.
 //
@@ -49,10 +48,6 @@ struct Epi {
   // Per-row partial statistics of the stored outputs, 64-column chunks:
   // part[(cmap(m) * (N/64) + n/64) * 2 + {0,1}] = {mean, M2} (whole-line epilogue only)
   float* part;
-  // first-round stagger (sdp_gemm_set_desync): blocks b < delay_blocks with (b >> 3) odd
-  // sleep `delay` x s_sleep(127) before their prologue
-  int delay = 0;
-  int delay_blocks = 0;
   int nt_store = 0;  // whole-line epilogue: non-temporal (streaming) output stores
   int group_m = 1;   // 8ph tile raster: M-blocks per group (1 = row-major tiles)
 };
@@ -119,12 +114,11 @@ SDP_DEV void epi_store4(const Epi<T>& e, int64_t m, int n, int N, f32x4 acc) {
 }
 
 // ---------------------------------------------------------------------------
-// Hot kernel: bf16, 256x256x64, glds double buffer.
+// Hot kernel: bf16, 256x256x64 tiles, LDS-DMA double buffer (gemm_bf16_8ph below).
 // ---------------------------------------------------------------------------
 namespace fast {
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int TILE_BYTES = BM * BK * 2;       // 32 KiB per operand per stage
-constexpr int STAGE_BYTES = 2 * TILE_BYTES;   // A + W
 constexpr int NTHREADS = 512;
 
 // LDS image of one operand tile: [256 rows][64 bf16] = 128 B per row, 16-B chunk
@@ -132,25 +126,6 @@ constexpr int NTHREADS = 512;
 // group reading one logical chunk of 16 consecutive rows hits 16 distinct 4-bank
 // slots (conflict-free).
 SDP_DEV int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
-
-// Issue the 4 global_load_lds_dwordx4 pieces of one 256x64 tile for this wave.
-// A piece = 8 rows x 128 B = one wave-instruction (lane-linear LDS destination),
-// so the swizzle is applied to the per-lane SOURCE chunk (involution).
-SDP_DEV void stage_tile(const bf16_t* __restrict__ base, int64_t ld, RowMap map, int row0,
-                        int nrows, int k0, char* lds_tile, int wave, int lane) {
-  const int rr = lane >> 3;          // row inside the piece
-  const int pc = lane & 7;           // physical chunk this lane fills
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int piece = wave * 4 + i;  // 0..31
-    const int r = piece * 8 + rr;
-    const int c = swz(r, pc);        // logical chunk to fetch
-    int grow = row0 + r;
-    grow = grow < nrows ? grow : nrows - 1;  // clamp (tail rows are never stored)
-    const bf16_t* src = base + map(grow) * ld + k0 + c * 8;
-    __builtin_amdgcn_global_load_lds((const AS1 void*)src, (AS3 void*)(lds_tile + piece * 1024), 16, 0, 0);
-  }
-}
 
 SDP_DEV bf16x8 lds_frag(const char* lds_tile, int r, int c) {
   return *(const bf16x8*)(lds_tile + r * 128 + swz(r, c) * 16);
@@ -162,6 +137,7 @@ template <int ACT>
 SDP_DEV float epi_act(int code, float v) {
   if constexpr (ACT == ACT_NONE) return v;
   else if constexpr (ACT == ACT_GELU) return gelu_fast(v);
+  else if constexpr (ACT == ACT_TANH) return tanhf(v);
   else return apply_act(code, v);
 }
 
@@ -462,145 +438,6 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
 }
 
 // EPI: 0 = 8-B stores, 1 = permlane-paired 16-B stores, 2 = no stores (timing probe only)
-template <int ACT, int EPI>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_256x256(
-    const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap, const bf16_t* __restrict__ W,
-    int64_t ldw, Epi<bf16_t> epi, int M, int N, int K, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
-
-  // XCD-aware, bijective block -> tile remap: blocks b and b+8 share an XCD,
-  // give each XCD a contiguous range of tiles (row-panel major, N fastest) so
-  // concurrently resident blocks on one L2 share X row panels and W panels.
-  const int nwg = tiles_m * tiles_n;
-  const int b = blockIdx.x;
-  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
-  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
-  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2;  // 0..1  -> 128 rows of X each
-  const int wn = wave & 3;   // 0..3  -> 64 rows of W each
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const RowMap wmap{0x7fffffff, 0, 0};
-  const int nk = K / BK;
-  stage_tile(X, ldx, xmap, m0, M, 0, smem, wave, lane);
-  stage_tile(W, ldw, wmap, n0, N, 0, smem + TILE_BYTES, wave, lane);
-  __syncthreads();
-
-  const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * STAGE_BYTES;
-    if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
-      stage_tile(X, ldx, xmap, m0, M, (kt + 1) * BK, nxt, wave, lane);
-      stage_tile(W, ldw, wmap, n0, N, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
-    }
-    const char* xt = cur;
-    const char* wt = cur + TILE_BYTES;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c = ks * 4 + fq;
-      bf16x8 bx[8], aw[4];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bx[j] = lds_frag(xt, wm * 128 + j * 16 + fr, c);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) aw[i] = lds_frag(wt, wn * 64 + i * 16 + fr, c);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[i], bx[j], acc[i][j], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-
-  tile_epilogue<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
-}
-
-
-
-// Deep-X variant: the streamed activation operand X gets a 3-slot LDS ring, the
-// weight operand W (L2/MALL resident) a 2-slot ring: 5 x 32 KiB = all 160 KiB.
-// Iteration kt issues W(kt+1) then X(kt+2) and ends with a COUNTED
-// s_waitcnt vmcnt(4) (X(kt+2)'s four wave-instructions stay in flight across the
-// barrier; they are the youngest) + lgkmcnt(0) + raw s_barrier, so an HBM miss
-// on X has two K-steps (~4 us) to land instead of one.
-template <int ACT>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_deepx(
-    const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap, const bf16_t* __restrict__ W,
-    int64_t ldw, Epi<bf16_t> epi, int M, int N, int K, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[5 * TILE_BYTES];
-  char* xring = smem;                   // 3 slots
-  char* wring = smem + 3 * TILE_BYTES;  // 2 slots
-  const int nwg = tiles_m * tiles_n;
-  const int b = blockIdx.x;
-  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
-  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
-  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int fr = lane & 15, fq = lane >> 4;
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const RowMap wmap{0x7fffffff, 0, 0};
-  const int nk = K / BK;
-  // prologue: W(0), X(0), X(1)
-  stage_tile(W, ldw, wmap, n0, N, 0, wring, wave, lane);
-  stage_tile(X, ldx, xmap, m0, M, 0, xring, wave, lane);
-  if (nk > 1) {
-    stage_tile(X, ldx, xmap, m0, M, BK, xring + TILE_BYTES, wave, lane);
-    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-
-  int xs = 0, ws = 0;  // current ring slots
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more1 = kt + 1 < nk, more2 = kt + 2 < nk;
-    if (more1) stage_tile(W, ldw, wmap, n0, N, (kt + 1) * BK, wring + (ws ^ 1) * TILE_BYTES, wave, lane);
-    if (more2) {
-      const int xs2 = xs >= 1 ? xs - 1 : 2;  // (xs + 2) % 3
-      stage_tile(X, ldx, xmap, m0, M, (kt + 2) * BK, xring + xs2 * TILE_BYTES, wave, lane);
-    }
-    const char* xt = xring + xs * TILE_BYTES;
-    const char* wt = wring + ws * TILE_BYTES;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c = ks * 4 + fq;
-      bf16x8 bx[8], aw[4];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bx[j] = lds_frag(xt, wm * 128 + j * 16 + fr, c);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) aw[i] = lds_frag(wt, wn * 64 + i * 16 + fr, c);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[i], bx[j], acc[i][j], 0, 0, 0);
-    }
-    if (more2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    xs = xs == 2 ? 0 : xs + 1;
-    ws ^= 1;
-  }
-  tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
-}
-
 // ---------------------------------------------------------------------------
 // 8-phase ping-pong kernel: 256x256x64 tiles, 8 waves (2 along M x 4 along N,
 // 128x64 per wave), two LDS buffers of one K-tile each (X + W = 64 KiB).
@@ -660,9 +497,6 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   const int wm = wave >> 2, wn = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
   const int nk = K / BK;
-  if (epi.delay > 0 && b < epi.delay_blocks && ((b >> 3) & 1)) {
-    for (int i = 0; i < epi.delay; ++i) __builtin_amdgcn_s_sleep(127);
-  }
 
   // The wave's 8 DMA pieces per K-tile (8 rows x 128 B each): [0,1] S1-X,
   // [2,3] S1-W, [4,5] S2-W, [6,7] S3-X.  Source pointers advance by BK per tile.
@@ -777,426 +611,17 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     mfma_section([&] { quad(1, 0, w0); });
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
-  if constexpr (EPI == 3) {  // whole-line epilogue through the (drained) LDS buffers; the
-    // host routes resid_pre-with-activation and unaligned calls to EPI 1
-    tile_epilogue_rows<ACT>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + wave * 2048);
-    return;
-  }
-  if constexpr (EPI == 4) {  // same, all eight row groups staged first (16 KiB per wave:
-    // both K buffers, free once the balancing barrier above has passed)
+  if constexpr (EPI == 4) {  // whole-line epilogue, all eight row groups staged first (16 KiB
+    // per wave: both K buffers, free once the balancing barrier above has passed); the host
+    // routes resid_pre-with-activation and unaligned calls to EPI 1
     tile_epilogue_rows<ACT, 4, true>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + wave * 16384);
-    return;
-  }
-  if constexpr (EPI == 2) {
-    float v = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v += acc[i][j][0] + acc[i][j][3];
-    if (v == 1234.5f) epi.out[tid] = f2bf(v);
     return;
   }
   tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
 }
-// ---------------------------------------------------------------------------
-// Persistent form of gemm_bf16_8ph: one block per CU walks a tile sequence and
-// the K-tile stream (and its 3-sub-stage DMA schedule) runs on across tile
-// boundaries, so the next tile's first K-tiles are already in flight when a
-// tile's epilogue starts, and the epilogue's stores drain underneath the next
-// tile's MFMAs instead of ending the block.
-//
-// Tile sequence: block b takes virtual ids b, b+G, b+2G, ... (G = grid, a
-// multiple of 8), each mapped through the same XCD-aware remap as the one-shot
-// kernel; b+iG and b share b's XCD, so an XCD's resident blocks stay on
-// neighbouring tiles.  A sub-stage's source pointers are recomputed when its own
-// stream reaches K-tile 0 of a new tile.
-//
-// vmcnt: the epilogue issues E store instructions (16 on full tiles, counted as 0
-// on ragged ones) after S2(g+2) and before S3(g+1)-of-the-next-step; the four
-// waits that retire a DMA issued before those stores (t = 0: phases 0, 1, 3;
-// t = 1: phase 0) add E so the stores are not drained.  Counting fewer
-// instructions than were issued only waits longer, never shorter, so E may be a
-// lower bound (epilogue loads are older than its stores and consumed by them).
-// ---------------------------------------------------------------------------
-SDP_DEV void tile_of(int v, int nwg, int tiles_n, int& m0, int& n0) {
-  const int xcd = v & 7, q = nwg >> 3, rem = nwg & 7;
-  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (v >> 3);
-  m0 = (wgid / tiles_n) * BM;
-  n0 = (wgid % tiles_n) * BN;
-}
-
-template <int ACT, bool ROWS = false>
-__global__ __launch_bounds__(NTHREADS) void gemm_bf16_8php(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
-                                                          const bf16_t* __restrict__ W, int64_t ldw, Epi<bf16_t> epi,
-                                                          int M, int N, int K, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF8 + (ROWS ? 8 * 2048 : 0)];
-  const int nwg = tiles_m * tiles_n;
-  const int G = gridDim.x, b = blockIdx.x;
-  const int ntile = (nwg - b + G - 1) / G;  // tiles of this block
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int nk = K / BK;
-  const int total = ntile * nk;
-  if (ntile <= 0) return;
-
-  // Piece s of this wave (8 rows x 128 B; [0,1] S1-X, [2,3] S1-W, [4,5] S2-W,
-  // [6,7] S3-X): tile row and LDS offset are compile-time functions of (s, wave);
-  // the source is kept as a 32-bit element offset from X or W (K-tile 0 of the
-  // piece's current tile), recomputed when the sub-stage enters a new tile.
-  auto piece_of = [&](int s) {
-    const int idx = wave * 2 + (s & 1);
-    if (s < 2) return idx < 8 ? idx : idx + 8;
-    if (s < 4) return (idx >> 2) * 8 + (idx & 3);
-    if (s < 6) return (idx >> 2) * 8 + 4 + (idx & 3);
-    return idx < 8 ? idx + 8 : idx + 16;
-  };
-  uint32_t soff[8];
-  auto set_src = [&](int s, int m0, int n0) {
-    const int r = piece_of(s) * 8 + (lane >> 3);
-    const int c = swz(r, lane & 7);
-    if (s < 2 || s >= 6) {
-      int g = m0 + r;
-      g = g < M ? g : M - 1;
-      soff[s] = (uint32_t)(xmap(g) * ldx + c * 8);
-    } else {
-      int g = n0 + r;
-      g = g < N ? g : N - 1;
-      soff[s] = (uint32_t)((int64_t)g * ldw + c * 8);
-    }
-  };
-  // issue sub-stage pieces [s0, s1) for K-tile t of the block's tile i (global
-  // K-tile index g = i * nk + t picks the LDS buffer)
-  auto stage = [&](int s0, int s1, int i, int t, int g) {
-    if (t == 0) {
-      int m0, n0;
-      tile_of(b + i * G, nwg, tiles_n, m0, n0);
-#pragma unroll
-      for (int s = s0; s < s1; ++s) set_src(s, m0, n0);
-    }
-#pragma unroll
-    for (int s = s0; s < s1; ++s) {
-      const bf16_t* base = (s < 2 || s >= 6) ? X : W;
-      const int lo = ((s < 2 || s >= 6) ? 0 : TILE_BYTES) + piece_of(s) * 1024;
-      __builtin_amdgcn_global_load_lds((const AS1 void*)(base + soff[s] + (uint32_t)(t * BK)),
-                                       (AS3 void*)(smem + (g & 1) * BUF8 + lo), 16, 0, 0);
-    }
-  };
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8 xf[8], w0[4], w1[4];
-  auto read_x = [&](const char* xt, int jm) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) xf[j * 2 + ks] = lds_frag(xt, wm * 128 + jm * 64 + j * 16 + fr, ks * 4 + fq);
-  };
-  auto read_w = [&](const char* wt, int in, bf16x8(&wf)[4]) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) wf[i * 2 + ks] = lds_frag(wt, wn * 64 + in * 32 + i * 16 + fr, ks * 4 + fq);
-  };
-  // ks outermost: the two K-halves of one accumulator are 8 MFMAs apart, so no MFMA
-  // waits on its predecessor's result (ks innermost made 8 dependent back-to-back pairs)
-  auto quad = [&](int jm, int in, const bf16x8(&wf)[4]) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[in * 2 + i][jm * 4 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i * 2 + ks], xf[j * 2 + ks], acc[in * 2 + i][jm * 4 + j], 0, 0, 0);
-  };
-  auto mfma_section = [&](auto&& body) {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-    body();
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  // (i, t) of K-tiles g+1 and g+2, advanced incrementally (no division in the loop)
-  int i1 = nk > 1 ? 0 : 1, t1 = nk > 1 ? 1 : 0;
-  int i2 = i1, t2 = t1;
-  if (++t2 == nk) { t2 = 0; ++i2; }
-  stage(0, 4, 0, 0, 0); stage(4, 6, 0, 0, 0); stage(6, 8, 0, 0, 0);
-  if (total > 1) { stage(0, 4, i1, t1, 1); stage(4, 6, i1, t1, 1); SDP_VMCNT(10); }
-  else SDP_VMCNT(4);
-  __builtin_amdgcn_s_barrier();
-  if (wm == 1) __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-
-  // e0: stores of the previous epilogue are younger than the DMA retired by the
-  // waits of t = 0 (phases 0, 1, 3); e1: of t = 1 phase 0.
-  bool e0 = false, e1 = false;
-  int tile = 0, t = 0;
-  for (int g = 0; g < total; ++g) {
-    const char* xt = smem + (g & 1) * BUF8;
-    const char* wt = xt + TILE_BYTES;
-    const bool more1 = g + 1 < total, more2 = g + 2 < total;
-    const bool ee = e0 || e1;
-    // phase 0: Q(m0, n0); retire S2(g)
-    read_w(wt, 0, w0);
-    read_x(xt, 0);
-    if (more1) {
-      stage(6, 8, i1, t1, g + 1);
-      if (ee) SDP_VMCNT(26); else SDP_VMCNT(10);
-    } else {
-      SDP_VMCNT(2);
-    }
-    mfma_section([&] { quad(0, 0, w0); });
-    // phase 1: Q(m0, n1); retire S3(g)
-    read_w(wt, 1, w1);
-    if (more1) { if (e0) SDP_VMCNT(24); else SDP_VMCNT(8); }
-    else SDP_VMCNT(0);
-    mfma_section([&] { quad(0, 1, w1); });
-    // phase 2: Q(m1, n1)
-    read_x(xt, 1);
-    if (more2) stage(0, 4, i2, t2, g + 2);
-    mfma_section([&] { quad(1, 1, w1); });
-    // phase 3: Q(m1, n0); retire S1(g+1)
-    if (more2) { stage(4, 6, i2, t2, g + 2); if (e0) SDP_VMCNT(26); else SDP_VMCNT(10); }
-    else if (more1) SDP_VMCNT(4);
-    mfma_section([&] { quad(1, 0, w0); });
-    e1 = e0;
-    e0 = false;
-    i1 = i2; t1 = t2;
-    if (++t2 == nk) { t2 = 0; ++i2; }
-    if (++t == nk) {
-      int m0, n0;
-      tile_of(b + tile * G, nwg, tiles_n, m0, n0);
-      const bool full = n0 + BN <= N && m0 + BM <= M;
-      // Close each epilogue with a wait the compiler's waitcnt pass can see (the
-      // builtin, not inline asm), so no epilogue load stays "pending" into the
-      // next K-tile and forces a vmcnt(0) at the loop header: full tiles end with
-      // 16 stores younger than every epilogue load -> vmcnt(16); ragged: vmcnt(0).
-      if (ROWS) {
-        tile_epilogue_rows<ACT, 2>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + 2 * BUF8 + wave * 2048);
-        if (full) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
-        else __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0)
-      } else if (full) {
-        tile_epilogue16<ACT, BN, 4, true>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
-        __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16) expcnt(7) lgkmcnt(15)
-      } else {
-        tile_epilogue<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      }
-      e0 = nk >= 2 && full;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      t = 0;
-      ++tile;
-    }
-  }
-  if (wm == 0) __builtin_amdgcn_s_barrier();
-}
 #undef SDP_VMCNT
 
 }  // namespace fast
-
-// Half-width tile for two blocks per CU: 256x128x32 tiles, 4 waves (2 along M x 2
-// along N, 128x64 each as above), 3-slot LDS ring per operand (3 x 24 KiB = 72 KiB)
-// -> two co-resident blocks per CU, so one block's prologue / epilogue overlaps
-// the other's MFMAs.  LDS rows are 64 B (32 bf16): 16-B chunk c of row r at
-// c ^ H[(r >> 2) & 3], H = {0,2,3,1}.  ds_read_b128 serves the wave in the lane
-// groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59},
-// {36-43,48-51,60-63}; with this H every group's 16 (row, chunk) reads land on
-// 16 distinct 16-B bank slots (a plain c ^ ((r>>2)&3) collides 2-way in group 0).
-namespace half {
-constexpr int BM = 256, BN = 128, BK = 32;
-constexpr int XT = BM * BK * 2, WT = BN * BK * 2, STAGE = XT + WT;  // 16 + 8 KiB
-constexpr int NT = 256;
-SDP_DEV int swz(int r, int c) { return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3); }  // H = {0,2,3,1}
-
-// rows [row0, row0+nrows_tile) x 32 k, per wave `pieces` glds of 16 rows x 64 B
-template <int PIECES>
-SDP_DEV void stage(const bf16_t* __restrict__ base, int64_t ld, RowMap map, int row0, int nrows, int k0, char* lds,
-                   int wave, int lane) {
-  const int rr = lane >> 2, pc = lane & 3;
-#pragma unroll
-  for (int i = 0; i < PIECES; ++i) {
-    const int piece = wave * PIECES + i;
-    const int r = piece * 16 + rr;
-    const int c = swz(r, pc);
-    int grow = row0 + r;
-    grow = grow < nrows ? grow : nrows - 1;
-    const bf16_t* src = base + map(grow) * ld + k0 + c * 8;
-    __builtin_amdgcn_global_load_lds((const AS1 void*)src, (AS3 void*)(lds + piece * 1024), 16, 0, 0);
-  }
-}
-SDP_DEV bf16x8 frag(const char* lds, int r, int c) { return *(const bf16x8*)(lds + r * 64 + swz(r, c) * 16); }
-
-template <int ACT>
-__global__ __launch_bounds__(NT, 2) void gemm_bf16_256x128(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
-                                                           const bf16_t* __restrict__ W, int64_t ldw,
-                                                           Epi<bf16_t> epi, int M, int N, int K, int tiles_m,
-                                                           int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
-  const int nwg = tiles_m * tiles_n;
-  const int b = blockIdx.x;
-  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
-  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
-  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int fr = lane & 15, fq = lane >> 4;
-  const RowMap wmap{0x7fffffff, 0, 0};
-  const int nk = K / BK;
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: stages 0 and 1 (6 glds per wave each)
-  stage<4>(X, ldx, xmap, m0, M, 0, smem, wave, lane);
-  stage<2>(W, ldw, wmap, n0, N, 0, smem + XT, wave, lane);
-  if (nk > 1) {
-    stage<4>(X, ldx, xmap, m0, M, BK, smem + STAGE, wave, lane);
-    stage<2>(W, ldw, wmap, n0, N, BK, smem + STAGE + XT, wave, lane);
-    asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more2 = kt + 2 < nk;
-    if (more2) {
-      const int nx = cur >= 1 ? cur - 1 : 2;  // (cur + 2) % 3
-      char* st = smem + nx * STAGE;
-      stage<4>(X, ldx, xmap, m0, M, (kt + 2) * BK, st, wave, lane);
-      stage<2>(W, ldw, wmap, n0, N, (kt + 2) * BK, st + XT, wave, lane);
-    }
-    const char* xt = smem + cur * STAGE;
-    const char* wt = xt + XT;
-    bf16x8 bx[8], aw[4];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bx[j] = frag(xt, wm * 128 + j * 16 + fr, fq);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) aw[i] = frag(wt, wn * 64 + i * 16 + fr, fq);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[i], bx[j], acc[i][j], 0, 0, 0);
-    if (more2) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    cur = cur == 2 ? 0 : cur + 1;
-  }
-  fast::tile_epilogue16<ACT, BN>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
-}
-
-// Same tile / ring as gemm_bf16_256x128, but the six global_load_lds of the
-// prefetched stage are spread between the MFMA groups of the current K-step
-// (one piece before each group of 8 MFMAs) instead of a burst at the top of the
-// step, so a wave's LDS-DMA issue cost overlaps its own / its partner's MFMAs.
-template <int ACT>
-__global__ __launch_bounds__(NT, 2) void gemm_bf16_256x128i(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
-                                                            const bf16_t* __restrict__ W, int64_t ldw,
-                                                            Epi<bf16_t> epi, int M, int N, int K, int tiles_m,
-                                                            int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
-  const int nwg = tiles_m * tiles_n;
-  const int b = blockIdx.x;
-  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
-  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
-  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int fr = lane & 15, fq = lane >> 4;
-  const RowMap wmap{0x7fffffff, 0, 0};
-  const int nk = K / BK;
-
-  // per-lane source rows of this wave's 6 pieces (4 of X, 2 of W), fixed over K
-  const int rr = lane >> 2, pc = lane & 3;
-  const bf16_t* src[6];
-  int ldsoff[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const bool isx = i < 4;
-    const int piece = isx ? wave * 4 + i : wave * 2 + (i - 4);
-    const int r = piece * 16 + rr;
-    const int c = swz(r, pc);
-    if (isx) {
-      int grow = m0 + r;
-      grow = grow < M ? grow : M - 1;
-      src[i] = X + xmap(grow) * ldx + c * 8;
-      ldsoff[i] = piece * 1024;
-    } else {
-      int grow = n0 + r;
-      grow = grow < N ? grow : N - 1;
-      src[i] = W + (int64_t)grow * ldw + c * 8;
-      ldsoff[i] = XT + piece * 1024;
-    }
-  }
-  auto piece = [&](int i, int kt, char* st) {
-    __builtin_amdgcn_global_load_lds((const AS1 void*)(src[i] + (int64_t)kt * BK), (AS3 void*)(st + ldsoff[i]), 16,
-                                     0, 0);
-  };
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int i = 0; i < 6; ++i) piece(i, 0, smem);
-  if (nk > 1) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) piece(i, 1, smem + STAGE);
-    asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more2 = kt + 2 < nk;
-    char* nst = smem + (cur >= 1 ? cur - 1 : 2) * STAGE;
-    const char* xt = smem + cur * STAGE;
-    const char* wt = xt + XT;
-    bf16x8 bx[8], aw[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) aw[i] = frag(wt, wn * 64 + i * 16 + fr, fq);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bx[j] = frag(xt, wm * 128 + j * 16 + fr, fq);
-    if (more2) { piece(0, kt + 2, nst); piece(1, kt + 2, nst); }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (more2 && i < 2) piece(2 + 2 * i, kt + 2, nst), piece(3 + 2 * i, kt + 2, nst);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[i], bx[j], acc[i][j], 0, 0, 0);
-    }
-    if (more2) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    cur = cur == 2 ? 0 : cur + 1;
-  }
-  fast::tile_epilogue16<ACT, BN>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
-}
-}  // namespace half
-
 
 // ---------------------------------------------------------------------------
 // Generic masked kernel (fp32 exact-MFMA path and odd bf16 shapes).
@@ -1279,14 +704,6 @@ __global__ __launch_bounds__(256) void gemm_generic(const T* __restrict__ X, int
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
-// Largest physical row index a row map produces for logical rows [0, M).
-static int64_t max_phys_row(int M, const RowMap& m) {
-  if (M <= 0) return 0;
-  if (m.grp >= 0x7fffffff) return M - 1;
-  const int64_t last = M - 1;
-  return (last / m.grp) * m.gstride + m.off + (m.grp - 1);
-}
-
 static RowMap mk_map(int grp, int64_t gstride, int off) {
   RowMap r;
   r.grp = grp > 0 ? grp : 0x7fffffff;
@@ -1308,19 +725,14 @@ extern "C" int sdp_gemm_force_generic(int on) {
   return old;
 }
 
-// bf16 fast-kernel selection: 1 = 2-stage ring + 8-B stores, 3 = 2-stage ring + paired
-// 16-B stores, 5 = deep-X ring (3 X slots, 2 W slots, counted vmcnt) + 16-B stores,
-// 7 = 256x128 tiles, 3-slot ring, two blocks per CU, 8 = same with interleaved DMA,
-// 9 = 8-phase ping-pong 256x256, 11 = persistent form of 9, 12 / 13 = 9 / 11
-// with the whole-line LDS-staged epilogue,
-// 14 (default) = 12 with every row group staged before the first store (one LDS round
-// trip per wave; bit-identical to 12 and within +-2 % of it, order-balanced),
-// 4 / 10 = no-store timing probes of 3 / 9
-// (wrong results; benchmarks only).
+// bf16 fast-kernel selection: 14 (default) = 8-phase ping-pong 256x256 with the whole-line
+// LDS-staged epilogue (every row group staged before the first store); 9 = the same main
+// loop with the permlane-paired 16-B register epilogue (also the fallback for unaligned /
+// resid_pre-with-activation calls).  Other ids are refused (the old value is kept).
 static int g_fast_kernel = 14;
 extern "C" int sdp_gemm_set_fast_kernel(int k) {
   int old = g_fast_kernel;
-  if (k == 1 || k == 3 || k == 4 || k == 5 || (k >= 7 && k <= 14)) g_fast_kernel = k;
+  if (k == 9 || k == 14) g_fast_kernel = k;
   return old;
 }
 
@@ -1331,28 +743,18 @@ extern "C" int sdp_gemm_set_group_m(int gm) {
   return old;
 }
 
+static int g_exact_gelu = 0;
+extern "C" int sdp_gemm_set_exact_gelu(int on) {
+  int old = g_exact_gelu;
+  g_exact_gelu = on ? 1 : 0;
+  return old;
+}
+
 static int g_nt_store = 0;
 extern "C" int sdp_gemm_set_store_policy(int nt) {
   int old = g_nt_store;
   g_nt_store = nt ? 1 : 0;
   return old;
-}
-
-static int g_desync = 0;
-extern "C" int sdp_gemm_set_desync(int d) {
-  int old = g_desync;
-  g_desync = d < 0 ? 0 : d;
-  return old;
-}
-
-static int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  }
-  return n;
 }
 
 int sdp_row_partials(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, int M, int C,
@@ -1402,101 +804,41 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
   if (ln_colsum && (uintptr_t)ln_colsum % 16) return (int)hipErrorInvalidValue;
   if (dtype == 1) {
     Epi<bf16_t> e{bias, (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, act, resid_pre, ln_stats, ln_colsum, nullptr};
-    e.delay = g_desync;
     e.nt_store = g_nt_store;
     {
       const int tiles_n_ = (N + fast::BN - 1) / fast::BN;
       e.group_m = g_group_m >= 1 ? g_group_m : (tiles_n_ >= 8 ? 4 : 1);
     }
-    e.delay_blocks = num_cus();
     const bool aligned = (ldy % 4 == 0) && ((uintptr_t)Y % 8 == 0) && (!R || ((ldr % 4 == 0) && ((uintptr_t)R % 8 == 0))) &&
                          (!bias || ((uintptr_t)bias % 16 == 0)) && (ldx % 8 == 0) && ((uintptr_t)X % 16 == 0) &&
                          (ldw % 8 == 0) && ((uintptr_t)W % 16 == 0);
     if (!g_force_generic && aligned && sdp_gemm_variant(dtype, M, N, K) == 1) {
       const int tm = (M + fast::BM - 1) / fast::BM, tn = (N + fast::BN - 1) / fast::BN;
-#define SDP_FAST(A, E) hipLaunchKernelGGL((fast::gemm_bf16_256x256<A, E>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
-                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
-      if (g_fast_kernel == 7 || g_fast_kernel == 8) {
-        const int hm = (M + half::BM - 1) / half::BM, hn = (N + half::BN - 1) / half::BN;
-#define SDP_HALF(KN, A) hipLaunchKernelGGL((half::KN<A>), dim3(hm * hn), dim3(half::NT), 0, s, \
-                                           (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, hm, hn)
-        if (g_fast_kernel == 7) {
-          if (act == ACT_NONE) SDP_HALF(gemm_bf16_256x128, ACT_NONE);
-          else if (act == ACT_GELU) SDP_HALF(gemm_bf16_256x128, ACT_GELU);
-          else SDP_HALF(gemm_bf16_256x128, -1);
-        } else {
-          if (act == ACT_NONE) SDP_HALF(gemm_bf16_256x128i, ACT_NONE);
-          else if (act == ACT_GELU) SDP_HALF(gemm_bf16_256x128i, ACT_GELU);
-          else SDP_HALF(gemm_bf16_256x128i, -1);
-        }
-#undef SDP_HALF
-        return SDP_CHECK_LAUNCH();
-      }
-      if (g_fast_kernel == 10) {
-        hipLaunchKernelGGL((fast::gemm_bf16_8ph<ACT_NONE, 2>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,
-                           (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn);
-        return SDP_CHECK_LAUNCH();
-      }
       // the whole-line epilogue needs 16-B aligned output / residual rows and N % 8 == 0,
       // and implements resid_pre only without an activation
       const bool rows_ok = (N % 8 == 0) && (ldy % 8 == 0) && ((uintptr_t)Y % 16 == 0) &&
                            (!R || ((ldr % 8 == 0) && ((uintptr_t)R % 16 == 0))) && !(R && resid_pre && act != ACT_NONE);
-      const int fk = (!rows_ok && (g_fast_kernel == 12 || g_fast_kernel == 14)) ? 9
-                     : (!rows_ok && g_fast_kernel == 13) ? 11 : g_fast_kernel;
-      // persistent form: epilogues GELU / none only (the runtime-activation variant
-      // spills), 32-bit element offsets must cover both operands
-      if ((fk == 11 || fk == 13) && (act == ACT_NONE || act == ACT_GELU) &&
-          max_phys_row(M, xm) * ldx + K <= 0xffffffffLL && (int64_t)N * ldw <= 0xffffffffLL) {
-        const int nwg = tm * tn, ncu = num_cus();
-        const int grid = nwg <= ncu ? nwg : (ncu & ~7);
-#define SDP_8PHP(A, R) hipLaunchKernelGGL((fast::gemm_bf16_8php<A, R>), dim3(grid), dim3(fast::NTHREADS), 0, s, \
-                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
-        if (fk == 13) {
-          if (act == ACT_NONE) SDP_8PHP(ACT_NONE, true); else SDP_8PHP(ACT_GELU, true);
-        } else {
-          if (act == ACT_NONE) SDP_8PHP(ACT_NONE, false); else SDP_8PHP(ACT_GELU, false);
-        }
-#undef SDP_8PHP
-        return SDP_CHECK_LAUNCH();
+      const int fk = rows_ok ? g_fast_kernel : 9;
+      if (fk == 14 && part && N % 64 == 0) {  // the whole-line epilogue emits the row partial statistics
+        e.part = part;
+        if (part_done) *part_done = true;
       }
-      if (fk == 12 || fk == 14) {
-        if (part && N % 64 == 0) {  // the whole-line epilogue emits the row partial statistics
-          e.part = part;
-          if (part_done) *part_done = true;
-        }
 #define SDP_8PH(A, E) hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
                                          (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
-        if (fk == 14) {
-          if (act == ACT_NONE) SDP_8PH(ACT_NONE, 4); else if (act == ACT_GELU) SDP_8PH(ACT_GELU, 4); else SDP_8PH(-1, 4);
-        } else {
-          if (act == ACT_NONE) SDP_8PH(ACT_NONE, 3); else if (act == ACT_GELU) SDP_8PH(ACT_GELU, 3); else SDP_8PH(-1, 3);
-        }
-#undef SDP_8PH
-        return SDP_CHECK_LAUNCH();
-      }
-      if (fk == 9 || fk == 11 || fk == 13) {
-#define SDP_8PH(A) hipLaunchKernelGGL((fast::gemm_bf16_8ph<A>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
-                                      (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
-        if (act == ACT_NONE) SDP_8PH(ACT_NONE); else if (act == ACT_GELU) SDP_8PH(ACT_GELU); else SDP_8PH(-1);
-#undef SDP_8PH
-        return SDP_CHECK_LAUNCH();
-      }
-      if (g_fast_kernel == 5) {
-#define SDP_DEEP(A) hipLaunchKernelGGL((fast::gemm_bf16_deepx<A>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
-                                       (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
-        if (act == ACT_NONE) SDP_DEEP(ACT_NONE); else if (act == ACT_GELU) SDP_DEEP(ACT_GELU); else SDP_DEEP(-1);
-#undef SDP_DEEP
-        return SDP_CHECK_LAUNCH();
-      }
-      const int em = g_fast_kernel == 1 ? 0 : (g_fast_kernel == 4 ? 2 : 1);
-      if (em == 0) {
-        if (act == ACT_NONE) SDP_FAST(ACT_NONE, 0); else if (act == ACT_GELU) SDP_FAST(ACT_GELU, 0); else SDP_FAST(-1, 0);
-      } else if (em == 1) {
-        if (act == ACT_NONE) SDP_FAST(ACT_NONE, 1); else if (act == ACT_GELU) SDP_FAST(ACT_GELU, 1); else SDP_FAST(-1, 1);
+      // exact-erf GELU goes through the runtime-activation epilogue (apply_act)
+      const int ak = (act == ACT_GELU && g_exact_gelu) ? -1 : act;
+      if (fk == 14) {
+        if (ak == ACT_NONE) SDP_8PH(ACT_NONE, 4);
+        else if (ak == ACT_GELU) SDP_8PH(ACT_GELU, 4);
+        else if (ak == ACT_TANH) SDP_8PH(ACT_TANH, 4);
+        else SDP_8PH(-1, 4);
       } else {
-        SDP_FAST(ACT_NONE, 2);
+        if (ak == ACT_NONE) SDP_8PH(ACT_NONE, 1);
+        else if (ak == ACT_GELU) SDP_8PH(ACT_GELU, 1);
+        else if (ak == ACT_TANH) SDP_8PH(ACT_TANH, 1);
+        else SDP_8PH(-1, 1);
       }
-#undef SDP_FAST
+#undef SDP_8PH
     } else {
       dim3 grid((M + gen::BM - 1) / gen::BM, (N + gen::BN - 1) / gen::BN);
       hipLaunchKernelGGL(gen::gemm_generic<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)X, ldx, xm,

@@ -985,32 +985,25 @@ static int launch_dw3(int variant, int k, const void* X, int64_t ldx, RowMap xm,
   else                                                                                                           \
     hipLaunchKernelGGL((dwconv3_mfma<KS, NT, false, PF>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx, xm, \
                        stats, lg, lb, Wt, bias, (bf16_t*)Y, ldy, ym, B, H, W, C, ncg, ipb, nunits)
-  // 16 waves x 2 channels, 3 images in flight (variant 3) or 8 waves x 4 channels, 4 in flight (4)
-  if (variant == 4) {
-    switch (k) {
-      case 3: SDP_DW3(3, 512, 4); break;
-      case 5: SDP_DW3(5, 512, 4); break;
-      case 7: SDP_DW3(7, 512, 4); break;
-      default: return -1;
-    }
-  } else {
-    switch (k) {
-      case 3: SDP_DW3(3, 1024, 3); break;
-      case 5: SDP_DW3(5, 1024, 3); break;
-      case 7: SDP_DW3(7, 1024, 3); break;
-      default: return -1;
-    }
+  // 16 waves x 2 channels, 3 images in flight
+  (void)variant;
+  switch (k) {
+    case 3: SDP_DW3(3, 1024, 3); break;
+    case 5: SDP_DW3(5, 1024, 3); break;
+    case 7: SDP_DW3(7, 1024, 3); break;
+    default: return -1;
   }
 #undef SDP_DW3
   return SDP_CHECK_LAUNCH();
 }
 
-// 3 (default) / 4 = dwconv3_mfma (16 waves x 2 channels / 8 waves x 4 channels) where it
-// applies, 2 = dwconv2_nhwc, 1 = dwconv_ln_nhwc
+// Highest kernel tier allowed (each tier falls back to the next lower one per shape):
+// 3 (default) = dwconv3_mfma where it applies (bf16, H, W <= 16, C % 32 == 0, k in {3,5,7}),
+// 2 = dwconv2_nhwc (C % 8 == 0, 16-B rows), 1 = dwconv_ln_nhwc (any shape)
 static int g_dw_kernel = 3;
 extern "C" int sdp_dwconv_set_kernel(int k) {
   const int old = g_dw_kernel;
-  if (k >= 1 && k <= 4) g_dw_kernel = k;
+  if (k >= 1 && k <= 3) g_dw_kernel = k;
   return old;
 }
 

@@ -37,9 +37,9 @@ _SIGS = {
     "sdp_gemm_variant": ([_i32, _i32, _i32, _i32], _i32),
     "sdp_gemm_force_generic": ([_i32], _i32),
     "sdp_gemm_set_fast_kernel": ([_i32], _i32),
-    "sdp_gemm_set_desync": ([_i32], _i32),
     "sdp_gemm_set_store_policy": ([_i32], _i32),
     "sdp_gemm_set_group_m": ([_i32], _i32),
+    "sdp_gemm_set_exact_gelu": ([_i32], _i32),
     "sdp_layernorm": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _f32, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_qk_headnorm": ([_i32, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp], _i32),
     "sdp_rowstats": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _i32, _i32, _vp], _i32),
@@ -99,9 +99,6 @@ def lib():
         kern = os.environ.get("SDPNET_GEMM_KERNEL")  # A/B switch for the bf16 fast GEMM (benchmarks)
         if kern:
             L.sdp_gemm_set_fast_kernel(int(kern))
-        kern = os.environ.get("SDPNET_GEMM_DESYNC")  # first-round stagger of the GEMM blocks
-        if kern:
-            L.sdp_gemm_set_desync(int(kern))
         kern = os.environ.get("SDPNET_GEMM_NT_STORE")  # streaming output stores in the GEMM epilogue
         if kern:
             L.sdp_gemm_set_store_policy(int(kern))
@@ -120,6 +117,12 @@ def lib():
 
 def exported_symbols():
     return list(_SIGS.keys())
+
+
+def _req(cond, what: str = "argument check"):
+    """Boundary validation that survives ``python -O`` (unlike assert)."""
+    if not cond:
+        raise ValueError(f"sdpnet HIP op: invalid arguments ({what})")
 
 
 def _check(rc: int, name: str):
@@ -168,7 +171,7 @@ class Rows:
 
 
 def dense(t: torch.Tensor) -> Rows:
-    assert t.is_contiguous()
+    _req(t.is_contiguous())
     return Rows(t, t.shape[-1])
 
 
@@ -182,10 +185,10 @@ def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Option
     buffer [rows, ceil(N/64), 2] the output rows' {mean, M2} are written to."""
     _need_cuda(x.t, w, y.t, bias)
     dt = dcode(x.t.dtype)
-    assert w.dtype == x.t.dtype == y.t.dtype and w.is_contiguous() and w.shape[0] >= N
-    assert bias is None or (bias.dtype == torch.float32 and bias.is_contiguous())
+    _req(w.dtype == x.t.dtype == y.t.dtype and w.is_contiguous() and w.shape[0] >= N)
+    _req(bias is None or (bias.dtype == torch.float32 and bias.is_contiguous()))
     if resid is not None:
-        assert resid.t.dtype == x.t.dtype
+        _req(resid.t.dtype == x.t.dtype)
         r = [resid.t.data_ptr(), resid.ld, *resid.map()]
     else:
         r = [None, 0, 0, 0, 0]
@@ -198,8 +201,8 @@ def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Option
                             int(bool(resid_pre)), _stream(y.t))
     else:
         if ln is not None:
-            assert ln[0].dtype == ln[1].dtype == torch.float32 and ln[0].numel() >= 2 * M and ln[1].numel() >= N
-        assert part is None or part.dtype == torch.float32
+            _req(ln[0].dtype == ln[1].dtype == torch.float32 and ln[0].numel() >= 2 * M and ln[1].numel() >= N)
+        _req(part is None or part.dtype == torch.float32)
         rc = lib().sdp_gemm_ln(dt, *x.args(), w.data_ptr(), w.stride(0), _ptr(bias), *r, *y.args(), M, N, K, act,
                                int(bool(resid_pre)), _ptr(ln[0]) if ln else None, _ptr(ln[1]) if ln else None,
                                _ptr(part), _stream(y.t))
@@ -214,7 +217,7 @@ def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Option
 def layernorm(x: Rows, gamma: torch.Tensor, beta: torch.Tensor, eps: float, y: Rows, M: int, C: int):
     _need_cuda(x.t, y.t, gamma, beta)
     dt = dcode(x.t.dtype)
-    assert y.t.dtype == x.t.dtype and gamma.dtype == beta.dtype == torch.float32
+    _req(y.t.dtype == x.t.dtype and gamma.dtype == beta.dtype == torch.float32)
     rc = lib().sdp_layernorm(dt, *x.args(), gamma.data_ptr(), beta.data_ptr(), float(eps), *y.args(), M, C,
                              _stream(y.t))
     _check(rc, "layernorm")
@@ -230,7 +233,7 @@ def qk_headnorm(qkv: torch.Tensor, rows: int, n_head: int, head_dim: int, gq, bq
 def row_partials(x: Rows, M: int, C: int, part: torch.Tensor):
     """part[phys_row] = per-64-column {mean, M2} of the rows of x (LN statistics by parts)."""
     _need_cuda(x.t, part)
-    assert part.dtype == torch.float32
+    _req(part.dtype == torch.float32)
     rc = lib().sdp_row_partials(dcode(x.t.dtype), *x.args(), M, C, part.data_ptr(), _stream(part))
     _check(rc, "row_partials")
 
@@ -238,14 +241,14 @@ def row_partials(x: Rows, M: int, C: int, part: torch.Tensor):
 def ln_stats(part: torch.Tensor, rows: Rows, M: int, C: int, eps: float, stats: torch.Tensor):
     """stats[m] = (mean, rstd) of logical row m of ``rows`` (its map over ``part``'s physical rows)."""
     _need_cuda(part, stats)
-    assert part.dtype == stats.dtype == torch.float32 and stats.numel() >= 2 * M
+    _req(part.dtype == stats.dtype == torch.float32 and stats.numel() >= 2 * M)
     rc = lib().sdp_ln_stats(part.data_ptr(), *rows.map(), M, C, float(eps), stats.data_ptr(), _stream(stats))
     _check(rc, "ln_stats")
 
 
 def rowstats(x: Rows, eps: float, stats: torch.Tensor, M: int, C: int):
     _need_cuda(x.t, stats)
-    assert stats.dtype == torch.float32 and stats.numel() >= 2 * M
+    _req(stats.dtype == torch.float32 and stats.numel() >= 2 * M)
     rc = lib().sdp_rowstats(dcode(x.t.dtype), *x.args(), float(eps), stats.data_ptr(), M, C, _stream(stats))
     _check(rc, "rowstats")
 
@@ -254,7 +257,7 @@ def dwconv(x: Rows, weight: torch.Tensor, bias: Optional[torch.Tensor], y: Rows,
            k: int, stats: Optional[torch.Tensor] = None, ln_gamma: Optional[torch.Tensor] = None,
            ln_beta: Optional[torch.Tensor] = None):
     _need_cuda(x.t, y.t, weight, bias, stats)
-    assert weight.dtype == torch.float32 and weight.is_contiguous()
+    _req(weight.dtype == torch.float32 and weight.is_contiguous())
     rc = lib().sdp_dwconv(dcode(x.t.dtype), *x.args(), _ptr(stats), _ptr(ln_gamma), _ptr(ln_beta), weight.data_ptr(),
                           _ptr(bias), *y.args(), B, H, W, C, k, _stream(y.t))
     _check(rc, "dwconv")
@@ -266,7 +269,7 @@ def attention(qkv: torch.Tensor, out: torch.Tensor, B: int, N: int, n_head: int,
     """qk_norm = (q_gamma, q_beta, k_gamma, k_beta) fp32 or None.  NOTE: when the
     generic kernel is taken the norms are applied in place on ``qkv``."""
     _need_cuda(qkv, out, mask)
-    assert qkv.dtype == out.dtype
+    _req(qkv.dtype == out.dtype)
     gq, bq, gk, bk = qk_norm if qk_norm is not None else (None, None, None, None)
     rc = lib().sdp_attention(dcode(qkv.dtype), qkv.data_ptr(), qkv.stride(0), out.data_ptr(), out.stride(0), B, N,
                              n_head, head_dim, _ptr(gq), _ptr(bq), _ptr(gk), _ptr(bk), float(eps), _ptr(mask),
@@ -276,7 +279,7 @@ def attention(qkv: torch.Tensor, out: torch.Tensor, B: int, N: int, n_head: int,
 
 def patchify(img: torch.Tensor, out: torch.Tensor, p: int, kpad: int):
     _need_cuda(img, out)
-    assert img.is_contiguous() and img.dim() == 4 and img.shape[1] == 3
+    _req(img.is_contiguous() and img.dim() == 4 and img.shape[1] == 3)
     B, _, Hi, Wi = img.shape
     rc = lib().sdp_patchify(dcode(img.dtype), img.data_ptr(), dcode(out.dtype), out.data_ptr(), B, Hi, Wi, p, kpad,
                             _stream(out))
@@ -291,7 +294,7 @@ def pos_table(eh: torch.Tensor, ew: torch.Tensor, out: torch.Tensor, H: int, W: 
 
 def avgpool_table(bone: torch.Tensor, out: torch.Tensor, H: int, W: int, C: int, k: int):
     _need_cuda(bone, out)
-    assert bone.is_contiguous() and bone.dtype == torch.float32
+    _req(bone.is_contiguous() and bone.dtype == torch.float32)
     rc = lib().sdp_avgpool_table(bone.data_ptr(), bone.shape[-2], bone.shape[-1], out.data_ptr(), H, W, C, k,
                                  _stream(out))
     _check(rc, "avgpool_table")
@@ -309,7 +312,7 @@ def copy_rows(src: torch.Tensor, lds: int, sgstride: int, dst: torch.Tensor, ldd
 
 def nchw_add_table(x: torch.Tensor, table: torch.Tensor):
     _need_cuda(x, table)
-    assert x.is_contiguous() and table.dtype == torch.float32
+    _req(x.is_contiguous() and table.dtype == torch.float32)
     B, C, H, W = x.shape
     rc = lib().sdp_nchw_add_table(dcode(x.dtype), x.data_ptr(), table.data_ptr(), B, C, H * W, _stream(x))
     _check(rc, "nchw_add_table")
@@ -317,7 +320,7 @@ def nchw_add_table(x: torch.Tensor, table: torch.Tensor):
 
 def act(x: torch.Tensor, y: torch.Tensor, code: int):
     _need_cuda(x, y)
-    assert x.is_contiguous() and y.is_contiguous() and x.dtype == y.dtype
+    _req(x.is_contiguous() and y.is_contiguous() and x.dtype == y.dtype)
     rc = lib().sdp_act(dcode(x.dtype), x.data_ptr(), y.data_ptr(), x.numel(), code, _stream(y))
     _check(rc, "act")
 
@@ -331,7 +334,7 @@ def group_mean(x: Rows, out: torch.Tensor, G: int, rows: int, C: int):
 
 def nchw_to_rows(x: torch.Tensor, y: Rows):
     _need_cuda(x, y.t)
-    assert x.is_contiguous()
+    _req(x.is_contiguous())
     B, C, H, W = x.shape
     rc = lib().sdp_nchw_to_rows(dcode(x.dtype), x.data_ptr(), dcode(y.t.dtype), *y.args(), B, C, H * W,
                                 _stream(y.t))
@@ -340,7 +343,7 @@ def nchw_to_rows(x: torch.Tensor, y: Rows):
 
 def rows_to_nchw(x: Rows, y: torch.Tensor):
     _need_cuda(x.t, y)
-    assert y.is_contiguous()
+    _req(y.is_contiguous())
     B, C, H, W = y.shape
     rc = lib().sdp_rows_to_nchw(dcode(x.t.dtype), *x.args(), dcode(y.dtype), y.data_ptr(), B, C, H * W,
                                 _stream(y))
@@ -368,8 +371,8 @@ def fold_ln_weight(w: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, bia
                    dtype: torch.dtype):
     """(W * gamma cast to dtype, colsum [N] fp32, beta . W^T + bias [N] fp32) for sdp_gemm_ln."""
     _need_cuda(w, gamma, beta, bias)
-    assert w.dtype == gamma.dtype == beta.dtype == torch.float32 and w.is_contiguous() and w.dim() == 2
-    assert bias is None or (bias.dtype == torch.float32 and bias.is_contiguous())
+    _req(w.dtype == gamma.dtype == beta.dtype == torch.float32 and w.is_contiguous() and w.dim() == 2)
+    _req(bias is None or (bias.dtype == torch.float32 and bias.is_contiguous()))
     N, K = w.shape
     wf = torch.empty(N, K, dtype=dtype, device=w.device)
     colsum = torch.empty(N, dtype=torch.float32, device=w.device)
@@ -386,7 +389,7 @@ def val_preprocess(pix: torch.Tensor, offs: torch.Tensor, hw: torch.Tensor, resi
                    max_w: int = 0):
     """Batched validation transform (sdp_val_preprocess); returns (out NCHW, out_u8 or None)."""
     _need_cuda(pix, offs, hw)
-    assert pix.dtype == torch.uint8 and offs.dtype == torch.int64 and hw.dtype == torch.int32
+    _req(pix.dtype == torch.uint8 and offs.dtype == torch.int64 and hw.dtype == torch.int32)
     B = hw.shape[0]
     (RH, RW), (CH, CW) = resize, crop
     dev = pix.device
@@ -406,7 +409,7 @@ def val_preprocess(pix: torch.Tensor, offs: torch.Tensor, hw: torch.Tensor, resi
 def logits_metrics(logits: torch.Tensor, labels: torch.Tensor, label_smoothing: float = 0.0) -> torch.Tensor:
     """[B, 3] fp32: per-row cross-entropy, BCE-with-logits row sum, top-1 hit."""
     _need_cuda(logits, labels)
-    assert logits.dim() == 2 and logits.stride(1) == 1 and labels.dtype == torch.int64
+    _req(logits.dim() == 2 and logits.stride(1) == 1 and labels.dtype == torch.int64)
     B, C = logits.shape
     labels = labels.contiguous()
     out = torch.empty(B, 3, dtype=torch.float32, device=logits.device)

@@ -30,25 +30,6 @@ class StochasticDepth(torch.nn.Module):
         return x
 
 
-class StochasticDepth_2(torch.nn.Module):
-    """Whole-module drop path variant (utility_layers.py:32-59)."""
-
-    def __init__(self, module: torch.nn.Module, p: float = 0.2):
-        super().__init__()
-        assert 0 < p < 1, "p must be a positive number or <1"
-        self.p = float(p)
-        self.module = module
-
-    def forward(self, x: torch.Tensor, register: torch.Tensor):
-        x_new, register_new = self.module(x, register)
-        if self.training:
-            size = [1] * x.ndim
-            noise_x = torch.empty(size, dtype=x_new.dtype, device=x_new.device, requires_grad=False).bernoulli(1 - self.p).div(1 - self.p)
-            noise_register = noise_x.squeeze([-1, -2])
-            return x_new, noise_register * register_new
-        return x_new, register_new
-
-
 class SdPModel(nn.Module):
     """Base class with the reference's utility surface (utility_layers.py:93-198)."""
 

@@ -178,7 +178,7 @@ def test_qk_headnorm(dtype, H, hd):
                                        (1, 20, 37, 36, 9), (2, 3, 3, 8, 1)])
 @pytest.mark.parametrize("bias", [False, True])
 @pytest.mark.parametrize("ln", [False, True])
-@pytest.mark.parametrize("kern", [1, 2, 3, 4])
+@pytest.mark.parametrize("kern", [1, 2, 3])
 def test_dwconv(dtype, B, H, W, C, k, bias, ln, kern):
     x = rnd(B, C, H, W, dtype=dtype, seed=30, scale=2.0) + 0.5
     w = rnd(C, 1, k, k, seed=31, scale=0.2)
@@ -364,7 +364,7 @@ def test_nchw_add_table():
     assert torch.allclose(x, ref, atol=1e-6)
 
 
-@pytest.mark.parametrize("kern", [1, 3, 5, 7, 8, 9, 11, 12, 13, 14])
+@pytest.mark.parametrize("kern", [9, 14])
 @pytest.mark.parametrize("M,N,K,act,res", [(1000, 768, 768, 1, True), (300, 384, 128, 0, False),
                                            (777, 3072, 768, 1, False), (520, 768, 3072, 0, True),
                                            (256, 256, 64, 3, True), (600, 2304, 192, 0, False),
@@ -405,7 +405,7 @@ def test_row_partials_and_ln_stats(dtype, M, C):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
-@pytest.mark.parametrize("kern", [9, 12, 14])
+@pytest.mark.parametrize("kern", [9, 14])
 @pytest.mark.parametrize("M,N,K,act,has_b", [(600, 3072, 768, 1, False), (700, 768, 768, 0, True),
                                              (513, 2304, 768, 0, False), (100, 200, 128, 1, True)])
 def test_gemm_ln_fold(dtype, kern, M, N, K, act, has_b):
@@ -433,7 +433,7 @@ def test_gemm_ln_fold(dtype, kern, M, N, K, act, has_b):
     close(y, ref, dtype, rel=2e-5 if dtype == torch.float32 else 2e-2, what=f"ln-folded gemm kern {kern}")
 
 
-@pytest.mark.parametrize("kern", [9, 12, 14])
+@pytest.mark.parametrize("kern", [9, 14])
 @pytest.mark.parametrize("M,N,K", [(600, 768, 768), (257, 768, 3072), (90, 128, 256), (70, 100, 64)])
 def test_gemm_emits_row_partials(kern, M, N, K):
     """The residual GEMM's whole-line epilogue writes the output rows' LN partials
@@ -461,27 +461,3 @@ def test_gemm_emits_row_partials(kern, M, N, K):
         close(pr[:, c, 0], mu, torch.float32, rel=1e-5, what="emitted chunk mean")
         close(pr[:, c, 1], ((blk - mu[:, None]) ** 2).sum(1), torch.float32, rel=1e-4, what="emitted chunk M2")
     assert torch.isnan(part.view(B_, Nt, nch, 2)[:, :R]).all()  # register rows untouched
-
-
-@pytest.mark.parametrize("M,N,K,act,resid", [(5000, 768, 768, 1, True), (2100, 3072, 768, 1, False),
-                                             (1999, 768, 3072, 0, True)])
-def test_gemm_all_staged_epilogue_bit_identical(M, N, K, act, resid):
-    """Kernel 14 (every row group staged before the first store) runs the same arithmetic
-    as kernel 12 (one row group at a time): outputs and row partials are bit-identical."""
-    x = rnd(M, K, dtype=BF, seed=81)
-    w = rnd(N, K, dtype=BF, seed=82, scale=0.05)
-    r = rnd(M, N, dtype=BF, seed=83) if resid else None
-    outs = []
-    for kern in (12, 14):
-        y = torch.empty(M, N, dtype=BF, device=DEV)
-        part = torch.full((M, N // 64, 2), float("nan"), device=DEV)
-        old = sp.lib().sdp_gemm_set_fast_kernel(kern)
-        try:
-            sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, act=act, resid=None if r is None else sp.dense(r),
-                    part=part)
-        finally:
-            sp.lib().sdp_gemm_set_fast_kernel(old)
-        torch.cuda.synchronize()
-        outs.append((y, part))
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])

@@ -87,3 +87,29 @@ def test_two_rank_shards_match_single_process():
     assert abs(logits - ref).max() < 1e-5
     assert abs(logits - arr["logits"]).max() < 1e-4   # and the reference's own logits
     assert tmax == 2.0 and tsum == float(ref.shape[0])
+
+
+def test_bench_launcher_spawns_ranks():
+    """bench.py --gpus 2 (outside torch.distributed.run) must start two ranks as a child
+    torch.distributed.run and report n_gpus 2; --dry-run swaps the model for a trivial
+    CPU step on gloo so the launch / barrier / max-over-ranks path runs here."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run",
+                          "--steps", "3", "--warmup", "1"], capture_output=True, text=True, env=env, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["comm_world"] == 2 and rec["backend"] == "gloo"
+    assert rec["global_batch"] == 512
+    assert len({r["pid"] for r in rec["ranks"]}) == 2
+    assert [r["shard"] for r in rec["ranks"]] == [[0, 256], [256, 512]]
+    # a rank whose WORLD_SIZE disagrees with --gpus refuses to run
+    bad = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, env=dict(env, WORLD_SIZE="1"), timeout=120)
+    assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr

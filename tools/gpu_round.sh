@@ -20,13 +20,10 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) step benchq 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
-    gemm) step gemm 600 python tools/gemm_bench.py --streams 1 --kernels 12,13 ;;
     streams) step s1 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 1 &&
              step s2 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 2 &&
              step s3 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 3 &&
              step s4 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 4 ;;
-    ab) step ab8 600 env SDPNET_GEMM_KERNEL=9 python bench.py --steps 10 --warmup 3 --no-cpu-baseline &&
-        step ab9 600 env SDPNET_GEMM_KERNEL=12 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     kb) step kb 300 python tools/kern_bench.py ;;
     pmc) export TMPDIR=/tmp; rm -rf gpurun_out/pmc*
          step pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES -d gpurun_out/pmc1 -o run --output-format csv -- python tools/kern_bench.py --reps 3 &&
@@ -34,7 +31,7 @@ for s in "$@"; do
          step pmc3 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc3 -o run --output-format csv -- python tools/kern_bench.py --reps 3 &&
          step pmc4 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc4 -o run --output-format csv -- python tools/kern_bench.py --reps 3 ;;
     gpmc) export TMPDIR=/tmp; rm -rf gpurun_out/gpmc*
-         GB="python tools/gemm_bench.py --reps 2 --kernels 5,8 --shapes mixer_up,mixer_down,sq8192"
+         GB="python tools/gemm_bench.py --reps 2 --kernels 14 --shapes mixer_up,mixer_down,sq8192"
          step gpmcA 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAIT_INST_LDS -d gpurun_out/gpmcA -o run --output-format csv -- $GB &&
          step gpmcB 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_LDS_UNALIGNED_STALL GRBM_GUI_ACTIVE SQ_INSTS_VMEM -d gpurun_out/gpmcB -o run --output-format csv -- $GB &&
          step gpmcC 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/gpmcC -o run --output-format csv -- $GB &&
