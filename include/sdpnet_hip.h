@@ -252,6 +252,103 @@ int sdp_val_preprocess(const uint8_t* pix, const int64_t* offs, const int* hw, i
 int sdp_logits_metrics(int dtype, const void* X, int64_t ld, const int64_t* labels, int B, int C,
                        float label_smoothing, float* out, void* stream);
 
+/* ======================================================================================
+ * Training step (BASELINE.json configs[4]).  Replaces the autograd
+ * backward of the modules above under training_tools.py:85-99 (bf16 autocast forward,
+ * scaler.scale(loss).backward(), unscale_ + clip_grad_norm_(5), AdamW step), the train-mode
+ * StochasticDepth (utility_layers.py:16-27) and the dropouts (layers.py:291, :301-308).
+ * ====================================================================================== */
+
+/* Batched GEMM with either operand transposed (no transposed copies in HBM):
+ *   C[z](i, j) = alpha * sum_k A[z](i, k) B[z](k, j)  (+ C[z](i, j) if accum)
+ *   A(i, k) = ta ? A[k * lda + i] : A[i * lda + k];  B(k, j) = tb ? B[j * ldb + k] : B[k * ldb + j]
+ *   batch z < Z: operand offset (z / zdiv) * s1 + (z % zdiv) * s2 elements.
+ *   splits > 1: K is split into `splits` ranges (multiples of 32), range s writes its fp32
+ *   partial to C + s * split_stride (reduce with sdp_seg_colsum); accum must be 0 then.
+ * dtype 1 (bf16 operands, fp32 accumulate; out_dtype 0 fp32 / 1 bf16; 16-B vector loads where
+ * leading dims, batch strides and bases are 8-element aligned, element loads otherwise) or
+ * 0 (fp32, exact f32 MFMA).
+ * Used for dW = dY^T X of every Linear / 1x1 conv (layers.py:79-91, :242-249, :308), the
+ * patch-conv weight gradient (layers.py:34-42), dX = dY W, and the attention products of
+ * the train-mode forward and backward (layers.py:289-298). */
+int sdp_gemm_flex(int dtype, int out_dtype, int ta, int tb, const void* A, int64_t lda, int64_t sa1, int64_t sa2,
+                  const void* B, int64_t ldb, int64_t sb1, int64_t sb2, void* C, int64_t ldc, int64_t sc1,
+                  int64_t sc2, int M, int N, int K, int Z, int zdiv, int splits, int64_t split_stride, float alpha,
+                  int accum, void* stream);
+
+/* out[g * ldo + c] = scale * sum_{e < len} X[(g * gstride + e * estride) * ldx + c] (+ out if
+ * accum), fp32 out: bias / LayerNorm-affine / embedding-table gradients and split-K reduction. */
+int sdp_seg_colsum(int dtype, const void* X, int64_t ldx, int G, int len, int64_t gstride, int64_t estride, int C,
+                   float* out, int64_t ldo, float scale, int accum, void* stream);
+
+/* Y = act(Z) with dropout p (keep iff hash(seed, m * N + n) >= p, kept values / (1 - p));
+ * backward DZ = DY * mask / (1 - p) * act'(Z).  Exact-erf GELU.  p = 0: no mask.
+ * (layers.py:83-88 activation, :308 FFN dropouts, :445-454 head dropout.) */
+int sdp_act_fwd(int dtype, const void* Z, int64_t ldz, void* Y, int64_t ldy, int M, int N, int act, float p,
+                uint64_t seed, void* stream);
+int sdp_act_bwd(int dtype, const void* Z, int64_t ldz, const void* DY, int64_t lddy, void* DZ, int64_t lddz, int M,
+                int N, int act, float p, uint64_t seed, void* stream);
+
+/* Y[m] = X[m] * scale[m / sgrp] (+ R[m]) over row maps: per-sample drop path
+ * (StochasticDepth, utility_layers.py:16-27) on a residual branch; scale may be NULL. */
+int sdp_rowscale_add(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                     const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp, int64_t r_gstride, int r_off,
+                     void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int M, int N, void* stream);
+
+/* LayerNorm from given statistics (stats[2m] = mean, stats[2m+1] = rstd, from sdp_rowstats):
+ * Y = (X - mean) * rstd * gamma + beta; and its backward
+ * DX = rstd * (g.DY - mean(g.DY) - xhat * mean(g.DY * xhat)) (+ ADD), per-block partials
+ * part[b][0][c] = sum DY * xhat, part[b][1][c] = sum DY for b < sdp_ln_bwd_blocks(M) (C <= 2048).
+ * (layers.py:12-24 channel LN, :252-253 / :236-237 nn.LayerNorm, :445 head LN.) */
+int sdp_ln_apply(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                 const float* stats, const float* gamma, const float* beta, void* Y, int64_t ldy, int y_grp,
+                 int64_t y_gstride, int y_off, int M, int C, void* stream);
+int sdp_ln_bwd_blocks(int M);
+int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, const float* stats,
+               const float* gamma, const void* DY, int64_t lddy, int dy_grp, int64_t dy_gstride, int dy_off,
+               const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride, int a_off, void* DX, int64_t lddx,
+               int dx_grp, int64_t dx_gstride, int dx_off, int M, int C, float* part, void* stream);
+
+/* Attention rows (layers.py:289-298, SDPA dropout_p in training): P = softmax(scale * S[:, :N])
+ * (S fp32), Pd = P with dropout p (may be NULL), columns [N, Npad) zeroed; backward
+ * DS = P * (DPm - sum(DPm * P)), DPm = DPd with the same mask. */
+int sdp_softmax_fwd(int dtype, const float* S, int64_t lds, void* P, void* Pd, int64_t ldp, int rows, int N, int Npad,
+                    float scale, float p, uint64_t seed, void* stream);
+int sdp_softmax_bwd(int dtype, const void* P, int64_t ldp, const void* DPd, int64_t lddp, void* DS, int64_t ldds,
+                    int rows, int N, int Npad, float p, uint64_t seed, void* stream);
+
+/* Depthwise-conv weight gradient (layers.py:73-78): part[chunk][c][t] = sum over the chunk's
+ * images of DY[b, h, w, c] * A[b, h + ty - k/2, w + tx - k/2, c] (zero padded), NHWC rows,
+ * chunk < sdp_dw_wgrad_chunks(B); H * W <= 256, odd k <= 9.  The input gradient is
+ * sdp_dwconv with the kernel flipped. */
+int sdp_dw_wgrad_chunks(int B);
+int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, int64_t a_gstride, int a_off, const void* DY,
+                 int64_t lddy, int dy_grp, int64_t dy_gstride, int dy_off, int B, int H, int W, int C, int k,
+                 float* part, void* stream);
+
+/* Label-smoothed cross entropy, mean over B (nn.CrossEntropyLoss(label_smoothing),
+ * training_tools.py:76, :88): *loss += mean loss (fp32, atomic);
+ * dlogits = grad_scale / B * (softmax - ((1 - eps) onehot + eps / K)) (may be NULL). */
+int sdp_ce_loss(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K, float eps,
+                float grad_scale, void* dlogits, int64_t ldd, float* loss, void* stream);
+
+/* Multi-tensor optimizer step over fp32 tensors (device arrays of pointers / sizes and a
+ * block table of sdp_mt_block_bytes()-sized {int tensor; int64 start} entries, 4096
+ * elements per block):
+ *   sdp_grad_sumsq: state[0] += sum g^2, state[1] (int) = 1 on any non-finite g;
+ *   sdp_adamw: unless state[1] != 0 (GradScaler skip), g = grad * inv_scale * min(1,
+ *     max_norm / (sqrt(state[0]) * inv_scale + 1e-6)) (clip_grad_norm_, max_norm <= 0: off),
+ *     then torch.optim.AdamW (decoupled decay, bias corrections of step);
+ *   sdp_scaler_update: GradScaler.update on sc[0] = scale, sc[1] = growth tracker, resets state.
+ * (training_tools.py:91-99, :235.) */
+int sdp_mt_block_bytes(void);
+int sdp_grad_sumsq(float* const* grads, const int64_t* sizes, const void* blocks, int nblocks, float* state,
+                   void* stream);
+int sdp_adamw(float* const* params, float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+              const int64_t* sizes, const void* blocks, int nblocks, const float* state, float lr, float beta1,
+              float beta2, float eps, float weight_decay, int step, float inv_scale, float max_norm, void* stream);
+int sdp_scaler_update(float* state, float* scale_tracker, float growth, float backoff, int interval, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,983 @@
+// Training-step kernels of the SdP-Net path on gfx950 (BASELINE.json configs[4]: fwd + bwd +
+// AdamW).  Reference: the bf16-autocast forward + backward,
+// GradScaler, clip_grad_norm_(5) and AdamW of training_tools.py:77-103 / :230-259, the
+// train-mode StochasticDepth of utility_layers.py:16-27 and the dropouts of layers.py:291,
+// :301-308.
+//
+//  * gemm_flex — batched MFMA GEMM with either operand transposed, split-K partial slabs:
+//      C[z](i, j) = alpha * sum_k A[z](i, k) * B[z](k, j)
+//      A(i, k) = TA ? A[k * lda + i] : A[i * lda + k];  B(k, j) = TB ? B[j * ldb + k] : B[k * ldb + j]
+//    bf16: 128x128x32 tiles, 4 waves (64x64 each, v_mfma_f32_16x16x32_bf16).  An operand
+//    whose K runs along its rows ([i][k], [j][k]) is staged as [row][32] 64-B rows and read
+//    with ds_read_b128; one whose K runs down its columns ([k][i], [k][j]) is staged as it
+//    lies ([32][128] 256-B rows) and read with ds_read_b64_tr_b16, the hardware transpose
+//    (no transposed copy in HBM).  fp32: v_mfma_f32_16x16x4_f32 (exact f32), scalar LDS reads.
+//    Covers dW = dY^T X (both operands k-major), the attention products of the backward
+//    (S = QK^T, O = PV, dV = P^T dO, dP = dO V^T, dQ = dS K, dK = dS^T Q) and dX = dY W.
+//  * seg_colsum — out[g][c] = sum over a strided segment of rows (bias / LayerNorm-affine /
+//    embedding-table gradients, split-K slab reduction).
+//  * act_fwd / act_bwd with a counter-hash dropout mask (regenerated, never stored).
+//  * ln_apply (LayerNorm with given statistics), ln_bwd (dx + per-block dgamma/dbeta partials).
+//  * softmax_fwd / softmax_bwd over attention rows (with attention dropout).
+//  * dw_wgrad — depthwise-conv weight gradient (per-channel correlation).
+//  * ce_loss — label-smoothed cross entropy (training_tools.py:76) loss and dlogits.
+//  * sumsq / adamw — fused gradient norm (clip_grad_norm_, unscale, inf check) and the
+//    multi-tensor AdamW update (torch.optim.AdamW semantics), no host synchronisation.
+#include "common.h"
+
+static RowMap mk_tmap(int grp, int64_t gstride, int off) {
+  RowMap r;
+  r.grp = grp > 0 ? grp : 0x7fffffff;
+  r.gstride = grp > 0 ? gstride : 0;
+  r.off = grp > 0 ? off : 0;
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// counter-hash RNG for dropout / drop-path masks: keep(seed, idx) = u(seed, idx) >= p
+// ---------------------------------------------------------------------------
+SDP_DEV uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+SDP_DEV float uniform01(uint64_t seed, uint64_t idx) {
+  const uint32_t h = mix32((uint32_t)idx ^ mix32((uint32_t)seed ^ mix32((uint32_t)(idx >> 32) + (uint32_t)(seed >> 32) * 0x9e3779b9U)));
+  return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+// ---------------------------------------------------------------------------
+// gemm_flex
+// ---------------------------------------------------------------------------
+namespace flex {
+constexpr int BI = 128, BJ = 128, BK = 32, NT = 256;
+constexpr int TILE = 8192;  // bytes per operand tile (bf16: 128 x 32 x 2)
+
+// [128][32] bf16, 64-B rows: 16-B chunk c of row r at c ^ H[(r >> 2) & 3], H = {0, 2, 3, 1}
+// (conflict-free ds_read_b128 for the 16x16x32 operand map: lane -> row l & 15, chunk l >> 4)
+SDP_DEV int rr_off(int r, int c) { return r * 64 + ((c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3)) << 4); }
+// [32][128] bf16, 256-B rows, XOR image for ds_read_b64_tr_b16 (one image serves row and
+// transposed reads; cdna_hip_programming.md T10 layout (b))
+SDP_DEV int tr_off(int r, int ch) { return r * 256 + ((ch ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 4); }
+
+struct Op {
+  const void* p;
+  int64_t ld;
+  int64_t s1, s2;  // batch strides: z -> (z / zdiv) * s1 + (z % zdiv) * s2
+  int vec;         // rows 16-B aligned: 8-element vector loads (else element loads)
+};
+
+SDP_DEV int64_t zoff(const Op& o, int z, int zdiv) { return (int64_t)(z / zdiv) * o.s1 + (int64_t)(z % zdiv) * o.s2; }
+
+// Load 8 consecutive bf16 (along the contiguous axis) of logical row `row`, starting at
+// contiguous index `c0`; zero outside [0, nrow) x [0, ncol).
+SDP_DEV bf16x8 load8(const bf16_t* base, int64_t ld, int row, int nrow, int c0, int ncol, int vec) {
+  bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (row >= nrow) return v;
+  const bf16_t* p = base + (int64_t)row * ld + c0;
+  if (vec && c0 + 8 <= ncol) return *(const bf16x8*)p;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (c0 + e < ncol) v[e] = (short)p[e];
+  return v;
+}
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+template <bool TR>
+SDP_DEV bf16x8 frag(const char* tile, int rbase, int lane) {
+  if constexpr (!TR) {
+    return *(const bf16x8*)(tile + rr_off(rbase + (lane & 15), lane >> 4));
+  } else {
+    // rbase = first column (multiple of 16) of the 16-wide block; K rows 8g .. 8g+7
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    const int ch = (rbase >> 3) + (p >> 1);
+    const char* a0 = tile + tr_off(8 * g + q, ch) + 8 * (p & 1);
+    const char* a1 = tile + tr_off(8 * g + 4 + q, ch) + 8 * (p & 1);
+    v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((AS3 v4i16*)(a0));
+    v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((AS3 v4i16*)(a1));
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+}
+
+// Stage one operand tile (128 along i/j, 32 along k) into LDS; the loads for the NEXT
+// k-step are issued into registers first (reg), then written after the MFMAs.
+template <bool KMAJ>  // KMAJ: the operand's k runs down its rows ([k][i]) -> [32][128] image
+SDP_DEV void gload(bf16x8 (&reg)[2], const bf16_t* base, int64_t ld, int r0, int nr, int k0, int K, int tid,
+                   int vec) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int idx = tid + s * NT;
+    if constexpr (!KMAJ) {
+      const int row = idx >> 2, c = idx & 3;  // row of 128, chunk of 8 k
+      reg[s] = load8(base, ld, r0 + row, nr, k0 + 8 * c, K, vec);
+    } else {
+      const int kr = idx >> 4, ch = idx & 15;  // k row of 32, chunk of 8 along i
+      reg[s] = load8(base, ld, k0 + kr, K, r0 + 8 * ch, nr, vec);
+    }
+  }
+}
+template <bool KMAJ>
+SDP_DEV void lstore(const bf16x8 (&reg)[2], char* tile, int tid) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int idx = tid + s * NT;
+    if constexpr (!KMAJ) *(bf16x8*)(tile + rr_off(idx >> 2, idx & 3)) = reg[s];
+    else *(bf16x8*)(tile + tr_off(idx >> 4, idx & 15)) = reg[s];
+  }
+}
+
+template <typename TO>
+SDP_DEV void cstore(TO* C, int64_t ldc, int i, int j, int Mi, int Nj, float v, bool accum) {
+  if (i >= Mi || j >= Nj) return;
+  TO* p = C + (int64_t)i * ldc + j;
+  if (accum) v += to_f<TO>(*p);
+  *p = from_f<TO>(v);
+}
+
+// TA: A stored [k][i] (else [i][k]); TB: B stored [j][k] (else [k][j])
+template <bool TA, bool TB, typename TO>
+__global__ __launch_bounds__(NT) void gemm_flex_bf16(Op A, Op B, Op Cc, int Mi, int Nj, int K, int zdiv,
+                                                     int splits, int kchunk, int64_t split_stride, float alpha,
+                                                     int accum) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wi = wave >> 1, wj = wave & 1;
+  const int i0 = blockIdx.y * BI, j0 = blockIdx.x * BJ;
+  const int z = blockIdx.z / splits, sk = blockIdx.z % splits;
+  const int kb = sk * kchunk, ke = min(K, kb + kchunk);
+  const bf16_t* Ap = (const bf16_t*)A.p + zoff(A, z, zdiv);
+  const bf16_t* Bp = (const bf16_t*)B.p + zoff(B, z, zdiv);
+  TO* Cp = (TO*)Cc.p + zoff(Cc, z, zdiv) + (int64_t)sk * split_stride;
+  // A operand: rows i (KMAJ = TA); B operand: rows j (KMAJ = !TB)
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ra[2], rb[2];
+  if (kb < ke) {
+    gload<TA>(ra, Ap, A.ld, i0, Mi, kb, ke, tid, A.vec);
+    gload<!TB>(rb, Bp, B.ld, j0, Nj, kb, ke, tid, B.vec);
+    lstore<TA>(ra, smem, tid);
+    lstore<!TB>(rb, smem + TILE, tid);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    const bool more = k0 + BK < ke;
+    if (more) {
+      gload<TA>(ra, Ap, A.ld, i0, Mi, k0 + BK, ke, tid, A.vec);
+      gload<!TB>(rb, Bp, B.ld, j0, Nj, k0 + BK, ke, tid, B.vec);
+    }
+    const char* at = smem + buf * 2 * TILE;
+    const char* bt = at + TILE;
+    bf16x8 fa[4], fb[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) fa[t] = frag<TA>(at, wi * 64 + t * 16, lane);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) fb[t] = frag<!TB>(bt, wj * 64 + t * 16, lane);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+    if (more) {
+      char* nt = smem + (buf ^ 1) * 2 * TILE;
+      lstore<TA>(ra, nt, tid);
+      lstore<!TB>(rb, nt + TILE, tid);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  // D[i][j]: lane holds i = 4 * (lane >> 4) + r, j = lane & 15 of each 16x16 tile
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + wi * 64 + a * 16 + 4 * (lane >> 4) + r;
+        const int j = j0 + wj * 64 + b * 16 + (lane & 15);
+        cstore<TO>(Cp, Cc.ld, i, j, Mi, Nj, alpha * acc[a][b][r], accum != 0);
+      }
+}
+
+// fp32 (exact f32 MFMA): operands staged in their stored orientation, scalar LDS reads
+constexpr int FK = 16;
+template <bool TA, bool TB>
+__global__ __launch_bounds__(NT) void gemm_flex_f32(Op A, Op B, Op Cc, int Mi, int Nj, int K, int zdiv, int splits,
+                                                    int kchunk, int64_t split_stride, float alpha, int accum) {
+  // [i][k] pitch 17 or [k][i] pitch 132 floats (both 2176 / 2112 floats, <= 2176)
+  __shared__ float as[2176], bs[2176];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wi = wave >> 1, wj = wave & 1;
+  const int i0 = blockIdx.y * BI, j0 = blockIdx.x * BJ;
+  const int z = blockIdx.z / splits, sk = blockIdx.z % splits;
+  const int kb = sk * kchunk, ke = min(K, kb + kchunk);
+  const float* Ap = (const float*)A.p + zoff(A, z, zdiv);
+  const float* Bp = (const float*)B.p + zoff(B, z, zdiv);
+  float* Cp = (float*)Cc.p + zoff(Cc, z, zdiv) + (int64_t)sk * split_stride;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // logical element (r in 0..127 along i/j, k in 0..15)
+  auto stage = [&](float* s, const float* base, int64_t ld, int r0, int nr, int k0, bool kmaj) {
+    for (int e = tid; e < 128 * FK; e += NT) {
+      int r, k;
+      if (kmaj) { k = e >> 7; r = e & 127; } else { r = e >> 4; k = e & 15; }
+      const int gr = r0 + r, gk = k0 + k;
+      float v = 0.f;
+      if (gr < nr && gk < ke) v = kmaj ? base[(int64_t)gk * ld + gr] : base[(int64_t)gr * ld + gk];
+      if (kmaj) s[k * 132 + r] = v; else s[r * 17 + k] = v;
+    }
+  };
+  for (int k0 = kb; k0 < ke; k0 += FK) {
+    stage(as, Ap, A.ld, i0, Mi, k0, TA);
+    stage(bs, Bp, B.ld, j0, Nj, k0, !TB);
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < FK; kk += 4) {
+      float fa[4], fb[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int i = wi * 64 + t * 16 + (lane & 15), k = kk + (lane >> 4);
+        fa[t] = TA ? as[k * 132 + i] : as[i * 17 + k];
+        const int j = wj * 64 + t * 16 + (lane & 15);
+        fb[t] = !TB ? bs[k * 132 + j] : bs[j * 17 + k];
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a], fb[b], acc[a][b], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + wi * 64 + a * 16 + 4 * (lane >> 4) + r;
+        const int j = j0 + wj * 64 + b * 16 + (lane & 15);
+        cstore<float>(Cp, Cc.ld, i, j, Mi, Nj, alpha * acc[a][b][r], accum != 0);
+      }
+}
+}  // namespace flex
+
+extern "C" int sdp_gemm_flex(int dtype, int out_dtype, int ta, int tb, const void* A, int64_t lda, int64_t sa1,
+                             int64_t sa2, const void* B, int64_t ldb, int64_t sb1, int64_t sb2, void* C, int64_t ldc,
+                             int64_t sc1, int64_t sc2, int M, int N, int K, int Z, int zdiv, int splits,
+                             int64_t split_stride, float alpha, int accum, void* stream) {
+  if (!A || !B || !C || M < 0 || N < 0 || K < 0 || Z < 0 || zdiv <= 0 || splits <= 0) return (int)hipErrorInvalidValue;
+  if (M == 0 || N == 0 || Z == 0) return 0;
+  if (dtype == 1) {
+    if (out_dtype != 0 && out_dtype != 1) return (int)hipErrorInvalidValue;
+  } else if (dtype == 0) {
+    if (out_dtype != 0) return (int)hipErrorInvalidValue;
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  if (splits > 1 && accum) return (int)hipErrorInvalidValue;
+  int kchunk = (K + splits - 1) / splits;
+  const int kq = dtype == 1 ? flex::BK : flex::FK;
+  kchunk = (kchunk + kq - 1) / kq * kq;
+  // 16-B vector loads where leading dimensions, batch strides and bases are 8-element aligned
+  const int va = !(lda % 8 || sa1 % 8 || sa2 % 8 || ((uintptr_t)A % 16));
+  const int vb = !(ldb % 8 || sb1 % 8 || sb2 % 8 || ((uintptr_t)B % 16));
+  flex::Op a{A, lda, sa1, sa2, va}, b{B, ldb, sb1, sb2, vb}, c{C, ldc, sc1, sc2, 0};
+  dim3 grid((N + flex::BJ - 1) / flex::BJ, (M + flex::BI - 1) / flex::BI, Z * splits);
+  hipStream_t s = (hipStream_t)stream;
+#define SDP_FLEX(KN, TA_, TB_, ...)                                                                                 \
+  hipLaunchKernelGGL((flex::KN<TA_, TB_, ##__VA_ARGS__>), grid, dim3(flex::NT), 0, s, a, b, c, M, N, K, zdiv, splits, \
+                     kchunk, split_stride, alpha, accum)
+  if (dtype == 1) {
+    if (out_dtype == 0) {
+      if (!ta && !tb) SDP_FLEX(gemm_flex_bf16, false, false, float);
+      else if (!ta && tb) SDP_FLEX(gemm_flex_bf16, false, true, float);
+      else if (ta && !tb) SDP_FLEX(gemm_flex_bf16, true, false, float);
+      else SDP_FLEX(gemm_flex_bf16, true, true, float);
+    } else {
+      if (!ta && !tb) SDP_FLEX(gemm_flex_bf16, false, false, bf16_t);
+      else if (!ta && tb) SDP_FLEX(gemm_flex_bf16, false, true, bf16_t);
+      else if (ta && !tb) SDP_FLEX(gemm_flex_bf16, true, false, bf16_t);
+      else SDP_FLEX(gemm_flex_bf16, true, true, bf16_t);
+    }
+  } else {
+    if (!ta && !tb) SDP_FLEX(gemm_flex_f32, false, false);
+    else if (!ta && tb) SDP_FLEX(gemm_flex_f32, false, true);
+    else if (ta && !tb) SDP_FLEX(gemm_flex_f32, true, false);
+    else SDP_FLEX(gemm_flex_f32, true, true);
+  }
+#undef SDP_FLEX
+  return SDP_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// seg_colsum: out[g * ldo + c] (+)= sum_{e < len} X[row(g, e) * ldx + c],
+// row(g, e) = g * gstride + e * estride (in rows).  fp32 accumulation.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void seg_colsum_k(const T* __restrict__ X, int64_t ldx, int G, int len,
+                                                    int64_t gstride, int64_t estride, int C, float* __restrict__ out,
+                                                    int64_t ldo, float scale, int accum) {
+  // block: 64 columns x 4 row slices; grid (ceil(C/64), G)
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), sl = threadIdx.x >> 6, g = blockIdx.y;
+  float s = 0.f;
+  if (c < C) {
+    const T* p = X + (int64_t)g * gstride * ldx + c;
+    for (int e = sl; e < len; e += 4) s += to_f<T>(p[(int64_t)e * estride * ldx]);
+  }
+  red[sl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sl == 0 && c < C) {
+    const float v = scale * (red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
+    float* o = out + (int64_t)g * ldo + c;
+    *o = accum ? *o + v : v;
+  }
+}
+
+extern "C" int sdp_seg_colsum(int dtype, const void* X, int64_t ldx, int G, int len, int64_t gstride,
+                              int64_t estride, int C, float* out, int64_t ldo, float scale, int accum, void* stream) {
+  if (!X || !out || G < 0 || len < 0 || C < 0) return (int)hipErrorInvalidValue;
+  if (G == 0 || C == 0) return 0;
+  dim3 grid((C + 63) / 64, G);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 1)
+    hipLaunchKernelGGL(seg_colsum_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)X, ldx, G, len, gstride, estride, C,
+                       out, ldo, scale, accum);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(seg_colsum_k<float>, grid, dim3(256), 0, s, (const float*)X, ldx, G, len, gstride, estride, C,
+                       out, ldo, scale, accum);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// activation forward / backward with dropout (rows of a [M, N] matrix, row stride ld)
+//   fwd: y = act(z) * (keep ? 1 / (1 - p) : 0)           (p = 0: no mask)
+//   bwd: dz = dy * (keep ? 1 / (1 - p) : 0) * act'(z)
+// keep = uniform01(seed, m * N + n) >= p.  Exact-erf GELU (nn.GELU(), model.py:15).
+// ---------------------------------------------------------------------------
+SDP_DEV float act_grad(int act, float x) {
+  switch (act) {
+    case ACT_GELU: {
+      const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+      return cdf + x * 0.3989422804014327f * expf(-0.5f * x * x);
+    }
+    case ACT_RELU: return x > 0.0f ? 1.0f : 0.0f;
+    case ACT_TANH: { const float t = tanhf(x); return 1.0f - t * t; }
+    case ACT_SIGMOID: { const float s = 1.0f / (1.0f + expf(-x)); return s * (1.0f - s); }
+    case ACT_LEAKY_RELU: return x > 0.0f ? 1.0f : 0.01f;
+    case ACT_SELU: {
+      const float alpha = 1.6732632423543772848f, scale = 1.0507009873554804934f;
+      return x > 0.0f ? scale : scale * alpha * expf(x);
+    }
+    case ACT_KELU: {
+      const float a = 3.5f, k = 3.14159265358979323846f / a;
+      if (x < -a) return 0.0f;
+      if (x > a) return 1.0f;
+      return 0.5f * (1.0f + 2.0f * x / a + 0.31830988618379067f * sinf(k * x) + x * cosf(k * x) / a);
+    }
+    default: return 1.0f;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void act_fwd_k(const T* __restrict__ Z, int64_t ldz, T* __restrict__ Y, int64_t ldy,
+                                                 int M, int N, int act, float p, uint64_t seed) {
+  const int64_t total = (int64_t)M * N;
+  const float inv = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t m = e / N, n = e % N;
+    float v = apply_act(act, to_f<T>(Z[m * ldz + n]));
+    if (p > 0.f) v = uniform01(seed, e) >= p ? v * inv : 0.f;
+    Y[m * ldy + n] = from_f<T>(v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void act_bwd_k(const T* __restrict__ Z, int64_t ldz, const T* __restrict__ DY,
+                                                 int64_t lddy, T* __restrict__ DZ, int64_t lddz, int M, int N, int act,
+                                                 float p, uint64_t seed) {
+  const int64_t total = (int64_t)M * N;
+  const float inv = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t m = e / N, n = e % N;
+    float g = to_f<T>(DY[m * lddy + n]);
+    if (p > 0.f) g = uniform01(seed, e) >= p ? g * inv : 0.f;
+    DZ[m * lddz + n] = from_f<T>(g * act_grad(act, to_f<T>(Z[m * ldz + n])));
+  }
+}
+
+static int ew_grid(int64_t total) {
+  int64_t g = (total + 255) / 256;
+  return (int)(g < 16384 ? (g > 0 ? g : 1) : 16384);
+}
+
+extern "C" int sdp_act_fwd(int dtype, const void* Z, int64_t ldz, void* Y, int64_t ldy, int M, int N, int act, float p,
+                           uint64_t seed, void* stream) {
+  if (!Z || !Y || M < 0 || N < 0 || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;
+  if ((int64_t)M * N == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int g = ew_grid((int64_t)M * N);
+  if (dtype == 1)
+    hipLaunchKernelGGL(act_fwd_k<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)Z, ldz, (bf16_t*)Y, ldy, M, N, act, p, seed);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(act_fwd_k<float>, dim3(g), dim3(256), 0, s, (const float*)Z, ldz, (float*)Y, ldy, M, N, act, p, seed);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+extern "C" int sdp_act_bwd(int dtype, const void* Z, int64_t ldz, const void* DY, int64_t lddy, void* DZ, int64_t lddz,
+                           int M, int N, int act, float p, uint64_t seed, void* stream) {
+  if (!Z || !DY || !DZ || M < 0 || N < 0 || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;
+  if ((int64_t)M * N == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int g = ew_grid((int64_t)M * N);
+  if (dtype == 1)
+    hipLaunchKernelGGL(act_bwd_k<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)Z, ldz, (const bf16_t*)DY, lddy,
+                       (bf16_t*)DZ, lddz, M, N, act, p, seed);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(act_bwd_k<float>, dim3(g), dim3(256), 0, s, (const float*)Z, ldz, (const float*)DY, lddy,
+                       (float*)DZ, lddz, M, N, act, p, seed);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// Per-sample row scaling (drop path, utility_layers.py:16-27): y[m] = x[m] * scale[m / grp]
+// plus an optional residual: y = x * s + r.  In place allowed (y == x).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void rowscale_k(const T* __restrict__ X, int64_t ldx, RowMap xm,
+                                                  const float* __restrict__ sc, int sgrp, const T* __restrict__ R,
+                                                  int64_t ldr, RowMap rm, T* __restrict__ Y, int64_t ldy, RowMap ym,
+                                                  int M, int N) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t m = e / N, n = e % N;
+    float v = to_f<T>(X[xm(m) * ldx + n]) * (sc ? sc[m / sgrp] : 1.0f);
+    if (R) v += to_f<T>(R[rm(m) * ldr + n]);
+    Y[ym(m) * ldy + n] = from_f<T>(v);
+  }
+}
+
+extern "C" int sdp_rowscale_add(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                                const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp, int64_t r_gstride,
+                                int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int M, int N,
+                                void* stream) {
+  if (!X || !Y || M < 0 || N < 0 || (scale && sgrp <= 0)) return (int)hipErrorInvalidValue;
+  if ((int64_t)M * N == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), rm = mk_tmap(r_grp, r_gstride, r_off),
+               ym = mk_tmap(y_grp, y_gstride, y_off);
+  const int g = ew_grid((int64_t)M * N);
+  if (dtype == 1)
+    hipLaunchKernelGGL(rowscale_k<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)X, ldx, xm, scale, sgrp,
+                       (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, M, N);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(rowscale_k<float>, dim3(g), dim3(256), 0, s, (const float*)X, ldx, xm, scale, sgrp,
+                       (const float*)R, ldr, rm, (float*)Y, ldy, ym, M, N);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm with given statistics (stats[2m] = mean, stats[2m+1] = rstd): y = (x - mean) * rstd * g + b
+// and its backward.  One wave per row, any C.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void ln_apply_k(const T* __restrict__ X, int64_t ldx, RowMap xm,
+                                                  const float* __restrict__ st, const float* __restrict__ g,
+                                                  const float* __restrict__ b, T* __restrict__ Y, int64_t ldy,
+                                                  RowMap ym, int M, int C) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const float mean = st[2 * m], rstd = st[2 * m + 1];
+  const T* xp = X + xm(m) * ldx;
+  T* yp = Y + ym(m) * ldy;
+  for (int c = lane; c < C; c += 64) yp[c] = from_f<T>((to_f<T>(xp[c]) - mean) * rstd * g[c] + b[c]);
+}
+
+// dx = rstd * (gdy - mean(gdy) - xhat * mean(gdy * xhat)) [+ add];  per-block partials of
+// dgamma = sum dy * xhat, dbeta = sum dy in part[blockIdx.x][2][C] (C <= 2048).
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ X, int64_t ldx, RowMap xm,
+                                                const float* __restrict__ st, const float* __restrict__ g,
+                                                const T* __restrict__ DY, int64_t lddy, RowMap dym,
+                                                const T* __restrict__ ADD, int64_t ldadd, RowMap am,
+                                                T* __restrict__ DX, int64_t lddx, RowMap dxm, int M, int C,
+                                                float* __restrict__ part) {
+  constexpr int MAXV = 32;  // C <= 2048
+  __shared__ float red[2][4][2048];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float dg[MAXV], db[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) dg[i] = db[i] = 0.f;
+  const int nv = (C + 63) / 64;
+  for (int64_t m = (int64_t)blockIdx.x * 4 + w; m < M; m += (int64_t)gridDim.x * 4) {
+    const float mean = st[2 * m], rstd = st[2 * m + 1];
+    const T* xp = X + xm(m) * ldx;
+    const T* dyp = DY + dym(m) * lddy;
+    float xh[MAXV], gd[MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      xh[i] = gd[i] = 0.f;
+      if (i < nv && c < C) {
+        const float dy = to_f<T>(dyp[c]);
+        xh[i] = (to_f<T>(xp[c]) - mean) * rstd;
+        gd[i] = dy * g[c];
+        dg[i] += dy * xh[i];
+        db[i] += dy;
+        s1 += gd[i];
+        s2 += gd[i] * xh[i];
+      }
+    }
+    s1 = wave_sum(s1) / (float)C;
+    s2 = wave_sum(s2) / (float)C;
+    T* dxp = DX + dxm(m) * lddx;
+    const T* ap = ADD ? ADD + am(m) * ldadd : nullptr;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (i < nv && c < C) {
+        float v = rstd * (gd[i] - s1 - xh[i] * s2);
+        if (ap) v += to_f<T>(ap[c]);
+        dxp[c] = from_f<T>(v);
+      }
+    }
+  }
+  if (!part) return;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (i < nv && c < C) {
+      red[0][w][c] = dg[i];
+      red[1][w][c] = db[i];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    part[(int64_t)blockIdx.x * 2 * C + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    part[(int64_t)blockIdx.x * 2 * C + C + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+  }
+}
+
+extern "C" int sdp_ln_apply(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                            const float* stats, const float* gamma, const float* beta, void* Y, int64_t ldy, int y_grp,
+                            int64_t y_gstride, int y_off, int M, int C, void* stream) {
+  if (!X || !Y || !stats || !gamma || !beta || M < 0 || C <= 0) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), ym = mk_tmap(y_grp, y_gstride, y_off);
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((M + 3) / 4);
+  if (dtype == 1)
+    hipLaunchKernelGGL(ln_apply_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)X, ldx, xm, stats, gamma, beta,
+                       (bf16_t*)Y, ldy, ym, M, C);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(ln_apply_k<float>, grid, dim3(256), 0, s, (const float*)X, ldx, xm, stats, gamma, beta,
+                       (float*)Y, ldy, ym, M, C);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// Number of partial blocks sdp_ln_bwd uses for M rows (part needs nblk * 2 * C floats).
+extern "C" int sdp_ln_bwd_blocks(int M) {
+  int b = (M + 3) / 4;
+  return b < 1024 ? (b > 0 ? b : 1) : 1024;
+}
+
+extern "C" int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                          const float* stats, const float* gamma, const void* DY, int64_t lddy, int dy_grp,
+                          int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,
+                          int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride, int dx_off, int M, int C,
+                          float* part, void* stream) {
+  if (!X || !stats || !gamma || !DY || !DX || M < 0 || C <= 0 || C > 2048) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), dym = mk_tmap(dy_grp, dy_gstride, dy_off),
+               am = mk_tmap(a_grp, a_gstride, a_off), dxm = mk_tmap(dx_grp, dx_gstride, dx_off);
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(sdp_ln_bwd_blocks(M));
+  if (dtype == 1)
+    hipLaunchKernelGGL(ln_bwd_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)X, ldx, xm, stats, gamma,
+                       (const bf16_t*)DY, lddy, dym, (const bf16_t*)ADD, ldadd, am, (bf16_t*)DX, lddx, dxm, M, C, part);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(ln_bwd_k<float>, grid, dim3(256), 0, s, (const float*)X, ldx, xm, stats, gamma,
+                       (const float*)DY, lddy, dym, (const float*)ADD, ldadd, am, (float*)DX, lddx, dxm, M, C, part);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// Attention rows: P = softmax(scale * S) over the first N of each row (row stride ld),
+// Pd = P with dropout (keep ? P / (1 - p) : 0), columns [N, ld) of P and Pd are zeroed
+// (they feed the PV product as K padding).  Backward: dS = P * (dPm - sum(dPm * P)),
+// dPm = dPd with the same dropout mask.  One wave per row; S fp32.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_fwd_k(const float* __restrict__ S, int64_t lds, T* __restrict__ P,
+                                                     T* __restrict__ Pd, int64_t ldp, int rows, int N, int Npad,
+                                                     float scale, float p, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* sp_ = S + r * lds;
+  float mx = -INFINITY;
+  for (int c = lane; c < N; c += 64) mx = fmaxf(mx, sp_[c] * scale);
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int c = lane; c < N; c += 64) sum += expf(sp_[c] * scale - mx);
+  sum = wave_sum(sum);
+  const float inv = 1.0f / sum, kp = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  for (int c = lane; c < Npad; c += 64) {
+    float v = c < N ? expf(sp_[c] * scale - mx) * inv : 0.f;
+    P[r * ldp + c] = from_f<T>(v);
+    if (Pd) {
+      float d = v;
+      if (p > 0.f && c < N) d = uniform01(seed, (uint64_t)r * N + c) >= p ? v * kp : 0.f;
+      Pd[r * ldp + c] = from_f<T>(d);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_bwd_k(const T* __restrict__ P, int64_t ldp, const T* __restrict__ DPd,
+                                                     int64_t lddp, T* __restrict__ DS, int64_t ldds, int rows, int N,
+                                                     int Npad, float p, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float kp = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  auto dpm = [&](int c) {
+    float g = to_f<T>(DPd[r * lddp + c]);
+    if (p > 0.f) g = uniform01(seed, (uint64_t)r * N + c) >= p ? g * kp : 0.f;
+    return g;
+  };
+  float dot = 0.f;
+  for (int c = lane; c < N; c += 64) dot += dpm(c) * to_f<T>(P[r * ldp + c]);
+  dot = wave_sum(dot);
+  for (int c = lane; c < Npad; c += 64) {
+    const float v = c < N ? to_f<T>(P[r * ldp + c]) * (dpm(c) - dot) : 0.f;
+    DS[r * ldds + c] = from_f<T>(v);
+  }
+}
+
+extern "C" int sdp_softmax_fwd(int dtype, const float* S, int64_t lds, void* P, void* Pd, int64_t ldp, int rows, int N,
+                               int Npad, float scale, float p, uint64_t seed, void* stream) {
+  if (!S || !P || rows < 0 || N <= 0 || Npad < N || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;
+  if (rows == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((rows + 3) / 4);
+  if (dtype == 1)
+    hipLaunchKernelGGL(softmax_fwd_k<bf16_t>, grid, dim3(256), 0, s, S, lds, (bf16_t*)P, (bf16_t*)Pd, ldp, rows, N,
+                       Npad, scale, p, seed);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(softmax_fwd_k<float>, grid, dim3(256), 0, s, S, lds, (float*)P, (float*)Pd, ldp, rows, N, Npad,
+                       scale, p, seed);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+extern "C" int sdp_softmax_bwd(int dtype, const void* P, int64_t ldp, const void* DPd, int64_t lddp, void* DS,
+                               int64_t ldds, int rows, int N, int Npad, float p, uint64_t seed, void* stream) {
+  if (!P || !DPd || !DS || rows < 0 || N <= 0 || Npad < N || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;
+  if (rows == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((rows + 3) / 4);
+  if (dtype == 1)
+    hipLaunchKernelGGL(softmax_bwd_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)P, ldp, (const bf16_t*)DPd, lddp,
+                       (bf16_t*)DS, ldds, rows, N, Npad, p, seed);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(softmax_bwd_k<float>, grid, dim3(256), 0, s, (const float*)P, ldp, (const float*)DPd, lddp,
+                       (float*)DS, ldds, rows, N, Npad, p, seed);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// Depthwise-conv weight gradient (layers.py:73-78 backward):
+//   part[chunk][c][t] = sum over the chunk's images and pixels of DY[b,h,w,c] * A[b,h+ty-P,w+tx-P,c]
+// (zero padding), NHWC rows through row maps.  Block: 64 channels x (image chunk); both
+// planes of one image staged in LDS as fp32 [pixel][64].  Reduce the chunk slabs with
+// sdp_seg_colsum.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void dw_wgrad_k(const T* __restrict__ A, int64_t lda, RowMap am,
+                                                  const T* __restrict__ DY, int64_t lddy, RowMap dym, int B, int H,
+                                                  int W, int C, int k, int ipb, float* __restrict__ part) {
+  extern __shared__ float sm[];
+  const int HW = H * W;
+  float* ap = sm;            // [HW][64]
+  float* dp = sm + HW * 64;  // [HW][64]
+  const int c0 = blockIdx.x * 64, chunk = blockIdx.y;
+  const int cl = threadIdx.x & 63, tg = threadIdx.x >> 6;
+  const int P = k / 2, KK = k * k;
+  float acc[21];  // taps tg, tg+4, ... (k <= 9 -> 81 taps / 4 = 21)
+#pragma unroll
+  for (int i = 0; i < 21; ++i) acc[i] = 0.f;
+  const int b0 = chunk * ipb, b1 = min(B, b0 + ipb);
+  for (int b = b0; b < b1; ++b) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < HW * 64; e += 256) {
+      const int px = e >> 6, c = c0 + (e & 63);
+      const int64_t m = (int64_t)b * HW + px;
+      ap[e] = c < C ? to_f<T>(A[am(m) * lda + c]) : 0.f;
+      dp[e] = c < C ? to_f<T>(DY[dym(m) * lddy + c]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 21; ++i) {
+      const int t = tg + 4 * i;
+      if (t >= KK) break;
+      const int dy = t / k - P, dx = t % k - P;
+      float s = 0.f;
+      for (int h = 0; h < H; ++h) {
+        const int hh = h + dy;
+        if (hh < 0 || hh >= H) continue;
+        for (int w = 0; w < W; ++w) {
+          const int ww = w + dx;
+          if (ww < 0 || ww >= W) continue;
+          s = fmaf(dp[(h * W + w) * 64 + cl], ap[(hh * W + ww) * 64 + cl], s);
+        }
+      }
+      acc[i] += s;
+    }
+  }
+  if (c0 + cl >= C) return;
+#pragma unroll
+  for (int i = 0; i < 21; ++i) {
+    const int t = tg + 4 * i;
+    if (t >= KK) break;
+    part[((int64_t)chunk * C + c0 + cl) * KK + t] = acc[i];
+  }
+}
+
+extern "C" int sdp_dw_wgrad_chunks(int B) { return B < 64 ? (B > 0 ? B : 1) : 64; }
+
+extern "C" int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, int64_t a_gstride, int a_off,
+                            const void* DY, int64_t lddy, int dy_grp, int64_t dy_gstride, int dy_off, int B, int H,
+                            int W, int C, int k, float* part, void* stream) {
+  if (!A || !DY || !part || B < 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || k > 9 || (k % 2) == 0)
+    return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  const size_t lds = (size_t)H * W * 64 * 2 * sizeof(float);
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  if ((a_grp > 0 && a_grp % (H * W)) || (dy_grp > 0 && dy_grp % (H * W))) return (int)hipErrorInvalidValue;
+  const RowMap am = mk_tmap(a_grp, a_gstride, a_off), dym = mk_tmap(dy_grp, dy_gstride, dy_off);
+  const int nch = sdp_dw_wgrad_chunks(B), ipb = (B + nch - 1) / nch;
+  dim3 grid((C + 63) / 64, nch);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 1) {
+    (void)hipFuncSetAttribute((const void*)dw_wgrad_k<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(dw_wgrad_k<bf16_t>, grid, dim3(256), lds, s, (const bf16_t*)A, lda, am, (const bf16_t*)DY, lddy,
+                       dym, B, H, W, C, k, ipb, part);
+  } else if (dtype == 0) {
+    (void)hipFuncSetAttribute((const void*)dw_wgrad_k<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(dw_wgrad_k<float>, grid, dim3(256), lds, s, (const float*)A, lda, am, (const float*)DY, lddy,
+                       dym, B, H, W, C, k, ipb, part);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  return SDP_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// Label-smoothed cross entropy (nn.CrossEntropyLoss(label_smoothing=eps), mean over rows):
+//   loss_i = -(1 - eps) log p_{y_i} - eps / K * sum_k log p_k
+//   dlogits_i = grad_scale / B * (softmax_i - ((1 - eps) onehot(y_i) + eps / K))
+// loss_sum += sum_i loss_i / B (atomic, fp32).  One wave per row.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void ce_k(const T* __restrict__ L, int64_t ldl, const int64_t* __restrict__ y, int B,
+                                            int K, float eps, float grad_scale, T* __restrict__ D, int64_t ldd,
+                                            float* __restrict__ loss) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  const T* lp = L + r * ldl;
+  float mx = -INFINITY, sl = 0.f;
+  for (int c = lane; c < K; c += 64) {
+    const float v = to_f<T>(lp[c]);
+    mx = fmaxf(mx, v);
+    sl += v;
+  }
+  mx = wave_max(mx);
+  sl = wave_sum(sl);
+  float se = 0.f;
+  for (int c = lane; c < K; c += 64) se += expf(to_f<T>(lp[c]) - mx);
+  se = wave_sum(se);
+  const float lse = mx + logf(se);
+  const int64_t lab = y[r];
+  const float ly = to_f<T>(lp[lab]);
+  if (lane == 0) {
+    const float li = (1.0f - eps) * (lse - ly) + eps * (lse - sl / (float)K);
+    atomicAdd(loss, li / (float)B);
+  }
+  if (!D) return;
+  const float sc = grad_scale / (float)B, inv = 1.0f / se;
+  for (int c = lane; c < K; c += 64) {
+    const float pr = expf(to_f<T>(lp[c]) - mx) * inv;
+    const float tgt = (c == lab ? (1.0f - eps) : 0.0f) + eps / (float)K;
+    D[r * ldd + c] = from_f<T>(sc * (pr - tgt));
+  }
+}
+
+extern "C" int sdp_ce_loss(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K, float eps,
+                           float grad_scale, void* dlogits, int64_t ldd, float* loss, void* stream) {
+  if (!logits || !labels || !loss || B < 0 || K <= 0) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((B + 3) / 4);
+  if (dtype == 1)
+    hipLaunchKernelGGL(ce_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)logits, ldl, labels, B, K, eps, grad_scale,
+                       (bf16_t*)dlogits, ldd, loss);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(ce_k<float>, grid, dim3(256), 0, s, (const float*)logits, ldl, labels, B, K, eps, grad_scale,
+                       (float*)dlogits, ldd, loss);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// Multi-tensor gradient norm and AdamW.  Tensors are fp32; the work list is a table of
+// (tensor, first element) per 4096-element block built once by the host.
+//   sdp_grad_sumsq: state[0] += sum g^2 over every tensor, state[1] = 1 if any g is non-finite
+//   sdp_adamw: if state[1] == 0:  g = grad * inv_scale * clip, clip = min(1, max_norm /
+//     (sqrt(state[0]) * inv_scale + 1e-6)) (clip_grad_norm_ on the unscaled grads,
+//     training_tools.py:95-97);  p *= 1 - lr * wd;  m = b1 m + (1 - b1) g;
+//     v = b2 v + (1 - b2) g^2;  p -= lr / bc1 * m / (sqrt(v / bc2) + eps)   (torch AdamW)
+// ---------------------------------------------------------------------------
+struct MTBlock {
+  int tensor;
+  int64_t start;
+};
+
+__global__ __launch_bounds__(256) void sumsq_k(float* const* __restrict__ grads, const int64_t* __restrict__ sizes,
+                                               const MTBlock* __restrict__ blocks, float* __restrict__ state) {
+  const MTBlock bl = blocks[blockIdx.x];
+  const float* g = grads[bl.tensor];
+  const int64_t n = sizes[bl.tensor];
+  float s = 0.f;
+  int bad = 0;
+  for (int64_t i = bl.start + threadIdx.x; i < min(n, bl.start + 4096); i += 256) {
+    const float v = g[i];
+    s = fmaf(v, v, s);
+    bad |= !isfinite(v);
+  }
+  __shared__ float red[4];
+  __shared__ int rb[4];
+  s = wave_sum(s);
+  const int wb = __ballot(bad) != 0ull ? 1 : 0;
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = s;
+    rb[threadIdx.x >> 6] = wb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(state, red[0] + red[1] + red[2] + red[3]);
+    if (rb[0] | rb[1] | rb[2] | rb[3]) atomicMax((int*)(state + 1), 1);
+  }
+}
+
+__global__ __launch_bounds__(256) void adamw_k(float* const* __restrict__ params, float* const* __restrict__ grads,
+                                               float* const* __restrict__ m1, float* const* __restrict__ m2,
+                                               const int64_t* __restrict__ sizes, const MTBlock* __restrict__ blocks,
+                                               const float* __restrict__ state, float lr, float b1, float b2,
+                                               float eps, float wd, float bc1, float bc2, float inv_scale,
+                                               float max_norm) {
+  if (((const int*)state)[1] != 0) return;  // inf / nan in the grads: skip the step (GradScaler)
+  float sc = inv_scale;
+  if (max_norm > 0.f) {
+    const float norm = sqrtf(state[0]) * inv_scale;
+    const float clip = max_norm / (norm + 1e-6f);
+    if (clip < 1.f) sc *= clip;
+  }
+  const MTBlock bl = blocks[blockIdx.x];
+  float* p = params[bl.tensor];
+  const float* g = grads[bl.tensor];
+  float* a = m1[bl.tensor];
+  float* v = m2[bl.tensor];
+  const int64_t n = sizes[bl.tensor];
+  const float step = lr / bc1, rb2 = 1.0f / sqrtf(bc2);
+  for (int64_t i = bl.start + threadIdx.x; i < min(n, bl.start + 4096); i += 256) {
+    const float gi = g[i] * sc;
+    float pi = p[i] * (1.0f - lr * wd);
+    const float mi = b1 * a[i] + (1.0f - b1) * gi;
+    const float vi = b2 * v[i] + (1.0f - b2) * gi * gi;
+    a[i] = mi;
+    v[i] = vi;
+    pi -= step * mi / (sqrtf(vi) * rb2 + eps);
+    p[i] = pi;
+  }
+}
+
+extern "C" int sdp_grad_sumsq(float* const* grads, const int64_t* sizes, const void* blocks, int nblocks, float* state,
+                              void* stream) {
+  if (!grads || !sizes || !blocks || !state || nblocks < 0) return (int)hipErrorInvalidValue;
+  if (nblocks == 0) return 0;
+  hipLaunchKernelGGL(sumsq_k, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, grads, sizes,
+                     (const MTBlock*)blocks, state);
+  return SDP_CHECK_LAUNCH();
+}
+
+extern "C" int sdp_adamw(float* const* params, float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                         const int64_t* sizes, const void* blocks, int nblocks, const float* state, float lr,
+                         float beta1, float beta2, float eps, float weight_decay, int step, float inv_scale,
+                         float max_norm, void* stream) {
+  if (!params || !grads || !exp_avg || !exp_avg_sq || !sizes || !blocks || !state || nblocks < 0 || step <= 0)
+    return (int)hipErrorInvalidValue;
+  if (nblocks == 0) return 0;
+  const float bc1 = 1.0f - powf(beta1, (float)step), bc2 = 1.0f - powf(beta2, (float)step);
+  hipLaunchKernelGGL(adamw_k, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg, exp_avg_sq,
+                     sizes, (const MTBlock*)blocks, state, lr, beta1, beta2, eps, weight_decay, bc1, bc2, inv_scale,
+                     max_norm);
+  return SDP_CHECK_LAUNCH();
+}
+
+// Size of one work-list entry of sdp_grad_sumsq / sdp_adamw (host builds the table).
+extern "C" int sdp_mt_block_bytes(void) { return (int)sizeof(MTBlock); }
+
+// GradScaler.update (torch.amp.GradScaler semantics, training_tools.py:64, :99): scale *= backoff
+// and the growth tracker resets when state[1] flags a non-finite gradient, else the tracker
+// counts up and the scale grows by `growth` every `interval` clean steps.  Then state is reset
+// for the next step.  sc[0] = scale (fp32), sc[1] = tracker (int bits).
+__global__ void scaler_update_k(float* __restrict__ state, float* __restrict__ sc, float growth, float backoff,
+                                int interval) {
+  int* tr = (int*)(sc + 1);
+  if (((int*)state)[1] != 0) {
+    sc[0] *= backoff;
+    *tr = 0;
+  } else if (++*tr >= interval) {
+    sc[0] *= growth;
+    *tr = 0;
+  }
+  state[0] = 0.f;
+  ((int*)state)[1] = 0;
+}
+
+extern "C" int sdp_scaler_update(float* state, float* scale_tracker, float growth, float backoff, int interval,
+                                 void* stream) {
+  if (!state || !scale_tracker || interval <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(scaler_update_k, dim3(1), dim3(1), 0, (hipStream_t)stream, state, scale_tracker, growth, backoff,
+                     interval);
+  return SDP_CHECK_LAUNCH();
+}

@@ -151,7 +151,11 @@ class MainModel(SdPModel):
         return max(1, min(int(n), B))
 
     def forward(self, x: torch.Tensor, num_registers: int = 3, return_raw_outputs: bool = False):
-        check_eval(self)
+        if self.training:
+            # training_tools.py:77-103: the train-mode forward with dropout / drop path, whose
+            # backward runs on the HIP kernels too (sdpnet_train.py)
+            import sdpnet_train
+            return sdpnet_train.train_forward(self, x, num_registers, return_raw_outputs)
         if torch.compiler.is_compiling():
             # torch.compile (model_test.py:64, cifar100_test.py:93 fullgraph=True): the whole
             # fused forward is one opaque custom op with a shape-only fake (sdpnet_ops.py)

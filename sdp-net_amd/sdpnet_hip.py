@@ -24,7 +24,7 @@ LIB_PATH = os.environ.get("SDPNET_HIP_LIB", os.path.join(_HERE, "lib", "libsdpne
 F32, BF16 = 0, 1
 ACT_CODES = {"none": 0, "gelu": 1, "relu": 2, "tanh": 3, "sigmoid": 4, "leaky_relu": 5, "selu": 6, "kelu": 7}
 
-_i32, _i64, _f32, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+_i32, _i64, _f32, _vp, _u64 = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint64
 _ROWMAP = [_i32, _i64, _i32]
 
 # Signatures, in the order of include/sdpnet_hip.h.
@@ -66,6 +66,27 @@ _SIGS = {
     "sdp_val_preprocess": ([_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
                             _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp], _i32),
     "sdp_logits_metrics": ([_i32, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp], _i32),
+    # training step (train.hip)
+    "sdp_gemm_flex": ([_i32, _i32, _i32, _i32, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _i64,
+                       _i32, _i32, _i32, _i32, _i32, _i32, _i64, _f32, _i32, _vp], _i32),
+    "sdp_seg_colsum": ([_i32, _vp, _i64, _i32, _i32, _i64, _i64, _i32, _vp, _i64, _f32, _i32, _vp], _i32),
+    "sdp_act_fwd": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _f32, _u64, _vp], _i32),
+    "sdp_act_bwd": ([_i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _f32, _u64, _vp], _i32),
+    "sdp_rowscale_add": ([_i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _i32, _i32,
+                          _vp], _i32),
+    "sdp_ln_apply": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
+    "sdp_ln_bwd_blocks": ([_i32], _i32),
+    "sdp_ln_bwd": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _vp, _i64,
+                    *_ROWMAP, _i32, _i32, _vp, _vp], _i32),
+    "sdp_softmax_fwd": ([_i32, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _f32, _f32, _u64, _vp], _i32),
+    "sdp_softmax_bwd": ([_i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _f32, _u64, _vp], _i32),
+    "sdp_dw_wgrad_chunks": ([_i32], _i32),
+    "sdp_dw_wgrad": ([_i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _i32, _i32, _i32, _i32, _i32, _vp, _vp], _i32),
+    "sdp_ce_loss": ([_i32, _vp, _i64, _vp, _i32, _i32, _f32, _f32, _vp, _i64, _vp, _vp], _i32),
+    "sdp_mt_block_bytes": ([], _i32),
+    "sdp_grad_sumsq": ([_vp, _vp, _vp, _i32, _vp, _vp], _i32),
+    "sdp_adamw": ([_vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _f32, _f32, _f32, _f32, _f32, _i32, _f32, _f32, _vp], _i32),
+    "sdp_scaler_update": ([_vp, _vp, _f32, _f32, _i32, _vp], _i32),
 }
 
 _lib = None
@@ -417,3 +438,139 @@ def logits_metrics(logits: torch.Tensor, labels: torch.Tensor, label_smoothing: 
                                   float(label_smoothing), out.data_ptr(), _stream(out))
     _check(rc, "logits_metrics")
     return out
+
+
+# ---------------------------------------------------------------------------
+# training-step kernels (train.hip)
+# ---------------------------------------------------------------------------
+_NOMAP = [None, 0, 0, 0, 0]
+
+
+def _rows_args(r: Optional[Rows]):
+    return _NOMAP if r is None else r.args()
+
+
+def gemm_flex(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: int, ta: bool = False,
+              tb: bool = False, lda: Optional[int] = None, ldb: Optional[int] = None, ldc: Optional[int] = None,
+              Z: int = 1, zdiv: int = 1, sa=(0, 0), sb=(0, 0), sc=(0, 0), splits: int = 1, split_stride: int = 0,
+              alpha: float = 1.0, accum: bool = False, a_off: int = 0, b_off: int = 0, c_off: int = 0):
+    """C[z](i, j) = alpha * sum_k A(i, k) B(k, j): A(i, k) = A[k, i] if ta else A[i, k];
+    B(k, j) = B[j, k] if tb else B[k, j] (row strides lda / ldb / ldc elements, element
+    offsets *_off, batch z -> (z // zdiv) * s[0] + (z % zdiv) * s[1])."""
+    _need_cuda(A, B, C)
+    dt = dcode(A.dtype)
+    _req(B.dtype == A.dtype, "gemm_flex operand dtypes")
+    od = dcode(C.dtype)
+    lda = lda if lda is not None else A.shape[-1]
+    ldb = ldb if ldb is not None else B.shape[-1]
+    ldc = ldc if ldc is not None else C.shape[-1]
+    es, eo = A.element_size(), C.element_size()
+    rc = lib().sdp_gemm_flex(dt, od, int(ta), int(tb), A.data_ptr() + a_off * es, lda, sa[0], sa[1],
+                             B.data_ptr() + b_off * es, ldb, sb[0], sb[1], C.data_ptr() + c_off * eo, ldc, sc[0],
+                             sc[1], M, N, K, Z, zdiv, splits, split_stride, float(alpha), int(bool(accum)), _stream(C))
+    _check(rc, "gemm_flex")
+
+
+def seg_colsum(X: torch.Tensor, out: torch.Tensor, G: int, length: int, gstride: int, estride: int, C: int,
+               ldx: Optional[int] = None, ldo: Optional[int] = None, scale: float = 1.0, accum: bool = False,
+               x_off: int = 0):
+    """out[g, c] (+)= scale * sum_e X[(g * gstride + e * estride) * ldx + x_off + c] (fp32 out)."""
+    _need_cuda(X, out)
+    _req(out.dtype == torch.float32, "seg_colsum out fp32")
+    ldx = ldx if ldx is not None else X.shape[-1]
+    ldo = ldo if ldo is not None else C
+    rc = lib().sdp_seg_colsum(dcode(X.dtype), X.data_ptr() + x_off * X.element_size(), ldx, G, length, gstride,
+                              estride, C, out.data_ptr(), ldo, float(scale), int(bool(accum)), _stream(out))
+    _check(rc, "seg_colsum")
+
+
+def act_fwd(Z: torch.Tensor, Y: torch.Tensor, M: int, N: int, code: int, p: float = 0.0, seed: int = 0,
+            ldz: Optional[int] = None, ldy: Optional[int] = None):
+    _need_cuda(Z, Y)
+    _req(Z.dtype == Y.dtype, "act_fwd dtypes")
+    rc = lib().sdp_act_fwd(dcode(Z.dtype), Z.data_ptr(), ldz or N, Y.data_ptr(), ldy or N, M, N, code, float(p),
+                           int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(Y))
+    _check(rc, "act_fwd")
+
+
+def act_bwd(Z: torch.Tensor, DY: torch.Tensor, DZ: torch.Tensor, M: int, N: int, code: int, p: float = 0.0,
+            seed: int = 0):
+    _need_cuda(Z, DY, DZ)
+    _req(Z.dtype == DY.dtype == DZ.dtype, "act_bwd dtypes")
+    rc = lib().sdp_act_bwd(dcode(Z.dtype), Z.data_ptr(), N, DY.data_ptr(), N, DZ.data_ptr(), N, M, N, code, float(p),
+                           int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(DZ))
+    _check(rc, "act_bwd")
+
+
+def rowscale_add(x: Rows, y: Rows, M: int, N: int, scale: Optional[torch.Tensor] = None, sgrp: int = 1,
+                 resid: Optional[Rows] = None):
+    _need_cuda(x.t, y.t, scale)
+    _req(scale is None or scale.dtype == torch.float32, "rowscale scale fp32")
+    rc = lib().sdp_rowscale_add(dcode(x.t.dtype), *x.args(), _ptr(scale), sgrp, *_rows_args(resid), *y.args(), M, N,
+                                _stream(y.t))
+    _check(rc, "rowscale_add")
+
+
+def ln_apply(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, y: Rows, M: int, C: int):
+    _need_cuda(x.t, y.t, stats, gamma, beta)
+    _req(stats.dtype == gamma.dtype == beta.dtype == torch.float32, "ln_apply fp32 params")
+    rc = lib().sdp_ln_apply(dcode(x.t.dtype), *x.args(), stats.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                            *y.args(), M, C, _stream(y.t))
+    _check(rc, "ln_apply")
+
+
+def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows, M: int, C: int,
+           add: Optional[Rows] = None, want_affine: bool = True):
+    """dx (= LN backward [+ add]); returns (dgamma, dbeta) fp32 [C] or None."""
+    _need_cuda(x.t, stats, gamma, dy.t, dx.t)
+    nb = lib().sdp_ln_bwd_blocks(M)
+    part = torch.empty(nb, 2, C, dtype=torch.float32, device=dx.t.device) if want_affine else None
+    rc = lib().sdp_ln_bwd(dcode(x.t.dtype), *x.args(), stats.data_ptr(), gamma.data_ptr(), *dy.args(),
+                          *_rows_args(add), *dx.args(), M, C, _ptr(part), _stream(dx.t))
+    _check(rc, "ln_bwd")
+    if part is None:
+        return None
+    out = torch.empty(2, C, dtype=torch.float32, device=dx.t.device)
+    seg_colsum(part.view(nb, 2 * C), out.view(1, 2 * C), 1, nb, 0, 1, 2 * C)
+    return out[0], out[1]
+
+
+def softmax_fwd(S: torch.Tensor, P: torch.Tensor, Pd: Optional[torch.Tensor], rows: int, N: int, Npad: int,
+                scale: float, p: float = 0.0, seed: int = 0):
+    _need_cuda(S, P, Pd)
+    _req(S.dtype == torch.float32, "softmax S fp32")
+    rc = lib().sdp_softmax_fwd(dcode(P.dtype), S.data_ptr(), S.shape[-1], P.data_ptr(), _ptr(Pd), P.shape[-1], rows,
+                               N, Npad, float(scale), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(P))
+    _check(rc, "softmax_fwd")
+
+
+def softmax_bwd(P: torch.Tensor, dPd: torch.Tensor, dS: torch.Tensor, rows: int, N: int, Npad: int, p: float = 0.0,
+                seed: int = 0):
+    _need_cuda(P, dPd, dS)
+    rc = lib().sdp_softmax_bwd(dcode(P.dtype), P.data_ptr(), P.shape[-1], dPd.data_ptr(), dPd.shape[-1],
+                               dS.data_ptr(), dS.shape[-1], rows, N, Npad, float(p), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                               _stream(dS))
+    _check(rc, "softmax_bwd")
+
+
+def dw_wgrad(a: Rows, dy: Rows, B: int, H: int, W: int, C: int, k: int) -> torch.Tensor:
+    """Depthwise weight gradient [C, k*k] fp32 (reduced over the chunk slabs)."""
+    _need_cuda(a.t, dy.t)
+    nch = lib().sdp_dw_wgrad_chunks(B)
+    part = torch.empty(nch, C * k * k, dtype=torch.float32, device=a.t.device)
+    rc = lib().sdp_dw_wgrad(dcode(a.t.dtype), *a.args(), *dy.args(), B, H, W, C, k, part.data_ptr(), _stream(part))
+    _check(rc, "dw_wgrad")
+    out = torch.empty(C, k * k, dtype=torch.float32, device=a.t.device)
+    seg_colsum(part, out.view(1, -1), 1, nch, 0, 1, C * k * k)
+    return out
+
+
+def ce_loss(logits: torch.Tensor, labels: torch.Tensor, eps: float, grad_scale: float,
+            dlogits: Optional[torch.Tensor], loss: torch.Tensor):
+    _need_cuda(logits, labels, dlogits, loss)
+    _req(labels.dtype == torch.int64 and loss.dtype == torch.float32, "ce_loss dtypes")
+    B, K = logits.shape
+    rc = lib().sdp_ce_loss(dcode(logits.dtype), logits.data_ptr(), logits.stride(0), labels.contiguous().data_ptr(),
+                           B, K, float(eps), float(grad_scale), _ptr(dlogits),
+                           dlogits.stride(0) if dlogits is not None else 0, loss.data_ptr(), _stream(loss))
+    _check(rc, "ce_loss")

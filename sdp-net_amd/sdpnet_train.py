@@ -1,0 +1,693 @@
+"""Training step of the SdP-Net path on the gfx950 HIP kernels (BASELINE.json configs[4];
+SURVEY.md §8(f) rank 1, rows e2 / f1).
+
+``MainModel.forward`` in training mode (``model.train()``, the reference's
+``Trainer._run_batch``, training_tools.py:77-103) runs here instead of the eval fused
+path.  The forward is a chain of autograd Functions, one per sub-layer (patch embed +
+embedding, each ConvMixer, each EncoderLayer, the head), so DDP's bucketed gradient
+all-reduce (training_tools.py:36; RCCL over xGMI) fires per layer while the backward of
+the earlier layers still runs.  Every op of both directions is a HIP kernel of
+libsdpnet_hip.so:
+
+  forward   patchify + MFMA GEMM (+pos rows) | LN (rowstats + ln_apply) | depthwise conv |
+            GEMM + bias | act (+ dropout) | drop-path / residual (rowscale_add) |
+            attention as S = QK^T (gemm_flex) -> softmax (+ dropout) -> O = PV (gemm_flex)
+  backward  dX = dY W (gemm_flex, W read transposed from LDS) | dW = dY^T X (gemm_flex,
+            split-K slabs + seg_colsum) | bias / LN-affine / embedding grads (seg_colsum) |
+            act' (+ the same dropout mask, regenerated from its seed) | LN backward |
+            depthwise conv: input grad = conv with the flipped kernel, weight grad = dw_wgrad |
+            attention: dV = Pd^T dO, dPd = dO V^T, dS = softmax', dQ = dS K, dK = dS^T Q |
+            q/k head-LN backward
+  loss      cross_entropy(): label-smoothed CE + dlogits in one kernel (training_tools.py:76, :88)
+  optimizer AdamW: one multi-tensor kernel for GradScaler unscale + inf check +
+            clip_grad_norm_ + AdamW (training_tools.py:91-99, :235), no host sync.
+
+Randomness: dropout masks (layers.py:291, :301-308, head :450-454) come from a counter
+hash of a per-op seed drawn from torch's CPU generator (so ``torch.manual_seed`` fixes a
+run) and are regenerated, not stored; drop-path (StochasticDepth, utility_layers.py:16-27)
+draws one Bernoulli(1-p)/(1-p) scale per sample the same way.  The reference's own RNG
+stream cannot be reproduced bit for bit, so parity is pinned with dropout / drop-path
+off (the reference's gradients and AdamW step as fixtures) and the masks are tested
+statistically and for forward/backward consistency.
+
+dtype: fp32 params (as the reference keeps them), compute in bf16 under
+``torch.autocast("cuda", bf16)`` / bf16 inputs (the reference's training forward,
+training_tools.py:85) or exact fp32 otherwise.  Gradients are fp32.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+import sdpnet_hip as sp
+from sdpnet_engine import act_code, as_dtype, compute_dtype, f32, num_reg_rows
+
+Rows = sp.Rows
+
+
+def _dense(t: torch.Tensor) -> Rows:
+    return Rows(t, t.shape[-1])
+
+
+def _empty(shape, dt, dev):
+    return torch.empty(shape, dtype=dt, device=dev)
+
+
+def _seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+class _RNG:
+    """Per-forward seed source: op k of a forward gets base + k * golden (distinct streams)."""
+
+    def __init__(self):
+        self.base = _seed()
+        self.k = 0
+
+    def next(self) -> int:
+        self.k += 1
+        return (self.base + self.k * 0x9E3779B97F4A7C15) & 0x7FFFFFFFFFFFFFFF
+
+
+def _drop_path_scale(p: float, B: int, dev) -> Optional[torch.Tensor]:
+    """StochasticDepth (utility_layers.py:16-27): per-sample Bernoulli(1-p)/(1-p), or None."""
+    if p <= 1e-5:
+        return None
+    keep = (torch.rand(B) >= p).float() / (1.0 - p)
+    return keep.to(dev, non_blocking=True)
+
+
+# ---------------------------------------------------------------------------
+# GEMM helpers
+# ---------------------------------------------------------------------------
+def _linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out_dt) -> torch.Tensor:
+    """z = x . w^T + b (fast MFMA GEMM for bf16 shapes that take it, generic otherwise)."""
+    M, K = x.shape
+    N = w.shape[0]
+    z = _empty((M, N), out_dt, x.device)
+    sp.gemm(_dense(x), w, _dense(z), M, N, K, bias=b)
+    return z
+
+
+def _dgrad(dy: torch.Tensor, w: torch.Tensor, add: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx = dy . w (w [N, K] read transposed by gemm_flex) [+ add, in place into add]."""
+    M, N = dy.shape
+    K = w.shape[1]
+    if add is not None:
+        sp.gemm_flex(dy, w, add, M, K, N, ta=False, tb=False, accum=True)
+        return add
+    dx = _empty((M, K), dy.dtype, dy.device)
+    sp.gemm_flex(dy, w, dx, M, K, N, ta=False, tb=False)
+    return dx
+
+
+def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW [N, K] fp32 = dy^T x, reduction over the M token rows split across workgroups."""
+    M, N = dy.shape
+    K = x.shape[1]
+    tiles = ((N + 127) // 128) * ((K + 127) // 128)
+    splits = max(1, min(64, (1024 + tiles - 1) // tiles, M // 256))
+    if splits == 1:
+        dw = _empty((N, K), torch.float32, dy.device)
+        sp.gemm_flex(dy, x, dw, N, K, M, ta=True, tb=False)
+        return dw
+    slabs = _empty((splits, N * K), torch.float32, dy.device)
+    sp.gemm_flex(dy, x, slabs, N, K, M, ta=True, tb=False, splits=splits, split_stride=N * K)
+    dw = _empty((N, K), torch.float32, dy.device)
+    sp.seg_colsum(slabs, dw.view(1, N * K), 1, splits, 0, 1, N * K)
+    return dw
+
+
+def _colsum(x: torch.Tensor) -> torch.Tensor:
+    M, N = x.shape
+    out = _empty((N,), torch.float32, x.device)
+    sp.seg_colsum(x, out.view(1, N), 1, M, 0, 1, N)
+    return out
+
+
+def _dense_copy(src: Rows, M: int, C: int, dt, scale: Optional[torch.Tensor] = None, sgrp: int = 1) -> torch.Tensor:
+    out = _empty((M, C), dt, src.t.device)
+    sp.rowscale_add(src, _dense(out), M, C, scale=scale, sgrp=sgrp)
+    return out
+
+
+def _ln_fwd(x: Rows, M: int, C: int, g: torch.Tensor, b: torch.Tensor, eps: float, dt):
+    st = _empty((M, 2), torch.float32, x.t.device)
+    sp.rowstats(x, eps, st, M, C)
+    a = _empty((M, C), dt, x.t.device)
+    sp.ln_apply(x, st, g, b, _dense(a), M, C)
+    return a, st
+
+
+# ---------------------------------------------------------------------------
+# ConvMixer (layers.py:63-104)
+# ---------------------------------------------------------------------------
+def _mixer_params(m) -> List[Optional[nn.Parameter]]:
+    dw, cc, up, dn = m.conv2d[0], m.conv2d[1], m.conv1d[0], m.conv1d[2]
+    return [m.layer_norm_1.gamma, m.layer_norm_1.beta, dw.weight, dw.bias, cc.weight, cc.bias,
+            m.layer_norm_2.gamma, m.layer_norm_2.beta, up.weight, up.bias, dn.weight, dn.bias]
+
+
+def _drop_p(module) -> float:
+    return float(module.p) if hasattr(module, "p") else 0.0
+
+
+class _MixerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tok, geo, m, dt, *params):
+        B, R, H, W = geo
+        g1, b1, dww, dwb, ccw, ccb, g2, b2, upw, upb, dnw, dnb = params
+        C = ccw.shape[0]
+        P, N = H * W, R + H * W
+        M = B * P
+        k = dww.shape[-1]
+        dev = tok.device
+        act = act_code(m.activation)
+        img = Rows(tok, C, P, N, R)
+        W_ = dict(g1=f32(g1), b1=f32(b1), dww=f32(dww.reshape(C, k * k)), dwb=f32(dwb),
+                  ccw=as_dtype(ccw.reshape(C, C), dt), ccb=f32(ccb), g2=f32(g2), b2=f32(b2),
+                  upw=as_dtype(upw.reshape(4 * C, C), dt), upb=f32(upb),
+                  dnw=as_dtype(dnw.reshape(C, 4 * C), dt), dnb=f32(dnb))
+        dp2 = _drop_path_scale(_drop_p(m.drop_path_2), B, dev)
+        dp1 = _drop_path_scale(_drop_p(m.drop_path_1), B, dev)
+        # x_ = drop_path_2(act(PW(DW(LN1 x)))) + x
+        a1, s1 = _ln_fwd(img, M, C, W_["g1"], W_["b1"], m.layer_norm_1.eps, dt)
+        d = _empty((M, C), dt, dev)
+        sp.dwconv(_dense(a1), W_["dww"], W_["dwb"], _dense(d), B, H, W, C, k)
+        z1 = _linear(d, W_["ccw"], W_["ccb"], dt)
+        h1 = _empty((M, C), dt, dev)
+        sp.act_fwd(z1, h1, M, C, act)
+        mid = tok.clone()
+        imid = Rows(mid, C, P, N, R)
+        sp.rowscale_add(_dense(h1), imid, M, C, scale=dp2, sgrp=P, resid=img)
+        # x = drop_path_1(PW_down(act(PW_up(LN2 x_)))) + x_
+        a2, s2 = _ln_fwd(imid, M, C, W_["g2"], W_["b2"], m.layer_norm_2.eps, dt)
+        z2 = _linear(a2, W_["upw"], W_["upb"], dt)
+        h = _empty((M, 4 * C), dt, dev)
+        sp.act_fwd(z2, h, M, 4 * C, act)
+        z3 = _linear(h, W_["dnw"], W_["dnb"], dt)
+        out = mid.clone()
+        sp.rowscale_add(_dense(z3), Rows(out, C, P, N, R), M, C, scale=dp1, sgrp=P, resid=imid)
+        ctx.st = dict(tok=tok, mid=mid, a1=a1, s1=s1, d=d, z1=z1, a2=a2, s2=s2, z2=z2, h=h, W=W_, dp1=dp1, dp2=dp2,
+                      geo=(B, R, H, W, C, k), act=act, dt=dt, has=[p is not None for p in params])
+        ctx.shapes = [None if p is None else p.shape for p in params]
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        S = ctx.st
+        B, R, H, W, C, k = S["geo"]
+        P, N = H * W, R + H * W
+        M = B * P
+        dt, act, W_ = S["dt"], S["act"], S["W"]
+        dout = dout.contiguous().to(dt)
+        dev = dout.device
+        iout = Rows(dout, C, P, N, R)
+        # branch 1
+        dz3 = _dense_copy(iout, M, C, dt, S["dp1"], P)
+        dh = _dgrad(dz3, W_["dnw"])
+        gdn, gdnb = _wgrad(dz3, S["h"]), _colsum(dz3)
+        dz2 = _empty((M, 4 * C), dt, dev)
+        sp.act_bwd(S["z2"], dh, dz2, M, 4 * C, act)
+        da2 = _dgrad(dz2, W_["upw"])
+        gup, gupb = _wgrad(dz2, S["a2"]), _colsum(dz2)
+        dmid = dout.clone()
+        imid = Rows(dmid, C, P, N, R)
+        gg2, gb2 = sp.ln_bwd(Rows(S["mid"], C, P, N, R), S["s2"], W_["g2"], _dense(da2), imid, M, C, add=imid)
+        # branch 2
+        dh1 = _dense_copy(imid, M, C, dt, S["dp2"], P)
+        dz1 = _empty((M, C), dt, dev)
+        sp.act_bwd(S["z1"], dh1, dz1, M, C, act)
+        dd = _dgrad(dz1, W_["ccw"])
+        gcc, gccb = _wgrad(dz1, S["d"]), _colsum(dz1)
+        da1 = _empty((M, C), dt, dev)
+        wflip = W_["dww"].view(C, k, k).flip(1, 2).reshape(C, k * k).contiguous()
+        sp.dwconv(_dense(dd), wflip, None, _dense(da1), B, H, W, C, k)
+        gdw = sp.dw_wgrad(_dense(S["a1"]), _dense(dd), B, H, W, C, k)
+        gdwb = _colsum(dd)
+        dx = dmid  # residual; LN1's input gradient is added in place on the image rows
+        idx = Rows(dx, C, P, N, R)
+        gg1, gb1 = sp.ln_bwd(Rows(S["tok"], C, P, N, R), S["s1"], W_["g1"], _dense(da1), idx, M, C, add=idx)
+        grads = [gg1, gb1, gdw, gdwb, gcc, gccb, gg2, gb2, gup, gupb, gdn, gdnb]
+        ctx.st = None
+        return (dx, None, None, None, *[g.view(shp) if h else None for g, shp, h in zip(grads, ctx.shapes, S["has"])])
+
+
+# ---------------------------------------------------------------------------
+# EncoderLayer (layers.py:215-316)
+# ---------------------------------------------------------------------------
+def _enc_params(e) -> List[Optional[nn.Parameter]]:
+    qn = isinstance(e.q_norm, nn.LayerNorm)
+    return [e.norm1.weight, e.norm1.bias, e.q_proj.weight, e.k_proj.weight, e.v_proj.weight,
+            e.q_norm.weight if qn else None, e.q_norm.bias if qn else None,
+            e.k_norm.weight if qn else None, e.k_norm.bias if qn else None,
+            e.o_proj.weight, e.norm2.weight, e.norm2.bias, e.ff_linear1.weight, e.ff_linear1.bias,
+            e.ff_linear2.weight, e.ff_linear2.bias]
+
+
+class _EncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tok, geo, e, dt, rng, *params):
+        B, N = geo
+        (n1g, n1b, wq, wk, wv, qg, qb, kg, kb, wo, n2g, n2b, w1, b1, w2, b2) = params
+        C, Hn, hd = e.embedding_dim, e.n_head, e.head_dim
+        T = B * N
+        dev = tok.device
+        act = act_code(e.activation)
+        p_ff = float(e.dropout.p)
+        p_att = float(e.att_dropout) if e.fast_att else p_ff  # manual path drops with self.dropout (:297)
+        qn = qg is not None
+        wqkv32 = torch.cat([f32(wq), f32(wk), f32(wv)], 0)
+        W_ = dict(n1g=f32(n1g), n1b=f32(n1b), wqkv=as_dtype(wqkv32, dt), wo=as_dtype(wo, dt), n2g=f32(n2g),
+                  n2b=f32(n2b), w1=as_dtype(w1, dt), b1=f32(b1), w2=as_dtype(w2, dt), b2=f32(b2))
+        if qn:
+            W_.update(qg=f32(qg), qb=f32(qb), kg=f32(kg), kb=f32(kb))
+        seeds = [rng.next() for _ in range(4)]
+        dp1 = _drop_path_scale(_drop_p(e.drop_path1), B, dev)
+        dp2 = _drop_path_scale(_drop_p(e.drop_path2), B, dev)
+        a1, s1 = _ln_fwd(_dense(tok), T, C, W_["n1g"], W_["n1b"], e.norm1.eps, dt)
+        qkv = _linear(a1, W_["wqkv"], None, dt)                          # :282-284
+        qkvn, sq, sk = qkv, None, None
+        if qn:                                                          # :286
+            qkvn = qkv.clone()
+            rq = Rows(qkv, hd, Hn, 3 * Hn, 0)
+            rk = Rows(qkv, hd, Hn, 3 * Hn, Hn)
+            sq = _empty((T * Hn, 2), torch.float32, dev)
+            sk = _empty((T * Hn, 2), torch.float32, dev)
+            sp.rowstats(rq, e.q_norm.eps, sq, T * Hn, hd)
+            sp.rowstats(rk, e.k_norm.eps, sk, T * Hn, hd)
+            sp.ln_apply(rq, sq, W_["qg"], W_["qb"], Rows(qkvn, hd, Hn, 3 * Hn, 0), T * Hn, hd)
+            sp.ln_apply(rk, sk, W_["kg"], W_["kb"], Rows(qkvn, hd, Hn, 3 * Hn, Hn), T * Hn, hd)
+        # attention (:289-298): S = QK^T, P = softmax(S / sqrt(hd)), Pd = dropout(P), O = Pd V
+        Np = (N + 7) // 8 * 8
+        Z = B * Hn
+        Sm = _empty((B, Hn, N, Np), torch.float32, dev)
+        sp.gemm_flex(qkvn, qkvn, Sm, N, N, hd, ta=False, tb=True, lda=3 * C, ldb=3 * C, ldc=Np, Z=Z, zdiv=Hn,
+                     sa=(N * 3 * C, hd), sb=(N * 3 * C, hd), sc=(Hn * N * Np, N * Np), b_off=C)
+        Pm = _empty((B, Hn, N, Np), dt, dev)
+        Pd = _empty((B, Hn, N, Np), dt, dev) if p_att > 0 else Pm
+        sp.softmax_fwd(Sm.view(-1, Np), Pm.view(-1, Np), Pd.view(-1, Np) if p_att > 0 else None, Z * N, N, Np,
+                       1.0 / math.sqrt(hd), p_att, seeds[0])
+        del Sm
+        o = _empty((T, C), dt, dev)
+        sp.gemm_flex(Pd, qkvn, o, N, hd, N, ta=False, tb=False, lda=Np, ldb=3 * C, ldc=C, Z=Z, zdiv=Hn,
+                     sa=(Hn * N * Np, N * Np), sb=(N * 3 * C, hd), sc=(N * C, hd), b_off=2 * C)
+        # x = x + drop_path1(dropout(o_proj(o)))                       (:300-303)
+        zo = _linear(o, W_["wo"], None, dt)
+        if p_ff > 0:
+            sp.act_fwd(zo, zo, T, C, 0, p_ff, seeds[1])
+        t2 = _empty((T, C), dt, dev)
+        sp.rowscale_add(_dense(zo), _dense(t2), T, C, scale=dp1, sgrp=N, resid=_dense(tok))
+        del zo
+        # x = x + drop_path2(dropout(ff2(dropout(act(ff1(LN2 x))))))   (:306-309)
+        a2, s2 = _ln_fwd(_dense(t2), T, C, W_["n2g"], W_["n2b"], e.norm2.eps, dt)
+        z1 = _linear(a2, W_["w1"], W_["b1"], dt)
+        F_ = z1.shape[1]
+        h = _empty((T, F_), dt, dev)
+        sp.act_fwd(z1, h, T, F_, act, p_ff, seeds[2])
+        z2 = _linear(h, W_["w2"], W_["b2"], dt)
+        if p_ff > 0:
+            sp.act_fwd(z2, z2, T, C, 0, p_ff, seeds[3])
+        out = _empty((T, C), dt, dev)
+        sp.rowscale_add(_dense(z2), _dense(out), T, C, scale=dp2, sgrp=N, resid=_dense(t2))
+        ctx.st = dict(tok=tok, a1=a1, s1=s1, qkv=qkv, qkvn=qkvn, sq=sq, sk=sk, P=Pm, Pd=Pd, o=o, t2=t2, a2=a2, s2=s2,
+                      z1=z1, h=h, W=W_, seeds=seeds, dp1=dp1, dp2=dp2, geo=(B, N, C, Hn, hd, Np), act=act, dt=dt,
+                      p_ff=p_ff, p_att=p_att, qn=qn)
+        ctx.has = [p is not None for p in params]
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        S = ctx.st
+        B, N, C, Hn, hd, Np = S["geo"]
+        T, Z = B * N, B * Hn
+        dt, act, W_, seeds = S["dt"], S["act"], S["W"], S["seeds"]
+        p_ff, p_att = S["p_ff"], S["p_att"]
+        dout = dout.contiguous().to(dt)
+        dev = dout.device
+        # FFN branch
+        dz2 = _dense_copy(_dense(dout), T, C, dt, S["dp2"], N)
+        if p_ff > 0:
+            sp.act_bwd(dz2, dz2, dz2, T, C, 0, p_ff, seeds[3])
+        dh = _dgrad(dz2, W_["w2"])
+        gw2, gb2 = _wgrad(dz2, S["h"]), _colsum(dz2)
+        F_ = dh.shape[1]
+        dz1 = _empty((T, F_), dt, dev)
+        sp.act_bwd(S["z1"], dh, dz1, T, F_, act, p_ff, seeds[2])
+        del dh
+        da2 = _dgrad(dz1, W_["w1"])
+        gw1, gb1 = _wgrad(dz1, S["a2"]), _colsum(dz1)
+        dt2 = dout.clone()
+        gn2g, gn2b = sp.ln_bwd(_dense(S["t2"]), S["s2"], W_["n2g"], _dense(da2), _dense(dt2), T, C, add=_dense(dt2))
+        # attention branch
+        dzo = _dense_copy(_dense(dt2), T, C, dt, S["dp1"], N)
+        if p_ff > 0:
+            sp.act_bwd(dzo, dzo, dzo, T, C, 0, p_ff, seeds[1])
+        do = _dgrad(dzo, W_["wo"])
+        gwo = _wgrad(dzo, S["o"])
+        qkvn, Pm, Pd = S["qkvn"], S["P"], S["Pd"]
+        dqkv = _empty((T, 3 * C), dt, dev)
+        dPd = _empty((B, Hn, N, Np), dt, dev)
+        sp.gemm_flex(do, qkvn, dPd, N, N, hd, ta=False, tb=True, lda=C, ldb=3 * C, ldc=Np, Z=Z, zdiv=Hn,
+                     sa=(N * C, hd), sb=(N * 3 * C, hd), sc=(Hn * N * Np, N * Np), b_off=2 * C)
+        sp.gemm_flex(Pd, do, dqkv, N, hd, N, ta=True, tb=False, lda=Np, ldb=C, ldc=3 * C, Z=Z, zdiv=Hn,
+                     sa=(Hn * N * Np, N * Np), sb=(N * C, hd), sc=(N * 3 * C, hd), c_off=2 * C)      # dV
+        dS = _empty((B, Hn, N, Np), dt, dev)
+        sp.softmax_bwd(Pm.view(-1, Np), dPd.view(-1, Np), dS.view(-1, Np), Z * N, N, Np, p_att, seeds[0])
+        del dPd
+        scale = 1.0 / math.sqrt(hd)
+        dqk = dqkv if not S["qn"] else _empty((T, 3 * C), dt, dev)
+        sp.gemm_flex(dS, qkvn, dqk, N, hd, N, ta=False, tb=False, lda=Np, ldb=3 * C, ldc=3 * C, Z=Z, zdiv=Hn,
+                     sa=(Hn * N * Np, N * Np), sb=(N * 3 * C, hd), sc=(N * 3 * C, hd), b_off=C, alpha=scale)   # dQ
+        sp.gemm_flex(dS, qkvn, dqk, N, hd, N, ta=True, tb=False, lda=Np, ldb=3 * C, ldc=3 * C, Z=Z, zdiv=Hn,
+                     sa=(Hn * N * Np, N * Np), sb=(N * 3 * C, hd), sc=(N * 3 * C, hd), c_off=C, alpha=scale)   # dK
+        del dS
+        gqg = gqb = gkg = gkb = None
+        if S["qn"]:
+            qkv = S["qkv"]
+            gqg, gqb = sp.ln_bwd(Rows(qkv, hd, Hn, 3 * Hn, 0), S["sq"], W_["qg"], Rows(dqk, hd, Hn, 3 * Hn, 0),
+                                 Rows(dqkv, hd, Hn, 3 * Hn, 0), T * Hn, hd)
+            gkg, gkb = sp.ln_bwd(Rows(qkv, hd, Hn, 3 * Hn, Hn), S["sk"], W_["kg"], Rows(dqk, hd, Hn, 3 * Hn, Hn),
+                                 Rows(dqkv, hd, Hn, 3 * Hn, Hn), T * Hn, hd)
+        da1 = _dgrad(dqkv, W_["wqkv"])
+        gqkv = _wgrad(dqkv, S["a1"])
+        dx = dt2
+        gn1g, gn1b = sp.ln_bwd(_dense(S["tok"]), S["s1"], W_["n1g"], _dense(da1), _dense(dx), T, C, add=_dense(dx))
+        grads = [gn1g, gn1b, gqkv[:C], gqkv[C:2 * C], gqkv[2 * C:], gqg, gqb, gkg, gkb, gwo, gn2g, gn2b, gw1, gb1,
+                 gw2, gb2]
+        has = ctx.has
+        ctx.st = None
+        return (dx, None, None, None, None, *[g if h else None for g, h in zip(grads, has)])
+
+
+# ---------------------------------------------------------------------------
+# Patch embedding + positional / register embedding (layers.py:28-42, :116-209)
+# ---------------------------------------------------------------------------
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, geo, model, dt, wp, eh, ew, ereg):
+        B, R, Hp, Wp, nreg_arg = geo
+        pat = model.conv_init
+        emb = model.embedding_layer
+        C = wp.shape[0]
+        p = pat.patch_size
+        P, N = Hp * Wp, R + Hp * Wp
+        dev = x.device
+        if act_code(emb.activation) != 0:
+            raise NotImplementedError("sdpnet training path: embedding_activation must be 'none'")
+        kp = pat._kpad()
+        patches = _empty((B * P, kp), dt, dev)
+        sp.patchify(x.contiguous(), patches, p, kp)
+        w = as_dtype(wp.reshape(C, -1), dt)
+        if kp != w.shape[1]:
+            wpad = torch.zeros(C, kp, dtype=dt, device=dev)
+            wpad[:, : w.shape[1]].copy_(w)
+            w = wpad
+        conv_emb = eh is None
+        if conv_emb:  # ConvEmbedding: fixed avg-pooled bone table (a buffer)
+            pos = emb._pos_table(Hp, Wp)
+        else:
+            pos = _empty((P, C), torch.float32, dev)
+            sp.pos_table(f32(eh), f32(ew), pos, Hp, Wp, C)
+        posd = pos if dt == torch.float32 else as_dtype(pos, dt)
+        tok = _empty((B * N, C), dt, dev)
+        sp.gemm(_dense(patches), w, Rows(tok, C, P, N, R), B * P, C, kp, resid=Rows(posd, C, P, 0, 0),
+                resid_pre=True)
+        table, R2 = emb._register_rows(nreg_arg)
+        if R:
+            sp.copy_rows(table.contiguous(), C, 0, tok, C, N * C, B, R, C)
+        ctx.st = dict(patches=patches, geo=(B, R, Hp, Wp, C, P, N, p, kp), dt=dt, conv_emb=conv_emb,
+                      nrow_eh=None if conv_emb else eh.shape[0], nrow_ew=None if conv_emb else ew.shape[0],
+                      nreg=ereg.shape[0], wshape=wp.shape)
+        return tok
+
+    @staticmethod
+    def backward(ctx, dtok):
+        S = ctx.st
+        B, R, Hp, Wp, C, P, N, p, kp = S["geo"]
+        dt = S["dt"]
+        dtok = dtok.contiguous().to(dt)
+        dev = dtok.device
+        dimg = _dense_copy(Rows(dtok, C, P, N, R), B * P, C, dt)
+        gw = _wgrad(dimg, S["patches"])[:, : 3 * p * p].contiguous().view(S["wshape"])
+        geh = gew = None
+        if not S["conv_emb"]:
+            dpos = _empty((P, C), torch.float32, dev)
+            sp.seg_colsum(dtok, dpos, P, B, 1, N, C, x_off=R * C)         # sum over the batch
+            geh = torch.zeros(S["nrow_eh"], C, dtype=torch.float32, device=dev)
+            gew = torch.zeros(S["nrow_ew"], C, dtype=torch.float32, device=dev)
+            sp.seg_colsum(dpos, geh, Hp, Wp, Wp, 1, C)                      # Eh indexed by h (rows)
+            sp.seg_colsum(dpos, gew, Wp, Hp, 1, Wp, C)                      # Ew indexed by w (columns)
+        greg = torch.zeros(S["nreg"], C, dtype=torch.float32, device=dev)
+        if R:
+            off = 1 if S["conv_emb"] else 0  # ConvEmbedding takes Embedding rows 1..R (layers.py:206)
+            sp.seg_colsum(dtok, greg[off:], R, B, 1, N, C)
+        ctx.st = None
+        return None, None, None, None, gw, geh, gew, greg
+
+
+# ---------------------------------------------------------------------------
+# ClassificationHead (layers.py:429-465)
+# ---------------------------------------------------------------------------
+class _HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tok, geo, head, dt, rng, *params):
+        B, R, P, N, C = geo
+        ln_g, ln_b, w1, b1, w2, b2 = params
+        dev = tok.device
+        from_reg = head.from_register
+        rows, grp_off = (R, 0) if from_reg else (P, R)
+        m = _empty((B, C), dt, dev)
+        sp.group_mean(Rows(tok, C, rows, N, grp_off), m, B, rows, C)
+        st = dict(geo=geo, dt=dt, from_reg=from_reg, rows=rows, off=grp_off, m=m)
+        x = m
+        if ln_g is not None:
+            a, s = _ln_fwd(_dense(m), B, C, f32(ln_g), f32(ln_b), head.output_head[0].eps, dt)
+            st.update(a=a, s=s, lng=f32(ln_g))
+            x = a
+        W1 = as_dtype(w1, dt)
+        z1 = _linear(x, W1, f32(b1), dt)
+        st.update(x=x, W1=W1)
+        if w2 is None:
+            ctx.st, ctx.has = st, [p is not None for p in params]
+            return z1
+        drop = [mm for mm in head.output_head if isinstance(mm, nn.Dropout)]
+        pd = float(drop[0].p) if drop else 0.0
+        seed = rng.next()
+        hh = _empty(z1.shape, dt, dev)
+        sp.act_fwd(z1, hh, B, z1.shape[1], sp.ACT_CODES["tanh"], pd, seed)
+        W2 = as_dtype(w2, dt)
+        logits = _linear(hh, W2, f32(b2), dt)
+        st.update(z1=z1, h=hh, W2=W2, pd=pd, seed=seed)
+        ctx.st, ctx.has = st, [p is not None for p in params]
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlog):
+        S = ctx.st
+        B, R, P, N, C = S["geo"]
+        dt = S["dt"]
+        dlog = dlog.contiguous().to(dt)
+        dev = dlog.device
+        gw2 = gb2 = None
+        if "W2" in S:
+            dh = _dgrad(dlog, S["W2"])
+            gw2, gb2 = _wgrad(dlog, S["h"]), _colsum(dlog)
+            dz1 = _empty(dh.shape, dt, dev)
+            sp.act_bwd(S["z1"], dh, dz1, B, dh.shape[1], sp.ACT_CODES["tanh"], S["pd"], S["seed"])
+        else:
+            dz1 = dlog
+        dxh = _dgrad(dz1, S["W1"])
+        gw1, gb1 = _wgrad(dz1, S["x"]), _colsum(dz1)
+        glg = glb = None
+        if "a" in S:
+            dm = _empty((B, C), dt, dev)
+            glg, glb = sp.ln_bwd(_dense(S["m"]), S["s"], S["lng"], _dense(dxh), _dense(dm), B, C)
+        else:
+            dm = dxh
+        dtok = torch.zeros(B * N, C, dtype=dt, device=dev)
+        rows = S["rows"]
+        sp.copy_rows(dm, 0, C, dtok, C, N * C, B, rows, C, dst_offset_rows=S["off"])   # broadcast to the group
+        inv = torch.full((B * rows,), 1.0 / rows, dtype=torch.float32, device=dev)
+        grp = Rows(dtok, C, rows, N, S["off"])
+        sp.rowscale_add(grp, grp, B * rows, C, scale=inv, sgrp=1)                        # d mean = dm / rows
+        grads = [glg, glb, gw1, gb1, gw2, gb2]
+        has = ctx.has
+        ctx.st = None
+        return (dtok, None, None, None, None, *[g if h else None for g, h in zip(grads, has)])
+
+
+def _head_params(head) -> List[Optional[nn.Parameter]]:
+    seq = head.output_head
+    lns = [mm for mm in seq if isinstance(mm, nn.LayerNorm)]
+    lins = [mm for mm in seq if isinstance(mm, nn.Linear)]
+    ln_g, ln_b = (lns[0].weight, lns[0].bias) if lns else (None, None)
+    w1, b1 = lins[0].weight, lins[0].bias
+    w2, b2 = (lins[1].weight, lins[1].bias) if len(lins) > 1 else (None, None)
+    return [ln_g, ln_b, w1, b1, w2, b2]
+
+
+# ---------------------------------------------------------------------------
+def train_forward(model, x: torch.Tensor, num_registers: int = 3, return_raw_outputs: bool = False):
+    """MainModel.forward in training mode (model.py:129-149 with dropout / drop path active)."""
+    if return_raw_outputs:
+        raise NotImplementedError("sdpnet training path returns logits only (return_raw_outputs is eval-only)")
+    dt = compute_dtype(x, model)
+    B, _, Hi, Wi = x.shape
+    p = model.conv_init.patch_size
+    Hp, Wp = Hi // p, Wi // p
+    emb = model.embedding_layer
+    conv_emb = not hasattr(emb, "horizontal_embedding_layer")
+    if conv_emb:
+        R = num_reg_rows(emb.register.shape[0], num_registers)
+        eh = ew = None
+    else:
+        R = num_reg_rows(emb.max_num_registers, num_registers)
+        eh, ew = emb.horizontal_embedding_layer.weight, emb.vertical_embedding_layer.weight
+        if Hp > eh.shape[0] or Wp > ew.shape[0]:
+            raise RuntimeError(f"image grid {Hp}x{Wp} exceeds max_image_size {[ew.shape[0], eh.shape[0]]}")
+    N = R + Hp * Wp
+    C = model.conv_init.conv.out_channels
+    rng = _RNG()
+    xin = x if x.dtype == dt else as_dtype(x, dt)
+    tok = _EmbedFn.apply(xin, (B, R, Hp, Wp, num_registers), model, dt, model.conv_init.conv.weight, eh, ew,
+                         emb.register_embedding_layer.weight)
+
+    def enc(t, e):
+        return _EncoderFn.apply(t, (B, N), e, dt, rng, *_enc_params(e))
+
+    def mixers(t, blk):
+        for mx in blk.conv_blocks:
+            t = _MixerFn.apply(t, (B, R, Hp, Wp), mx, dt, *_mixer_params(mx))
+        return t
+
+    for blk in model.blocks:                                           # model.py:139-140, layers.py:381-386
+        if blk.conv_first:
+            tok = enc(mixers(tok, blk), blk.t_block)
+        else:
+            tok = mixers(enc(tok, blk.t_block), blk)
+    tok = enc(tok, model.final_block.t_block)                          # model.py:143
+    head = model.output_head
+    return _HeadFn.apply(tok, (B, R, Hp * Wp, N, C), head, dt, rng, *_head_params(head))
+
+
+# ---------------------------------------------------------------------------
+# Loss and optimizer
+# ---------------------------------------------------------------------------
+class _CEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, eps):
+        loss = torch.zeros(1, dtype=torch.float32, device=logits.device)
+        d = torch.empty_like(logits)
+        sp.ce_loss(logits.contiguous(), labels, eps, 1.0, d, loss)
+        ctx.save_for_backward(d)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        (d,) = ctx.saved_tensors
+        # g is the upstream scalar (the GradScaler scale, or 1): dlogits * g
+        out = torch.empty_like(d)
+        M, K = d.shape
+        sc = g.float().reshape(1).expand(M).contiguous()
+        sp.rowscale_add(_dense(d), _dense(out), M, K, scale=sc, sgrp=1)
+        return out, None, None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, label_smoothing: float = 0.0) -> torch.Tensor:
+    """nn.CrossEntropyLoss(label_smoothing=...)(logits, labels) (mean over the batch) as one
+    HIP kernel (training_tools.py:76, :88)."""
+    return _CEFn.apply(logits, labels, float(label_smoothing))
+
+
+class AdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW (training_tools.py:235; betas (0.9, 0.999), eps 1e-8, decoupled weight
+    decay) as one multi-tensor HIP kernel.  ``step(grad_scale=S, max_norm=M)`` also performs
+    GradScaler.unscale_ (grads / S), the inf/nan check that skips the step, and
+    clip_grad_norm_(M) (training_tools.py:94-99) on device, without a host sync; the
+    scaler state lives in ``self.scaler`` ([scale, growth tracker]) and updates like
+    torch.amp.GradScaler (growth 2, backoff 0.5, interval 2000)."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, init_scale=65536.0,
+                 growth_interval=2000):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self._tables = None
+        self.growth_interval = growth_interval
+        self._init_scale = float(init_scale)
+        self.scaler = None
+        self.state_buf = None
+
+    def _build(self, dev):
+        bb = sp.lib().sdp_mt_block_bytes()
+        self._tables = []
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if p.requires_grad]
+            for p in ps:
+                if p.dtype != torch.float32 or not p.is_contiguous():
+                    raise TypeError("sdpnet AdamW: fp32 contiguous parameters only")
+                st = self.state[p]
+                if not st:
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
+            blocks = []
+            for ti, p in enumerate(ps):
+                for s in range(0, p.numel(), 4096):
+                    blocks.append((ti, s))
+            raw = bytearray(bb * len(blocks))
+            import struct
+            for i, (t, s) in enumerate(blocks):
+                struct.pack_into("<iiq", raw, i * bb, t, 0, s)
+            btab = torch.frombuffer(raw, dtype=torch.uint8).to(dev) if blocks else torch.empty(0, dtype=torch.uint8,
+                                                                                                 device=dev)
+            sizes = torch.tensor([p.numel() for p in ps], dtype=torch.int64, device=dev)
+
+            def ptrs(ts):
+                return torch.tensor([t.data_ptr() for t in ts], dtype=torch.int64, device=dev)
+            self._tables.append(dict(params=ps, blocks=btab, nblocks=len(blocks), sizes=sizes, pp=ptrs(ps),
+                                     m1=ptrs([self.state[p]["exp_avg"] for p in ps]),
+                                     m2=ptrs([self.state[p]["exp_avg_sq"] for p in ps])))
+        self.state_buf = torch.zeros(2, dtype=torch.float32, device=dev)
+        self.scaler = torch.tensor([self._init_scale, 0.0], dtype=torch.float32, device=dev)
+        self.scaler[1:].view(torch.int32).zero_()
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: float = 1.0, max_norm: float = 0.0, update_scaler: bool = True):
+        loss = closure() if closure is not None else None
+        dev = self.param_groups[0]["params"][0].device
+        if self._tables is None:
+            self._build(dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        L = sp.lib()
+        gptr = []
+        for tab in self._tables:
+            gs = []
+            for p in tab["params"]:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                gs.append(p.grad)
+            g = torch.tensor([t.data_ptr() for t in gs], dtype=torch.int64, device=dev)
+            gptr.append(g)
+            sp._check(L.sdp_grad_sumsq(g.data_ptr(), tab["sizes"].data_ptr(), tab["blocks"].data_ptr(),
+                                       tab["nblocks"], self.state_buf.data_ptr(), stream), "grad_sumsq")
+        inv = 1.0 / float(grad_scale)
+        for tab, g, group in zip(self._tables, gptr, self.param_groups):
+            b1, b2 = group["betas"]
+            step = None
+            for p in tab["params"]:
+                self.state[p]["step"] += 1
+                step = self.state[p]["step"]
+            if step is None:
+                continue
+            sp._check(L.sdp_adamw(tab["pp"].data_ptr(), g.data_ptr(), tab["m1"].data_ptr(), tab["m2"].data_ptr(),
+                                  tab["sizes"].data_ptr(), tab["blocks"].data_ptr(), tab["nblocks"],
+                                  self.state_buf.data_ptr(), float(group["lr"]), float(b1), float(b2),
+                                  float(group["eps"]), float(group["weight_decay"]), int(step), inv,
+                                  float(max_norm), stream), "adamw")
+        if update_scaler:
+            sp._check(L.sdp_scaler_update(self.state_buf.data_ptr(), self.scaler.data_ptr(), 2.0, 0.5,
+                                          self.growth_interval, stream), "scaler_update")
+        return loss

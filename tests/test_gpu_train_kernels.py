@@ -1,0 +1,228 @@
+"""GPU: the training-step kernels (csrc/train.hip) against plain PyTorch fp32 references of the
+same ops (torch autograd for the backward ones).  Tolerances: fp32 paths ~1e-5 relative to
+the reference's max magnitude; bf16 operands 2e-2."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import sdpnet_hip as sp
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def rnd(*shape, seed=0, dtype=torch.float32, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype).to(DEV)
+
+
+def close(got, ref, rel, what=""):
+    got, ref = got.float(), ref.float()
+    err = (got - ref).abs().max().item()
+    scale = max(1.0, ref.abs().max().item()) if rel >= 1e-3 else max(1e-6, ref.abs().max().item())
+    assert err <= rel * scale, f"{what}: max abs err {err:.3e} vs scale {scale:.3e} (rel tol {rel})"
+
+
+def _logical(t, trans):
+    return t.t() if trans else t
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 32), (260, 96, 260), (200, 768, 96), (77, 300, 1000), (1, 17, 8)])
+def test_gemm_flex(dtype, ta, tb, M, N, K):
+    # bf16 rows must be 16-B aligned: pad the stored row length to a multiple of 8
+    def padded(r, c, seed):
+        cp = (c + 7) // 8 * 8
+        return rnd(r, cp, seed=seed, dtype=dtype)[:, :c]
+    A = padded(*((K, M) if ta else (M, K)), 1)
+    B = padded(*((N, K) if tb else (K, N)), 2)
+    C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    sp.gemm_flex(A, B, C, M, N, K, ta=ta, tb=tb, alpha=0.5, lda=A.stride(0), ldb=B.stride(0))
+    ref = 0.5 * _logical(A.float(), ta) @ _logical(B.float(), tb)
+    close(C, ref, 1e-5 if dtype == torch.float32 else 2e-2, f"flex ta={ta} tb={tb}")
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 1), (1, 0)])
+def test_gemm_flex_bf16_out_accum_and_batched(ta, tb):
+    # batched over (b, h) with two-level strides, as the attention products use it
+    Bn, H, Nq, d = 3, 4, 70, 32
+    q = rnd(Bn, Nq, 3 * H * d, seed=3, dtype=BF)
+    out = torch.zeros(Bn, H, Nq, Nq if tb else d, dtype=BF, device=DEV)
+    if tb:  # S = Q K^T per (b, h)
+        sp.gemm_flex(q, q, out, Nq, Nq, d, ta=False, tb=True, lda=3 * H * d, ldb=3 * H * d, ldc=Nq, Z=Bn * H, zdiv=H,
+                     sa=(Nq * 3 * H * d, d), sb=(Nq * 3 * H * d, d), sc=(H * Nq * Nq, Nq * Nq), b_off=H * d)
+        qq = q.float().view(Bn, Nq, 3, H, d)
+        ref = torch.einsum("bqhd,bkhd->bhqk", qq[:, :, 0], qq[:, :, 1])
+    else:  # dK = P^T Q per (b, h) with P [Nq, Nq]
+        P = rnd(Bn, H, Nq, 72, seed=4, dtype=BF)[..., :Nq]  # rows padded to 16 B
+        sp.gemm_flex(P, q, out, Nq, d, Nq, ta=True, tb=False, lda=72, ldb=3 * H * d, ldc=d, Z=Bn * H, zdiv=H,
+                     sa=(H * Nq * 72, Nq * 72), sb=(Nq * 3 * H * d, d), sc=(H * Nq * d, Nq * d))
+        qq = q.float().view(Bn, Nq, 3, H, d)
+        ref = torch.einsum("bhkq,bkhd->bhqd", P.float(), qq[:, :, 0])
+    close(out, ref, 2e-2, "batched flex")
+    # accumulate into fp32
+    A = rnd(64, 96, seed=5, dtype=BF)
+    Bm = rnd(40, 96, seed=6, dtype=BF)
+    C = rnd(64, 40, seed=7)
+    C0 = C.clone()
+    sp.gemm_flex(A, Bm, C, 64, 40, 96, tb=True, accum=True)
+    close(C, C0 + A.float() @ Bm.float().t(), 2e-2, "accum")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+def test_gemm_flex_split_k_dW(dtype):
+    """dW = dY^T X (both operands token-major) with split-K slabs reduced by seg_colsum."""
+    M, N, K, S = 3000, 192, 256, 5
+    dy = rnd(M, N, seed=8, dtype=dtype)
+    x = rnd(M, K, seed=9, dtype=dtype)
+    slabs = torch.empty(S, N, K, dtype=torch.float32, device=DEV)
+    sp.gemm_flex(dy, x, slabs, N, K, M, ta=True, tb=False, splits=S, split_stride=N * K)
+    dw = torch.empty(N, K, dtype=torch.float32, device=DEV)
+    sp.seg_colsum(slabs.view(S, N * K), dw.view(1, N * K), 1, S, 0, 1, N * K)
+    close(dw, dy.float().t() @ x.float(), 1e-5 if dtype == torch.float32 else 2e-2, "split-K dW")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+def test_seg_colsum(dtype):
+    X = rnd(6 * 50, 70, seed=10, dtype=dtype)
+    out = torch.empty(6, 70, dtype=torch.float32, device=DEV)
+    sp.seg_colsum(X, out, 6, 50, 1, 6, 70)  # group g = rows g, g+6, g+12, ...
+    close(out, X.float().view(50, 6, 70).sum(0), 1e-5, "strided segments")
+    out2 = torch.ones(1, 70, device=DEV)
+    sp.seg_colsum(X, out2, 1, 300, 0, 1, 70, scale=0.5, accum=True)
+    close(out2, 1 + 0.5 * X.float().sum(0, keepdim=True), 1e-5, "scaled accumulate")
+
+
+ACT_REF = {0: lambda x: x, 1: F.gelu, 2: F.relu, 3: torch.tanh, 4: torch.sigmoid,
+           5: lambda x: F.leaky_relu(x, 0.01), 6: F.selu,
+           7: lambda x: torch.where(x < -3.5, torch.zeros_like(x), torch.where(
+               x > 3.5, x, 0.5 * x * (1 + x / 3.5 + torch.sin(math.pi * x / 3.5) / math.pi)))}
+
+
+@pytest.mark.parametrize("code", list(ACT_REF))
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+def test_act_fwd_bwd(code, dtype):
+    M, N = 33, 257
+    z = (torch.linspace(-6, 6, M * N, device=DEV).view(M, N) + 0.013).to(dtype)
+    dy = rnd(M, N, seed=11, dtype=dtype)
+    y = torch.empty_like(z)
+    dz = torch.empty_like(z)
+    sp.act_fwd(z, y, M, N, code)
+    sp.act_bwd(z, dy, dz, M, N, code)
+    zr = z.float().clone().requires_grad_(True)
+    yr = ACT_REF[code](zr)
+    (gz,) = torch.autograd.grad(yr, zr, dy.float())
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    close(y, yr.detach(), tol, f"act {code} fwd")
+    close(dz, gz, tol, f"act {code} bwd")
+
+
+def test_dropout_mask_consistent():
+    M, N, p = 512, 1024, 0.2
+    z = rnd(M, N, seed=12).abs() + 0.5  # no exact zeros: y != 0 is the keep mask
+    y = torch.empty_like(z)
+    sp.act_fwd(z, y, M, N, 0, p=p, seed=1234)
+    keep = y != 0
+    rate = keep.float().mean().item()
+    assert abs(rate - (1 - p)) < 0.005, rate
+    close(y[keep], z[keep] / (1 - p), 1e-6, "kept values scaled")
+    dz = torch.empty_like(z)
+    ones = torch.ones_like(z)
+    sp.act_bwd(z, ones, dz, M, N, 0, p=p, seed=1234)
+    bad = ((dz != 0) != keep).sum().item()
+    assert bad == 0, (bad, dz[(dz != 0) != keep][:8].tolist(), z[(dz != 0) != keep][:8].tolist())
+    y2 = torch.empty_like(z)
+    sp.act_fwd(z, y2, M, N, 0, p=p, seed=1235)
+    assert not torch.equal(y2 != 0, keep)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("M,C,eps", [(300, 768, 1e-6), (77, 96, 1e-5), (5, 64, 1e-5)])
+def test_layernorm_fwd_bwd(dtype, M, C, eps):
+    x = (rnd(M, C, seed=13, scale=1.5) + rnd(M, 1, seed=14, scale=2)).to(dtype)
+    g = rnd(C, seed=15) * 0.2 + 1
+    b = rnd(C, seed=16) * 0.2
+    dy = rnd(M, C, seed=17, dtype=dtype)
+    add = rnd(M, C, seed=18, dtype=dtype)
+    st = torch.empty(M, 2, device=DEV)
+    sp.rowstats(sp.dense(x), eps, st, M, C)
+    y = torch.empty_like(x)
+    sp.ln_apply(sp.dense(x), st, g, b, sp.dense(y), M, C)
+    dx = torch.empty_like(x)
+    dg, db = sp.ln_bwd(sp.dense(x), st, g, sp.dense(dy), sp.dense(dx), M, C, add=sp.dense(add))
+    xr = x.float().clone().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (C,), gr, br, eps)
+    gx, gg, gb = torch.autograd.grad(yr, (xr, gr, br), dy.float())
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    close(y, yr.detach(), tol, "ln fwd")
+    close(dx, gx + add.float(), tol * 4, "ln dx")
+    close(dg, gg, tol * 4, "ln dgamma")
+    close(db, gb, tol * 4, "ln dbeta")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+def test_softmax_fwd_bwd(dtype):
+    rows, N, Npad, scale = 96, 260, 264, 1 / math.sqrt(96)
+    S = rnd(rows, Npad, seed=19, scale=4)
+    P = torch.empty(rows, Npad, dtype=dtype, device=DEV)
+    sp.softmax_fwd(S, P, None, rows, N, Npad, scale)
+    Sr = S[:, :N].clone().requires_grad_(True)
+    Pr = torch.softmax(Sr * scale, -1)
+    tol = 2e-6 if dtype == torch.float32 else 1e-2
+    close(P[:, :N], Pr.detach(), tol, "softmax")
+    assert (P[:, N:] == 0).all()
+    dP = rnd(rows, Npad, seed=20, dtype=dtype)
+    dS = torch.empty(rows, Npad, dtype=dtype, device=DEV)
+    sp.softmax_bwd(P, dP, dS, rows, N, Npad)
+    (gS,) = torch.autograd.grad(Pr, Sr, dP[:, :N].float())
+    close(dS[:, :N] * scale, gS, 1e-5 if dtype == torch.float32 else 2e-2, "softmax bwd")
+
+
+def test_softmax_dropout_mask_consistent():
+    rows, N, p = 64, 200, 0.2
+    S = rnd(rows, N, seed=21)
+    P = torch.empty(rows, N, device=DEV)
+    Pd = torch.empty(rows, N, device=DEV)
+    sp.softmax_fwd(S, P, Pd, rows, N, N, 1.0, p=p, seed=77)
+    keep = Pd != 0
+    close(Pd[keep], P[keep] / (1 - p), 1e-6, "dropped softmax scaled")
+    dS = torch.empty_like(P)
+    sp.softmax_bwd(P, torch.ones_like(P), dS, rows, N, N, p=p, seed=77)
+    Pr = torch.softmax(S.clone().requires_grad_(True), -1)
+    mask = keep.float() / (1 - p)
+    ref = P * (mask - (mask * P).sum(-1, keepdim=True))
+    close(dS, ref, 1e-5, "dropout softmax bwd")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("B,H,W,C,k", [(3, 14, 14, 128, 7), (2, 16, 16, 64, 3), (2, 7, 9, 96, 5)])
+def test_dw_wgrad(dtype, B, H, W, C, k):
+    a = rnd(B * H * W, C, seed=22, dtype=dtype)
+    dy = rnd(B * H * W, C, seed=23, dtype=dtype)
+    got = sp.dw_wgrad(sp.dense(a), sp.dense(dy), B, H, W, C, k)
+    an = a.float().view(B, H, W, C).permute(0, 3, 1, 2)
+    w = torch.zeros(C, 1, k, k, device=DEV, requires_grad=True)
+    y = F.conv2d(an, w, padding="same", groups=C)
+    (gw,) = torch.autograd.grad(y, w, dy.float().view(B, H, W, C).permute(0, 3, 1, 2))
+    close(got, gw.view(C, k * k), 1e-4 if dtype == torch.float32 else 2e-2, "dw wgrad")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("eps", [0.0, 0.1])
+def test_ce_loss(dtype, eps):
+    B, K = 37, 1000
+    logits = rnd(B, K, seed=24, dtype=dtype, scale=3)
+    labels = torch.randint(0, K, (B,), generator=torch.Generator().manual_seed(0)).to(DEV)
+    d = torch.empty_like(logits)
+    loss = torch.zeros(1, device=DEV)
+    sp.ce_loss(logits, labels, eps, 8.0, d, loss)
+    lr = logits.float().clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, labels, label_smoothing=eps)
+    (g,) = torch.autograd.grad(ref * 8.0, lr)
+    close(loss, ref.detach().view(1), 1e-5, "ce loss")
+    close(d, g, 1e-5 if dtype == torch.float32 else 2e-2, "ce dlogits")

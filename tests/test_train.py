@@ -1,0 +1,274 @@
+"""Training step (BASELINE.json configs[4]): the HIP training path
+against the reference's own gradients and AdamW step (tests/golden/train_*.npz, written by
+tests/golden/gen_train_golden.py from /root/reference with dropout / drop path off).
+
+CPU (always): the oracle's autograd gradients equal the fixtures (pins the oracle).
+GPU: ``model.train()`` forward + our cross_entropy + backward through the HIP kernels,
+fp32 (exact MFMA) and bf16 (autocast, the reference's training dtype), then our fused
+AdamW (+ clip_grad_norm_) step; dropout / drop path statistics and mask consistency; a
+gloo world-size-2 DDP run whose averaged gradient equals the single-process gradient.
+
+Tolerances: fp32 gradients within 1e-4 of each tensor's max |g| (relative), loss 1e-5;
+bf16 gradients within 2x the reference's own CPU-autocast-bf16 gradient error + 4e-2
+(relative); AdamW parameters 1e-5 absolute (fp32).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import golden_util as gu
+import sdpnet_oracle as orc
+import synth
+
+DEV = "cuda"
+CASES = sorted(json.load(open(os.path.join(gu.GOLDEN, "TRAIN_MANIFEST.json"))))
+
+
+def _case(name):
+    meta, arr = gu.load_case(name)
+    import model as ours
+    torch.manual_seed(0)
+    m = ours.MainModel.from_dict(**meta["config"])
+    sd = synth.synth_state_dict(m, meta["wseed"])
+    assert gu.digest(sd) == meta["weights_sha256"]
+    m.load_state_dict(sd)
+    x = synth.synth_images(meta["xseed"], meta["batch"], meta["image"])
+    y = torch.from_numpy(arr["labels"])
+    return meta, arr, m, sd, x, y
+
+
+def _rel(got, ref, floor=0.0):
+    """max |got - ref| over max(|ref|.max(), floor).  ``floor`` (a fraction of the largest
+    gradient of the model) keeps tensors whose exact gradient is zero -- k_norm.bias: a bias
+    added to every key shifts all scores of a query equally, so softmax ignores it -- from
+    being judged on rounding noise."""
+    return float(np.abs(got - ref).max()) / max(1e-12, float(np.abs(ref).max()), floor)
+
+
+def _floor(arr):
+    return 1e-3 * max(float(np.abs(v).max()) for k, v in arr.items() if k.startswith("grad/"))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_gradients_match_reference_fixture(name):
+    meta, arr, m, sd, x, y = _case(name)
+    osd = {k: v.clone().requires_grad_(v.is_floating_point()) for k, v in sd.items()}
+    logits = orc.forward.__wrapped__(x, osd, meta["config"], num_registers=meta["num_registers"])
+    loss = F.cross_entropy(logits, y, label_smoothing=meta["label_smoothing"])
+    loss.backward()
+    assert abs(float(loss) - float(arr["loss"])) <= 1e-5
+    for k, _ in m.named_parameters():
+        g = osd[k].grad
+        assert g is not None, k
+        assert _rel(g.numpy(), arr["grad/" + k], _floor(arr)) <= 1e-5, k
+
+
+def _train_step(name, bf16):
+    import sdpnet_train
+    meta, arr, m, sd, x, y = _case(name)
+    m = m.to(DEV).train()
+    xd, yd = x.to(DEV), y.to(DEV)
+    if bf16:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = m(xd, num_registers=meta["num_registers"])
+            loss = sdpnet_train.cross_entropy(logits, yd, meta["label_smoothing"])
+    else:
+        logits = m(xd, num_registers=meta["num_registers"])
+        loss = sdpnet_train.cross_entropy(logits, yd, meta["label_smoothing"])
+    loss.backward()
+    return meta, arr, m, logits, loss
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("bf16", [False, True])
+def test_gradients_match_reference(name, bf16):
+    """fp32: every gradient within 1e-4 (relative) of the reference's fp32 gradient.  bf16
+    (autocast): each tensor's error within 2x the reference's OWN CPU-autocast-bf16 gradient
+    error on the same inputs (grad_ac/* in the fixture) + 4e-2.  Our bf16 path also stores the
+    residual stream and the activation gradients in bf16 (autocast keeps them fp32), which
+    the ReLU case's step derivative turns into a few-percent error on the FFN weights."""
+    meta, arr, m, logits, loss = _train_step(name, bf16)
+    assert abs(float(loss) - float(arr["loss"])) <= (2e-2 if bf16 else 1e-5), (float(loss), float(arr["loss"]))
+    fl = _floor(arr)
+    worst = []
+    for k, p in m.named_parameters():
+        assert p.grad is not None, f"{k}: no gradient"
+        assert p.grad.dtype == torch.float32 and p.grad.shape == p.shape
+        r = _rel(p.grad.cpu().numpy(), arr["grad/" + k], fl)
+        rref = _rel(arr["grad_ac/" + k], arr["grad/" + k], fl)
+        tol = (2 * rref + 4e-2) if bf16 else 1e-4
+        worst.append((r / tol, r, rref, k))
+    worst.sort(reverse=True)
+    print(f"{name} bf16={bf16}: loss {float(loss):.6f} (ref {float(arr['loss']):.6f}); worst grads "
+          + ", ".join(f"{k} {r:.2e} (reference autocast {rr:.2e})" for _, r, rr, k in worst[:4]))
+    assert worst[0][0] <= 1.0, worst[:4]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_adamw_step_matches_reference(name):
+    """Our fused step (unscale 1, clip_grad_norm_(5), AdamW lr / wd of the fixture) after an fp32
+    backward reproduces the reference's post-step parameters."""
+    import sdpnet_train
+    meta, arr, m, logits, loss = _train_step(name, False)
+    opt = sdpnet_train.AdamW(m.parameters(), lr=meta["lr"], weight_decay=meta["weight_decay"])
+    opt.step(grad_scale=1.0, max_norm=meta["max_norm"])
+    torch.cuda.synchronize()
+    for k, p in m.named_parameters():
+        ref = arr["step/" + k]
+        err = float(np.abs(p.detach().cpu().numpy() - ref).max())
+        assert err <= 1e-5, (k, err)
+
+
+@pytest.mark.gpu
+def test_adamw_kernel_matches_torch_adamw_with_scaler_and_clip():
+    import sdpnet_train
+    torch.manual_seed(3)
+    shapes = [(300, 70), (5000,), (3, 4, 5), (1,)]
+    ps = [torch.randn(*s, device=DEV) for s in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    ours = [p.clone().requires_grad_(True) for p in ps]
+    opt_r = torch.optim.AdamW(ref, lr=3e-3, weight_decay=0.05)
+    opt_o = sdpnet_train.AdamW(ours, lr=3e-3, weight_decay=0.05)
+    scale = 1024.0
+    for it in range(3):
+        gs = [torch.randn(*s, device=DEV) * (10 if it == 1 else 0.1) for s in shapes]
+        for r, o, g in zip(ref, ours, gs):
+            r.grad = g.clone()
+            o.grad = g * scale  # scaled like scaler.scale(loss).backward()
+        torch.nn.utils.clip_grad_norm_(ref, 5.0)
+        opt_r.step()
+        opt_o.step(grad_scale=scale, max_norm=5.0)
+        for r, o in zip(ref, ours):
+            assert torch.allclose(r, o, atol=2e-6, rtol=1e-5), (it, (r - o).abs().max().item())
+    # a non-finite gradient skips the step and backs the scale off
+    before = [o.detach().clone() for o in ours]
+    ours[0].grad[0, 0] = float("inf")
+    opt_o.step(grad_scale=float(opt_o.scaler[0]), max_norm=5.0)
+    torch.cuda.synchronize()
+    assert all(torch.equal(b, o) for b, o in zip(before, ours))
+    assert float(opt_o.scaler[0]) == 65536.0 * 0.5
+
+
+@pytest.mark.gpu
+def test_dropout_and_drop_path_are_active_in_train_mode():
+    """Canonical-style dropouts (0.2) and drop path: train-mode logits differ between two
+    forwards and from eval; same seed -> same logits; gradients stay finite."""
+    import model as ours
+    import sdpnet_train
+    cfg = dict(embedding_dim=64, num_blocks=2, n_head=4, conv_kernel_size=7, patch_size=16, max_image_size=[16, 16],
+               head_output_from_register=True, ffn_dropout=0.2, attn_dropout=0.2, stochastic_depth_p=[0.3, 0.3],
+               output_classes=10)
+    torch.manual_seed(0)
+    m = ours.MainModel.from_dict(**cfg).to(DEV)
+    for prm in m.parameters():  # larger weights so the dropout effect is visible in the logits
+        with torch.no_grad():
+            prm.mul_(5)
+    x = torch.randn(8, 3, 64, 64, device=DEV)
+    m.train()
+    torch.manual_seed(1)
+    a = m(x)
+    b = m(x)
+    torch.manual_seed(1)
+    a2 = m(x)
+    assert torch.equal(a, a2)
+    assert not torch.allclose(a, b)
+    m.eval()
+    with torch.no_grad():
+        e = m(x)
+    assert not torch.allclose(a, e)
+    m.train()
+    y = torch.randint(0, 10, (8,), device=DEV)
+    loss = sdpnet_train.cross_entropy(m(x), y, 0.1)
+    loss.backward()
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+
+
+class _OracleModule(torch.nn.Module):
+    """The oracle forward (reference math, stock torch CPU ops) as a module whose parameters
+    DDP can hook (CPU gloo test of the data-parallel gradient average)."""
+
+    def __init__(self, sd, cfg, nreg):
+        super().__init__()
+        self.names = [k for k, v in sd.items() if v.is_floating_point()]
+        self.params = torch.nn.ParameterList([torch.nn.Parameter(sd[k].clone()) for k in self.names])
+        self.bufs = {k: v for k, v in sd.items() if not v.is_floating_point()}
+        self.cfg, self.nreg = cfg, nreg
+
+    def forward(self, x):
+        sd = dict(self.bufs)
+        sd.update(zip(self.names, self.params))
+        return orc.forward.__wrapped__(x, sd, self.cfg, num_registers=self.nreg)
+
+
+def _ddp_worker(rank, world, port, q, gpu):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        name = CASES[0]
+        meta, arr, m, sd, x, y = _case(name)
+        B = x.shape[0]
+        lo, hi = (0, 2) if rank == 0 else (2, B)
+        if gpu:  # our HIP training path, both ranks on the one GPU of the box
+            import sdpnet_train
+            m = m.to(DEV).train()
+            ddp = torch.nn.parallel.DistributedDataParallel(m)
+            logits = ddp(x[lo:hi].to(DEV), num_registers=meta["num_registers"])
+            yy = y[lo:hi].to(DEV)
+            # DDP averages over ranks: scale the local mean so the average is the global mean
+            loss = sdpnet_train.cross_entropy(logits, yy, meta["label_smoothing"]) * ((hi - lo) * world / B)
+            named = dict(m.named_parameters())
+        else:
+            om = _OracleModule(sd, meta["config"], meta["num_registers"])
+            ddp = torch.nn.parallel.DistributedDataParallel(om)
+            logits = ddp(x[lo:hi])
+            loss = F.cross_entropy(logits, y[lo:hi], label_smoothing=meta["label_smoothing"]) * ((hi - lo) * world / B)
+            named = dict(zip(om.names, om.params))
+        loss.backward()  # DDP's bucketed all-reduce (mean) runs in the backward hooks
+        if rank == 0:
+            q.put({k: p.grad.detach().cpu().numpy().copy() for k, p in named.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_two_ranks(gpu):
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q, gpu)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        grads = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    _, arr = gu.load_case(CASES[0])
+    worst = max(_rel(g, arr["grad/" + k], _floor(arr)) for k, g in grads.items())
+    return worst
+
+
+def test_two_rank_ddp_gradient_average_matches_single_process():
+    """World-size-2 gloo DDP over the oracle module: each rank's shard gradient, averaged by
+    DDP's all-reduce, equals the reference's full-batch gradient (fixture)."""
+    assert _run_two_ranks(False) <= 1e-5
+
+
+@pytest.mark.gpu
+def test_two_rank_ddp_on_hip_training_path():
+    """The same through DDP(MainModel) on the HIP training path (two gloo ranks sharing the
+    box's GPU; RCCL needs one GPU per rank, the bench's 8-GPU run uses it)."""
+    assert _run_two_ranks(True) <= 1e-4
