@@ -51,6 +51,11 @@ XL_CFG = dict(M_CFG, num_blocks=17, patch_size=14)
 CONFIGS = {
     "m": dict(cfg=M_CFG, batch=256, name="SdP-Net-M", metric=METRIC,
               desc="SdP-Net-M eval forward (12 blocks, d=768, patch 16, 200 tokens)"),
+    # BASELINE.json configs[4]: XL training step, 120 images per GPU (global 960 at DP=8)
+    "xl_train": dict(cfg=dict(XL_CFG), batch=120, name="SdP-Net-XL", train=True,
+                     metric="images/sec train step (fwd+bwd+AdamW) SdP-Net-XL 224x224 bs=120/GPU (BASELINE.json configs[4])",
+                     desc="SdP-Net-XL training step (17 blocks, d=768, patch 14, 260 tokens): bf16 autocast forward, "
+                          "label-smoothed CE, backward, GradScaler unscale + clip_grad_norm_(5) + AdamW"),
     "xl": dict(cfg=XL_CFG, batch=512, name="SdP-Net-XL",
                metric="images/sec fwd SdP-Net-XL 224×224 bs=512 @1 GPU (BASELINE.json configs[2])",
                desc="SdP-Net-XL eval forward (17 blocks, d=768, patch 14, 260 tokens)"),
@@ -171,6 +176,78 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def train_bench(args, C, world, rank, local):
+    """BASELINE.json configs[4]: one training step = bf16-autocast forward + label-smoothed CE
+    (training_tools.py:85-88) + backward (DDP bucketed gradient all-reduce over RCCL when
+    N > 1, training_tools.py:36, :91) + GradScaler unscale / clip_grad_norm_(5) / AdamW
+    (training_tools.py:94-99, fused into one HIP kernel) on each rank's 120 synthetic images."""
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    import model as sdp
+    import sdpnet_train
+    import sharding
+    cfg = C["cfg"]
+    torch.manual_seed(231424314)  # model_train.py:61
+    m = sdp.MainModel.from_dict(**cfg).to(dev).train()
+    net = m
+    if world > 1:
+        net = torch.nn.parallel.DistributedDataParallel(m, device_ids=[local])
+    opt = sdpnet_train.AdamW(m.parameters(), lr=0.0015, weight_decay=0.05)   # model_config_vit.yaml:49-51
+    lo, hi = sharding.shard_bounds(args.batch * world, world, rank)
+    B = hi - lo
+    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
+    x = torch.randn(B, 3, 224, 224, generator=g).to(dev)
+    y = torch.randint(0, cfg["output_classes"], (B,), generator=g).to(dev)
+    scale = 65536.0
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = net(x)
+            loss = sdpnet_train.cross_entropy(out, y, 0.1)
+        (loss * scale).backward()
+        opt.step(grad_scale=scale, max_norm=5.0)
+        return loss
+
+    for _ in range(max(1, args.warmup)):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = sharding.max_over_ranks(time.perf_counter() - t0, device=dev)
+    total = int(sharding.sum_over_ranks(B * args.steps, device=dev))
+    assert torch.isfinite(loss).all()
+    gf = 3 * flops_per_image(cfg) / 1e9   # forward + dX + dW GEMMs (SURVEY.md §8(d): 3x forward)
+    value = total / el
+    out = {
+        "metric": C["metric"], "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic N(0,1) 224x224 images + random labels resident in HBM; random-init weights",
+        "config": {"workload": C["desc"], "global_batch": args.batch * world, "per_gpu_batch": B,
+                   "parallelism": f"dp{world}" + (" DDP bucketed grad all-reduce over RCCL" if world > 1 else "")},
+        "model_flops_per_image_gf": round(gf, 3),
+        "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
+        "loss": round(float(loss), 4), "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -199,6 +276,8 @@ def main():
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch N ranks with --gpus N")
     if args.dry_run:
         return dry_run(args, world, rank)
+    if C.get("train"):
+        return train_bench(args, C, world, rank, local)
 
     import torch
     import torch.distributed as dist

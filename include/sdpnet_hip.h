@@ -276,6 +276,10 @@ int sdp_gemm_flex(int dtype, int out_dtype, int ta, int tb, const void* A, int64
                   int64_t sc2, int M, int N, int K, int Z, int zdiv, int splits, int64_t split_stride, float alpha,
                   int accum, void* stream);
 
+/* Y[c][r] = X[r][c] (X [R][C], row strides ldx / ldy): the weight transposes that let the
+ * input-gradient GEMMs dX = dY W run on the 256x256 MFMA kernel. */
+int sdp_transpose(int dtype, const void* X, int64_t ldx, void* Y, int64_t ldy, int R, int C, void* stream);
+
 /* out[g * ldo + c] = scale * sum_{e < len} X[(g * gstride + e * estride) * ldx + c] (+ out if
  * accum), fp32 out: bias / LayerNorm-affine / embedding-table gradients and split-K reduction. */
 int sdp_seg_colsum(int dtype, const void* X, int64_t ldx, int G, int len, int64_t gstride, int64_t estride, int C,

@@ -981,3 +981,39 @@ extern "C" int sdp_scaler_update(float* state, float* scale_tracker, float growt
                      interval);
   return SDP_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------
+// 2-D transpose through LDS (64 x 64 tiles): Y[c][r] = X[r][c], X [R][C] row stride ldx, Y row
+// stride ldy.  Weight transposes for the input-gradient GEMMs (dX = dY W runs on the fast
+// GEMM as dY . (W^T)^T).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_k(const T* __restrict__ X, int64_t ldx, T* __restrict__ Y,
+                                                   int64_t ldy, int R, int C) {
+  __shared__ T tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, c = c0 + tx;
+    if (r < R && c < C) tile[i][tx] = X[(int64_t)r * ldx + c];
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, r = r0 + tx;
+    if (r < R && c < C) Y[(int64_t)c * ldy + r] = tile[tx][i];
+  }
+}
+
+extern "C" int sdp_transpose(int dtype, const void* X, int64_t ldx, void* Y, int64_t ldy, int R, int C, void* stream) {
+  if (!X || !Y || R < 0 || C < 0) return (int)hipErrorInvalidValue;
+  if (R == 0 || C == 0) return 0;
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 1)
+    hipLaunchKernelGGL(transpose_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)X, ldx, (bf16_t*)Y, ldy, R, C);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(transpose_k<float>, grid, dim3(256), 0, s, (const float*)X, ldx, (float*)Y, ldy, R, C);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}

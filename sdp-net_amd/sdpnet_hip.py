@@ -69,6 +69,7 @@ _SIGS = {
     # training step (train.hip)
     "sdp_gemm_flex": ([_i32, _i32, _i32, _i32, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _i64,
                        _i32, _i32, _i32, _i32, _i32, _i32, _i64, _f32, _i32, _vp], _i32),
+    "sdp_transpose": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _vp], _i32),
     "sdp_seg_colsum": ([_i32, _vp, _i64, _i32, _i32, _i64, _i64, _i32, _vp, _i64, _f32, _i32, _vp], _i32),
     "sdp_act_fwd": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _f32, _u64, _vp], _i32),
     "sdp_act_bwd": ([_i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _f32, _u64, _vp], _i32),
@@ -465,6 +466,16 @@ def gemm_flex(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int,
     ldb = ldb if ldb is not None else B.shape[-1]
     ldc = ldc if ldc is not None else C.shape[-1]
     es, eo = A.element_size(), C.element_size()
+    # every element the launch can touch must lie inside the tensors' storage (no OOB launch)
+    zmax = lambda s_: ((Z - 1) // zdiv) * s_[0] + min(zdiv - 1, Z - 1) * s_[1]  # noqa: E731
+    ar, ac = (K, M) if ta else (M, K)
+    br, bc = (N, K) if tb else (K, N)
+    for t, off, s_, ld, r, c, what in ((A, a_off, sa, lda, ar, ac, "A"), (B, b_off, sb, ldb, br, bc, "B"),
+                                       (C, c_off + (splits - 1) * split_stride, sc, ldc, M, N, "C")):
+        if M and N and K and Z:
+            last = off + zmax(s_) + (r - 1) * ld + c - 1
+            avail = t.untyped_storage().nbytes() // t.element_size() - t.storage_offset()
+            _req(0 <= off and c <= ld and last < avail, f"gemm_flex operand {what} out of bounds")
     rc = lib().sdp_gemm_flex(dt, od, int(ta), int(tb), A.data_ptr() + a_off * es, lda, sa[0], sa[1],
                              B.data_ptr() + b_off * es, ldb, sb[0], sb[1], C.data_ptr() + c_off * eo, ldc, sc[0],
                              sc[1], M, N, K, Z, zdiv, splits, split_stride, float(alpha), int(bool(accum)), _stream(C))
@@ -574,3 +585,14 @@ def ce_loss(logits: torch.Tensor, labels: torch.Tensor, eps: float, grad_scale: 
                            B, K, float(eps), float(grad_scale), _ptr(dlogits),
                            dlogits.stride(0) if dlogits is not None else 0, loss.data_ptr(), _stream(loss))
     _check(rc, "ce_loss")
+
+
+def transpose(x: torch.Tensor) -> torch.Tensor:
+    """x [R, C] (row stride x.stride(0)) -> contiguous [C, R] on the HIP transpose kernel."""
+    _need_cuda(x)
+    _req(x.dim() == 2 and x.stride(1) == 1, "transpose of a row-major 2-D tensor")
+    R, C = x.shape
+    y = torch.empty(C, R, dtype=x.dtype, device=x.device)
+    rc = lib().sdp_transpose(dcode(x.dtype), x.data_ptr(), x.stride(0), y.data_ptr(), R, R, C, _stream(y))
+    _check(rc, "transpose")
+    return y

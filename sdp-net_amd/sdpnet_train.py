@@ -92,14 +92,17 @@ def _linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out_dt)
     return z
 
 
-def _dgrad(dy: torch.Tensor, w: torch.Tensor, add: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dx = dy . w (w [N, K] read transposed by gemm_flex) [+ add, in place into add]."""
+def _dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dx = dy . w.  Shapes the 256x256 MFMA kernel takes (bf16, N % 64 == 0, M >= 128) run on it
+    with a transposed weight copy (HIP transpose, small next to the GEMM); others on gemm_flex,
+    which reads w transposed from LDS."""
     M, N = dy.shape
     K = w.shape[1]
-    if add is not None:
-        sp.gemm_flex(dy, w, add, M, K, N, ta=False, tb=False, accum=True)
-        return add
     dx = _empty((M, K), dy.dtype, dy.device)
+    if sp.gemm_variant(dy.dtype, M, K, N) == 1:
+        wt = sp.transpose(w)
+        sp.gemm(_dense(dy), wt, _dense(dx), M, K, N)
+        return dx
     sp.gemm_flex(dy, w, dx, M, K, N, ta=False, tb=False)
     return dx
 
@@ -114,17 +117,28 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
         dw = _empty((N, K), torch.float32, dy.device)
         sp.gemm_flex(dy, x, dw, N, K, M, ta=True, tb=False)
         return dw
-    slabs = _empty((splits, N * K), torch.float32, dy.device)
-    sp.gemm_flex(dy, x, slabs, N, K, M, ta=True, tb=False, splits=splits, split_stride=N * K)
+    slabs = _empty((splits, N, K), torch.float32, dy.device)
+    sp.gemm_flex(dy, x, slabs, N, K, M, ta=True, tb=False, ldc=K, splits=splits, split_stride=N * K)
     dw = _empty((N, K), torch.float32, dy.device)
-    sp.seg_colsum(slabs, dw.view(1, N * K), 1, splits, 0, 1, N * K)
+    sp.seg_colsum(slabs.view(splits, N * K), dw.view(1, N * K), 1, splits, 0, 1, N * K)
     return dw
 
 
 def _colsum(x: torch.Tensor) -> torch.Tensor:
+    """Column sums (fp32) of a [M, N] matrix: per-256-row chunk sums first (parallel over
+    chunks), then the chunk sums (deterministic, no atomics)."""
     M, N = x.shape
     out = _empty((N,), torch.float32, x.device)
-    sp.seg_colsum(x, out.view(1, N), 1, M, 0, 1, N)
+    full = M // 256
+    if full < 4:
+        sp.seg_colsum(x, out.view(1, N), 1, M, 0, 1, N)
+        return out
+    tail = M - full * 256
+    part = _empty((full + (1 if tail else 0), N), torch.float32, x.device)
+    sp.seg_colsum(x, part, full, 256, 256, 1, N)
+    if tail:
+        sp.seg_colsum(x, part[full:], 1, tail, 0, 1, N, x_off=full * 256 * N)
+    sp.seg_colsum(part, out.view(1, N), 1, part.shape[0], 0, 1, N)
     return out
 
 

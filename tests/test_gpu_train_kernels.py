@@ -226,3 +226,12 @@ def test_ce_loss(dtype, eps):
     (g,) = torch.autograd.grad(ref * 8.0, lr)
     close(loss, ref.detach().view(1), 1e-5, "ce loss")
     close(d, g, 1e-5 if dtype == torch.float32 else 2e-2, "ce dlogits")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("R,C", [(768, 3072), (100, 37), (1, 64)])
+def test_transpose(dtype, R, C):
+    x = rnd(R, C, seed=25, dtype=dtype)
+    assert torch.equal(sp.transpose(x), x.t().contiguous())
+    y = rnd(R, C + 6, seed=26, dtype=dtype)[:, 3:3 + C]  # strided rows
+    assert torch.equal(sp.transpose(y), y.t().contiguous())

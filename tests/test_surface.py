@@ -84,8 +84,11 @@ def test_cpu_forward_fails_loudly():
         m(torch.randn(1, 3, 64, 64))
 
 
-def test_train_mode_forward_is_explicit():
+def test_train_mode_forward_has_no_cpu_fallback():
+    """Train mode runs the HIP training path (sdpnet_train.py); on CPU tensors it raises
+    instead of falling back to ATen."""
     import model as ours
     m = ours.MainModel(embedding_dim=32, num_blocks=1, n_head=2)
-    with pytest.raises(NotImplementedError):
+    assert m.training
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
         m(torch.randn(1, 3, 64, 64))
