@@ -343,12 +343,56 @@ __global__ __launch_bounds__(256) void seg_colsum_k(const T* __restrict__ X, int
   }
 }
 
+// 4 consecutive columns per thread (16-B fp32 / 8-B bf16 loads): block = 256 columns x 4 row
+// slices (C % 4 == 0, aligned rows).
+template <typename T>
+__global__ __launch_bounds__(256) void seg_colsum_v4(const T* __restrict__ X, int64_t ldx, int G, int len,
+                                                     int64_t gstride, int64_t estride, int C, float* __restrict__ out,
+                                                     int64_t ldo, float scale, int accum) {
+  __shared__ f32x4 red[4][64];
+  const int c = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4, sl = threadIdx.x >> 6, g = blockIdx.y;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    const T* p = X + (int64_t)g * gstride * ldx + c;
+    for (int e = sl; e < len; e += 4) {
+      const T* q = p + (int64_t)e * estride * ldx;
+      if constexpr (sizeof(T) == 2) {
+        const bf16x4 t = *(const bf16x4*)q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[r] += bf2f((bf16_t)t[r]);
+      } else {
+        s += *(const f32x4*)q;
+      }
+    }
+  }
+  red[sl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sl == 0 && c < C) {
+    const f32x4 v = scale * (red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
+    f32x4* o = (f32x4*)(out + (int64_t)g * ldo + c);
+    *o = accum ? *o + v : v;
+  }
+}
+
 extern "C" int sdp_seg_colsum(int dtype, const void* X, int64_t ldx, int G, int len, int64_t gstride,
                               int64_t estride, int C, float* out, int64_t ldo, float scale, int accum, void* stream) {
   if (!X || !out || G < 0 || len < 0 || C < 0) return (int)hipErrorInvalidValue;
   if (G == 0 || C == 0) return 0;
-  dim3 grid((C + 63) / 64, G);
   hipStream_t s = (hipStream_t)stream;
+  const int es = dtype == 1 ? 2 : 4;
+  if (C % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && (uintptr_t)X % (4 * es) == 0 && (uintptr_t)out % 16 == 0) {
+    dim3 g4((C / 4 + 63) / 64, G);
+    if (dtype == 1)
+      hipLaunchKernelGGL(seg_colsum_v4<bf16_t>, g4, dim3(256), 0, s, (const bf16_t*)X, ldx, G, len, gstride, estride, C,
+                         out, ldo, scale, accum);
+    else if (dtype == 0)
+      hipLaunchKernelGGL(seg_colsum_v4<float>, g4, dim3(256), 0, s, (const float*)X, ldx, G, len, gstride, estride, C,
+                         out, ldo, scale, accum);
+    else
+      return (int)hipErrorInvalidValue;
+    return SDP_CHECK_LAUNCH();
+  }
+  dim3 grid((C + 63) / 64, G);
   if (dtype == 1)
     hipLaunchKernelGGL(seg_colsum_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)X, ldx, G, len, gstride, estride, C,
                        out, ldo, scale, accum);
@@ -390,6 +434,105 @@ SDP_DEV float act_grad(int act, float x) {
   }
 }
 
+// 8 consecutive elements of a row per work item (16-B bf16 / 2 x 16-B fp32 accesses); the
+// host takes this form when N % 8 == 0 and every row stride / base is 8-element aligned.
+template <typename T>
+struct V8 {
+  float v[8];
+  SDP_DEV void load(const T* p) {
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8 t = *(const bf16x8*)p;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = bf2f((bf16_t)t[q]);
+    } else {
+      const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = a[q], v[4 + q] = b[q];
+    }
+  }
+  SDP_DEV void store(T* p) const {
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 t;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t[q] = (short)f2bf(v[q]);
+      *(bf16x8*)p = t;
+    } else {
+      *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+      *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  }
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void act_fwd_v8(const T* __restrict__ Z, int64_t ldz, T* __restrict__ Y,
+                                                  int64_t ldy, int M, int N, int act, float p, uint64_t seed) {
+  const int n8 = N >> 3;
+  const int64_t total = (int64_t)M * n8;
+  const float inv = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t m = e / n8;
+    const int n = (int)(e - m * n8) * 8;
+    V8<T> x;
+    x.load(Z + m * ldz + n);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float v = apply_act(act, x.v[q]);
+      if (p > 0.f) v = uniform01(seed, (uint64_t)m * N + n + q) >= p ? v * inv : 0.f;
+      x.v[q] = v;
+    }
+    x.store(Y + m * ldy + n);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void act_bwd_v8(const T* __restrict__ Z, int64_t ldz, const T* __restrict__ DY,
+                                                  int64_t lddy, T* __restrict__ DZ, int64_t lddz, int M, int N,
+                                                  int act, float p, uint64_t seed) {
+  const int n8 = N >> 3;
+  const int64_t total = (int64_t)M * n8;
+  const float inv = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t m = e / n8;
+    const int n = (int)(e - m * n8) * 8;
+    V8<T> z, g;
+    z.load(Z + m * ldz + n);
+    g.load(DY + m * lddy + n);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float d = g.v[q];
+      if (p > 0.f) d = uniform01(seed, (uint64_t)m * N + n + q) >= p ? d * inv : 0.f;
+      g.v[q] = act == ACT_NONE ? d : d * act_grad(act, z.v[q]);
+    }
+    g.store(DZ + m * lddz + n);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void rowscale_v8(const T* __restrict__ X, int64_t ldx, RowMap xm,
+                                                   const float* __restrict__ sc, int sgrp, const T* __restrict__ R,
+                                                   int64_t ldr, RowMap rm, T* __restrict__ Y, int64_t ldy, RowMap ym,
+                                                   int M, int N) {
+  const int n8 = N >> 3;
+  const int64_t total = (int64_t)M * n8;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t m = e / n8;
+    const int n = (int)(e - m * n8) * 8;
+    V8<T> x;
+    x.load(X + xm(m) * ldx + n);
+    const float s_ = sc ? sc[m / sgrp] : 1.0f;
+    if (R) {
+      V8<T> r;
+      r.load(R + rm(m) * ldr + n);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x.v[q] = fmaf(x.v[q], s_, r.v[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x.v[q] *= s_;
+    }
+    x.store(Y + ym(m) * ldy + n);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void act_fwd_k(const T* __restrict__ Z, int64_t ldz, T* __restrict__ Y, int64_t ldy,
                                                  int M, int N, int act, float p, uint64_t seed) {
@@ -427,6 +570,17 @@ extern "C" int sdp_act_fwd(int dtype, const void* Z, int64_t ldz, void* Y, int64
   if (!Z || !Y || M < 0 || N < 0 || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;
   if ((int64_t)M * N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  const int es = dtype == 1 ? 2 : 4;
+  if (N % 8 == 0 && ldz % 8 == 0 && ldy % 8 == 0 && (uintptr_t)Z % 16 == 0 && (uintptr_t)Y % 16 == 0 && (es == 2 || es == 4)) {
+    const int gv = ew_grid((int64_t)M * (N / 8));
+    if (dtype == 1)
+      hipLaunchKernelGGL(act_fwd_v8<bf16_t>, dim3(gv), dim3(256), 0, s, (const bf16_t*)Z, ldz, (bf16_t*)Y, ldy, M, N, act, p, seed);
+    else if (dtype == 0)
+      hipLaunchKernelGGL(act_fwd_v8<float>, dim3(gv), dim3(256), 0, s, (const float*)Z, ldz, (float*)Y, ldy, M, N, act, p, seed);
+    else
+      return (int)hipErrorInvalidValue;
+    return SDP_CHECK_LAUNCH();
+  }
   const int g = ew_grid((int64_t)M * N);
   if (dtype == 1)
     hipLaunchKernelGGL(act_fwd_k<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)Z, ldz, (bf16_t*)Y, ldy, M, N, act, p, seed);
@@ -442,6 +596,19 @@ extern "C" int sdp_act_bwd(int dtype, const void* Z, int64_t ldz, const void* DY
   if (!Z || !DY || !DZ || M < 0 || N < 0 || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;
   if ((int64_t)M * N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  if (N % 8 == 0 && ldz % 8 == 0 && lddy % 8 == 0 && lddz % 8 == 0 && (uintptr_t)Z % 16 == 0 &&
+      (uintptr_t)DY % 16 == 0 && (uintptr_t)DZ % 16 == 0) {
+    const int gv = ew_grid((int64_t)M * (N / 8));
+    if (dtype == 1)
+      hipLaunchKernelGGL(act_bwd_v8<bf16_t>, dim3(gv), dim3(256), 0, s, (const bf16_t*)Z, ldz, (const bf16_t*)DY, lddy,
+                         (bf16_t*)DZ, lddz, M, N, act, p, seed);
+    else if (dtype == 0)
+      hipLaunchKernelGGL(act_bwd_v8<float>, dim3(gv), dim3(256), 0, s, (const float*)Z, ldz, (const float*)DY, lddy,
+                         (float*)DZ, lddz, M, N, act, p, seed);
+    else
+      return (int)hipErrorInvalidValue;
+    return SDP_CHECK_LAUNCH();
+  }
   const int g = ew_grid((int64_t)M * N);
   if (dtype == 1)
     hipLaunchKernelGGL(act_bwd_k<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)Z, ldz, (const bf16_t*)DY, lddy,
@@ -481,6 +648,19 @@ extern "C" int sdp_rowscale_add(int dtype, const void* X, int64_t ldx, int x_grp
   hipStream_t s = (hipStream_t)stream;
   const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), rm = mk_tmap(r_grp, r_gstride, r_off),
                ym = mk_tmap(y_grp, y_gstride, y_off);
+  if (N % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && (!R || (ldr % 8 == 0 && (uintptr_t)R % 16 == 0)) &&
+      (uintptr_t)X % 16 == 0 && (uintptr_t)Y % 16 == 0) {
+    const int gv = ew_grid((int64_t)M * (N / 8));
+    if (dtype == 1)
+      hipLaunchKernelGGL(rowscale_v8<bf16_t>, dim3(gv), dim3(256), 0, s, (const bf16_t*)X, ldx, xm, scale, sgrp,
+                         (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, M, N);
+    else if (dtype == 0)
+      hipLaunchKernelGGL(rowscale_v8<float>, dim3(gv), dim3(256), 0, s, (const float*)X, ldx, xm, scale, sgrp,
+                         (const float*)R, ldr, rm, (float*)Y, ldy, ym, M, N);
+    else
+      return (int)hipErrorInvalidValue;
+    return SDP_CHECK_LAUNCH();
+  }
   const int g = ew_grid((int64_t)M * N);
   if (dtype == 1)
     hipLaunchKernelGGL(rowscale_k<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)X, ldx, xm, scale, sgrp,
@@ -512,35 +692,38 @@ __global__ __launch_bounds__(256) void ln_apply_k(const T* __restrict__ X, int64
 }
 
 // dx = rstd * (gdy - mean(gdy) - xhat * mean(gdy * xhat)) [+ add];  per-block partials of
-// dgamma = sum dy * xhat, dbeta = sum dy in part[blockIdx.x][2][C] (C <= 2048).
-template <typename T>
+// dgamma = sum dy * xhat, dbeta = sum dy in part[blockIdx.x][2][C].  V = ceil(C / 64) values
+// per lane (compile time, so the per-row arrays stay in registers).
+template <typename T, int V>
 __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ X, int64_t ldx, RowMap xm,
                                                 const float* __restrict__ st, const float* __restrict__ g,
                                                 const T* __restrict__ DY, int64_t lddy, RowMap dym,
                                                 const T* __restrict__ ADD, int64_t ldadd, RowMap am,
                                                 T* __restrict__ DX, int64_t lddx, RowMap dxm, int M, int C,
                                                 float* __restrict__ part) {
-  constexpr int MAXV = 32;  // C <= 2048
-  __shared__ float red[2][4][2048];
+  extern __shared__ float red[];  // [2][4][C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float dg[MAXV], db[MAXV];
+  float dg[V], db[V], gv[V];
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) dg[i] = db[i] = 0.f;
-  const int nv = (C + 63) / 64;
+  for (int i = 0; i < V; ++i) {
+    const int c = lane + 64 * i;
+    dg[i] = db[i] = 0.f;
+    gv[i] = c < C ? g[c] : 0.f;
+  }
   for (int64_t m = (int64_t)blockIdx.x * 4 + w; m < M; m += (int64_t)gridDim.x * 4) {
     const float mean = st[2 * m], rstd = st[2 * m + 1];
     const T* xp = X + xm(m) * ldx;
     const T* dyp = DY + dym(m) * lddy;
-    float xh[MAXV], gd[MAXV];
+    float xh[V], gd[V];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < V; ++i) {
       const int c = lane + 64 * i;
       xh[i] = gd[i] = 0.f;
-      if (i < nv && c < C) {
+      if (c < C) {
         const float dy = to_f<T>(dyp[c]);
         xh[i] = (to_f<T>(xp[c]) - mean) * rstd;
-        gd[i] = dy * g[c];
+        gd[i] = dy * gv[i];
         dg[i] += dy * xh[i];
         db[i] += dy;
         s1 += gd[i];
@@ -552,9 +735,9 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ X, int64_t
     T* dxp = DX + dxm(m) * lddx;
     const T* ap = ADD ? ADD + am(m) * ldadd : nullptr;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < V; ++i) {
       const int c = lane + 64 * i;
-      if (i < nv && c < C) {
+      if (c < C) {
         float v = rstd * (gd[i] - s1 - xh[i] * s2);
         if (ap) v += to_f<T>(ap[c]);
         dxp[c] = from_f<T>(v);
@@ -563,17 +746,18 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ X, int64_t
   }
   if (!part) return;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
+  for (int i = 0; i < V; ++i) {
     const int c = lane + 64 * i;
-    if (i < nv && c < C) {
-      red[0][w][c] = dg[i];
-      red[1][w][c] = db[i];
+    if (c < C) {
+      red[(0 * 4 + w) * C + c] = dg[i];
+      red[(1 * 4 + w) * C + c] = db[i];
     }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
-    part[(int64_t)blockIdx.x * 2 * C + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
-    part[(int64_t)blockIdx.x * 2 * C + C + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    part[(int64_t)blockIdx.x * 2 * C + c] = red[0 * C + c] + red[1 * C + c] + red[2 * C + c] + red[3 * C + c];
+    part[(int64_t)blockIdx.x * 2 * C + C + c] =
+        red[4 * C + c] + red[5 * C + c] + red[6 * C + c] + red[7 * C + c];
   }
 }
 
@@ -613,14 +797,27 @@ extern "C" int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int6
                am = mk_tmap(a_grp, a_gstride, a_off), dxm = mk_tmap(dx_grp, dx_gstride, dx_off);
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(sdp_ln_bwd_blocks(M));
-  if (dtype == 1)
-    hipLaunchKernelGGL(ln_bwd_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)X, ldx, xm, stats, gamma,
-                       (const bf16_t*)DY, lddy, dym, (const bf16_t*)ADD, ldadd, am, (bf16_t*)DX, lddx, dxm, M, C, part);
-  else if (dtype == 0)
-    hipLaunchKernelGGL(ln_bwd_k<float>, grid, dim3(256), 0, s, (const float*)X, ldx, xm, stats, gamma,
-                       (const float*)DY, lddy, dym, (const float*)ADD, ldadd, am, (float*)DX, lddx, dxm, M, C, part);
-  else
+  const size_t lds = (size_t)8 * C * sizeof(float);
+  const int v = (C + 63) / 64;
+#define SDP_LNB(TT, VV)                                                                                          \
+  hipLaunchKernelGGL((ln_bwd_k<TT, VV>), grid, dim3(256), lds, s, (const TT*)X, ldx, xm, stats, gamma, (const TT*)DY, \
+                     lddy, dym, (const TT*)ADD, ldadd, am, (TT*)DX, lddx, dxm, M, C, part)
+#define SDP_LNB_T(TT)                                 \
+  if (v <= 2) SDP_LNB(TT, 2);                         \
+  else if (v <= 4) SDP_LNB(TT, 4);                    \
+  else if (v <= 8) SDP_LNB(TT, 8);                    \
+  else if (v <= 12) SDP_LNB(TT, 12);                  \
+  else if (v <= 16) SDP_LNB(TT, 16);                  \
+  else SDP_LNB(TT, 32)
+  if (dtype == 1) {
+    SDP_LNB_T(bf16_t);
+  } else if (dtype == 0) {
+    SDP_LNB_T(float);
+  } else {
     return (int)hipErrorInvalidValue;
+  }
+#undef SDP_LNB_T
+#undef SDP_LNB
   return SDP_CHECK_LAUNCH();
 }
 
@@ -719,55 +916,69 @@ extern "C" int sdp_softmax_bwd(int dtype, const void* P, int64_t ldp, const void
 // planes of one image staged in LDS as fp32 [pixel][64].  Reduce the chunk slabs with
 // sdp_seg_colsum.
 // ---------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(256) void dw_wgrad_k(const T* __restrict__ A, int64_t lda, RowMap am,
-                                                  const T* __restrict__ DY, int64_t lddy, RowMap dym, int B, int H,
-                                                  int W, int C, int k, int ipb, float* __restrict__ part) {
+// Thread (channel cl, tap row ty): for every output row h it loads the 16-wide DY row and the
+// (16 + KS - 1)-wide zero-padded A row hh = h + ty - KS/2 into registers once and does the
+// KS x W FMAs of that row pair from registers (LDS reads per FMA ~ 1/3.5 instead of 2).
+template <typename T, int KS>
+__global__ __launch_bounds__(64 * KS) void dw_wgrad_k(const T* __restrict__ A, int64_t lda, RowMap am,
+                                                      const T* __restrict__ DY, int64_t lddy, RowMap dym, int B, int H,
+                                                      int W, int C, int ipb, float* __restrict__ part) {
   extern __shared__ float sm[];
+  constexpr int P = KS / 2, MW = 16;
   const int HW = H * W;
   float* ap = sm;            // [HW][64]
   float* dp = sm + HW * 64;  // [HW][64]
   const int c0 = blockIdx.x * 64, chunk = blockIdx.y;
-  const int cl = threadIdx.x & 63, tg = threadIdx.x >> 6;
-  const int P = k / 2, KK = k * k;
-  float acc[21];  // taps tg, tg+4, ... (k <= 9 -> 81 taps / 4 = 21)
+  const int cl = threadIdx.x & 63, ty = threadIdx.x / 64;
+  float acc[KS];
 #pragma unroll
-  for (int i = 0; i < 21; ++i) acc[i] = 0.f;
+  for (int i = 0; i < KS; ++i) acc[i] = 0.f;
   const int b0 = chunk * ipb, b1 = min(B, b0 + ipb);
+  const bool v8 = (sizeof(T) == 2) && (c0 + 64 <= C) && (lda % 8 == 0) && (lddy % 8 == 0) &&
+                  (((uintptr_t)A & 15) == 0) && (((uintptr_t)DY & 15) == 0);
   for (int b = b0; b < b1; ++b) {
     __syncthreads();
-    for (int e = threadIdx.x; e < HW * 64; e += 256) {
-      const int px = e >> 6, c = c0 + (e & 63);
-      const int64_t m = (int64_t)b * HW + px;
-      ap[e] = c < C ? to_f<T>(A[am(m) * lda + c]) : 0.f;
-      dp[e] = c < C ? to_f<T>(DY[dym(m) * lddy + c]) : 0.f;
-    }
-    __syncthreads();
+    if (v8) {  // 16-B loads: 8 chunks of 8 channels per pixel
+      for (int e = threadIdx.x; e < HW * 8; e += 64 * KS) {
+        const int px = e >> 3, ch = e & 7;
+        const int64_t m = (int64_t)b * HW + px;
+        const bf16x8 va = *(const bf16x8*)(A + am(m) * lda + c0 + ch * 8);
+        const bf16x8 vd = *(const bf16x8*)(DY + dym(m) * lddy + c0 + ch * 8);
 #pragma unroll
-    for (int i = 0; i < 21; ++i) {
-      const int t = tg + 4 * i;
-      if (t >= KK) break;
-      const int dy = t / k - P, dx = t % k - P;
-      float s = 0.f;
-      for (int h = 0; h < H; ++h) {
-        const int hh = h + dy;
-        if (hh < 0 || hh >= H) continue;
-        for (int w = 0; w < W; ++w) {
-          const int ww = w + dx;
-          if (ww < 0 || ww >= W) continue;
-          s = fmaf(dp[(h * W + w) * 64 + cl], ap[(hh * W + ww) * 64 + cl], s);
+        for (int q = 0; q < 8; ++q) {
+          ap[px * 64 + ch * 8 + q] = bf2f((bf16_t)va[q]);
+          dp[px * 64 + ch * 8 + q] = bf2f((bf16_t)vd[q]);
         }
       }
-      acc[i] += s;
+    } else {
+      for (int e = threadIdx.x; e < HW * 64; e += 64 * KS) {
+        const int px = e >> 6, c = c0 + (e & 63);
+        const int64_t m = (int64_t)b * HW + px;
+        ap[e] = c < C ? to_f<T>(A[am(m) * lda + c]) : 0.f;
+        dp[e] = c < C ? to_f<T>(DY[dym(m) * lddy + c]) : 0.f;
+      }
+    }
+    __syncthreads();
+    for (int h = 0; h < H; ++h) {
+      const int hh = h + ty - P;
+      if (hh < 0 || hh >= H) continue;
+      float ar[MW + KS - 1], dr[MW];
+#pragma unroll
+      for (int q = 0; q < MW + KS - 1; ++q) {
+        const int ww = q - P;
+        ar[q] = (ww >= 0 && ww < W) ? ap[(hh * W + ww) * 64 + cl] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < MW; ++q) dr[q] = q < W ? dp[(h * W + q) * 64 + cl] : 0.f;
+#pragma unroll
+      for (int q = 0; q < MW; ++q)
+#pragma unroll
+        for (int tx = 0; tx < KS; ++tx) acc[tx] = fmaf(dr[q], ar[q + tx], acc[tx]);
     }
   }
   if (c0 + cl >= C) return;
 #pragma unroll
-  for (int i = 0; i < 21; ++i) {
-    const int t = tg + 4 * i;
-    if (t >= KK) break;
-    part[((int64_t)chunk * C + c0 + cl) * KK + t] = acc[i];
-  }
+  for (int tx = 0; tx < KS; ++tx) part[((int64_t)chunk * C + c0 + cl) * (KS * KS) + ty * KS + tx] = acc[tx];
 }
 
 extern "C" int sdp_dw_wgrad_chunks(int B) { return B < 64 ? (B > 0 ? B : 1) : 64; }
@@ -775,7 +986,7 @@ extern "C" int sdp_dw_wgrad_chunks(int B) { return B < 64 ? (B > 0 ? B : 1) : 64
 extern "C" int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, int64_t a_gstride, int a_off,
                             const void* DY, int64_t lddy, int dy_grp, int64_t dy_gstride, int dy_off, int B, int H,
                             int W, int C, int k, float* part, void* stream) {
-  if (!A || !DY || !part || B < 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || k > 9 || (k % 2) == 0)
+  if (!A || !DY || !part || B < 0 || H <= 0 || W <= 0 || W > 16 || C <= 0 || (k != 3 && k != 5 && k != 7 && k != 9))
     return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
   const size_t lds = (size_t)H * W * 64 * 2 * sizeof(float);
@@ -785,17 +996,28 @@ extern "C" int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, in
   const int nch = sdp_dw_wgrad_chunks(B), ipb = (B + nch - 1) / nch;
   dim3 grid((C + 63) / 64, nch);
   hipStream_t s = (hipStream_t)stream;
+#define SDP_DWG(TT, KK)                                                                                              \
+  do {                                                                                                               \
+    (void)hipFuncSetAttribute((const void*)dw_wgrad_k<TT, KK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    hipLaunchKernelGGL((dw_wgrad_k<TT, KK>), grid, dim3(64 * KK), lds, s, (const TT*)A, lda, am, (const TT*)DY, lddy, \
+                       dym, B, H, W, C, ipb, part);                                                                  \
+  } while (0)
+#define SDP_DWG_T(TT)                  \
+  switch (k) {                         \
+    case 3: SDP_DWG(TT, 3); break;     \
+    case 5: SDP_DWG(TT, 5); break;     \
+    case 7: SDP_DWG(TT, 7); break;     \
+    default: SDP_DWG(TT, 9); break;    \
+  }
   if (dtype == 1) {
-    (void)hipFuncSetAttribute((const void*)dw_wgrad_k<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(dw_wgrad_k<bf16_t>, grid, dim3(256), lds, s, (const bf16_t*)A, lda, am, (const bf16_t*)DY, lddy,
-                       dym, B, H, W, C, k, ipb, part);
+    SDP_DWG_T(bf16_t)
   } else if (dtype == 0) {
-    (void)hipFuncSetAttribute((const void*)dw_wgrad_k<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(dw_wgrad_k<float>, grid, dim3(256), lds, s, (const float*)A, lda, am, (const float*)DY, lddy,
-                       dym, B, H, W, C, k, ipb, part);
+    SDP_DWG_T(float)
   } else {
     return (int)hipErrorInvalidValue;
   }
+#undef SDP_DWG_T
+#undef SDP_DWG
   return SDP_CHECK_LAUNCH();
 }
 

@@ -112,7 +112,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     M, N = dy.shape
     K = x.shape[1]
     tiles = ((N + 127) // 128) * ((K + 127) // 128)
-    splits = max(1, min(64, (1024 + tiles - 1) // tiles, M // 256))
+    splits = max(1, min(32, (512 + tiles - 1) // tiles, M // 512))
     if splits == 1:
         dw = _empty((N, K), torch.float32, dy.device)
         sp.gemm_flex(dy, x, dw, N, K, M, ta=True, tb=False)
@@ -145,6 +145,21 @@ def _colsum(x: torch.Tensor) -> torch.Tensor:
 def _dense_copy(src: Rows, M: int, C: int, dt, scale: Optional[torch.Tensor] = None, sgrp: int = 1) -> torch.Tensor:
     out = _empty((M, C), dt, src.t.device)
     sp.rowscale_add(src, _dense(out), M, C, scale=scale, sgrp=sgrp)
+    return out
+
+
+def _branch_grad(d: torch.Tensor, T: int, C: int, dt, dp: Optional[torch.Tensor], grp: int, p: float, seed: int):
+    """Gradient into a residual branch y = x + drop_path(dropout(z)): dz = d * mask / (1-p) * dp
+    (one pass; no copy at all when neither is active)."""
+    if p <= 0 and dp is None:
+        return d
+    out = _empty((T, C), dt, d.device)
+    if p > 0:
+        sp.act_bwd(d, d, out, T, C, 0, p, seed)
+        if dp is not None:
+            sp.rowscale_add(_dense(out), _dense(out), T, C, scale=dp, sgrp=grp)
+    else:
+        sp.rowscale_add(_dense(d), _dense(out), T, C, scale=dp, sgrp=grp)
     return out
 
 
@@ -343,9 +358,7 @@ class _EncoderFn(torch.autograd.Function):
         dout = dout.contiguous().to(dt)
         dev = dout.device
         # FFN branch
-        dz2 = _dense_copy(_dense(dout), T, C, dt, S["dp2"], N)
-        if p_ff > 0:
-            sp.act_bwd(dz2, dz2, dz2, T, C, 0, p_ff, seeds[3])
+        dz2 = _branch_grad(dout, T, C, dt, S["dp2"], N, p_ff, seeds[3])
         dh = _dgrad(dz2, W_["w2"])
         gw2, gb2 = _wgrad(dz2, S["h"]), _colsum(dz2)
         F_ = dh.shape[1]
@@ -357,9 +370,7 @@ class _EncoderFn(torch.autograd.Function):
         dt2 = dout.clone()
         gn2g, gn2b = sp.ln_bwd(_dense(S["t2"]), S["s2"], W_["n2g"], _dense(da2), _dense(dt2), T, C, add=_dense(dt2))
         # attention branch
-        dzo = _dense_copy(_dense(dt2), T, C, dt, S["dp1"], N)
-        if p_ff > 0:
-            sp.act_bwd(dzo, dzo, dzo, T, C, 0, p_ff, seeds[1])
+        dzo = _branch_grad(dt2, T, C, dt, S["dp1"], N, p_ff, seeds[1])
         do = _dgrad(dzo, W_["wo"])
         gwo = _wgrad(dzo, S["o"])
         qkvn, Pm, Pd = S["qkvn"], S["P"], S["Pd"]
