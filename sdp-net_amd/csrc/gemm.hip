@@ -619,6 +619,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   }
   tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
 }
+
 #undef SDP_VMCNT
 
 }  // namespace fast

@@ -366,6 +366,8 @@ def test_nchw_add_table():
 
 @pytest.mark.parametrize("kern", [9, 14])
 @pytest.mark.parametrize("M,N,K,act,res", [(1000, 768, 768, 1, True), (300, 384, 128, 0, False),
+                                           (9000, 3072, 768, 1, False), (70000, 768, 768, 1, True),
+                                           (66000, 768, 3072, 0, True), (20000, 2304, 768, 3, False),
                                            (777, 3072, 768, 1, False), (520, 768, 3072, 0, True),
                                            (256, 256, 64, 3, True), (600, 2304, 192, 0, False),
                                            (5000, 768, 768, 1, True), (3000, 512, 640, 0, True)])
@@ -407,6 +409,7 @@ def test_row_partials_and_ln_stats(dtype, M, C):
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
 @pytest.mark.parametrize("kern", [9, 14])
 @pytest.mark.parametrize("M,N,K,act,has_b", [(600, 3072, 768, 1, False), (700, 768, 768, 0, True),
+                                             (30000, 3072, 768, 1, False), (90000, 768, 768, 0, True),
                                              (513, 2304, 768, 0, False), (100, 200, 128, 1, True)])
 def test_gemm_ln_fold(dtype, kern, M, N, K, act, has_b):
     """LN(x) . W^T + b computed as the folded GEMM (sdp_fold_ln_weight + sdp_gemm_ln)."""
@@ -434,7 +437,8 @@ def test_gemm_ln_fold(dtype, kern, M, N, K, act, has_b):
 
 
 @pytest.mark.parametrize("kern", [9, 14])
-@pytest.mark.parametrize("M,N,K", [(600, 768, 768), (257, 768, 3072), (90, 128, 256), (70, 100, 64)])
+@pytest.mark.parametrize("M,N,K", [(600, 768, 768), (257, 768, 3072), (90, 128, 256), (70, 100, 64),
+                                   (80000, 768, 768), (70001, 768, 3072)])
 def test_gemm_emits_row_partials(kern, M, N, K):
     """The residual GEMM's whole-line epilogue writes the output rows' LN partials
     (other kernels: the library computes them after the GEMM), on a row-mapped output."""
@@ -461,3 +465,4 @@ def test_gemm_emits_row_partials(kern, M, N, K):
         close(pr[:, c, 0], mu, torch.float32, rel=1e-5, what="emitted chunk mean")
         close(pr[:, c, 1], ((blk - mu[:, None]) ** 2).sum(1), torch.float32, rel=1e-4, what="emitted chunk M2")
     assert torch.isnan(part.view(B_, Nt, nch, 2)[:, :R]).all()  # register rows untouched
+
