@@ -308,6 +308,11 @@ int sdp_ln_apply(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gst
                  const float* stats, const float* gamma, const float* beta, void* Y, int64_t ldy, int y_grp,
                  int64_t y_gstride, int y_off, int M, int C, void* stream);
 int sdp_ln_bwd_blocks(int M);
+/* Training-forward LayerNorm in one pass: stats[m] = (mean, rstd) and Y = LN(X) (C % 8 == 0,
+ * C <= 2048, 16-B aligned rows). */
+int sdp_ln_fwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, float eps,
+               const float* gamma, const float* beta, float* stats, void* Y, int64_t ldy, int y_grp,
+               int64_t y_gstride, int y_off, int M, int C, void* stream);
 int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, const float* stats,
                const float* gamma, const void* DY, int64_t lddy, int dy_grp, int64_t dy_gstride, int dy_off,
                const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride, int a_off, void* DX, int64_t lddx,

@@ -761,6 +761,162 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ X, int64_t
   }
 }
 
+// Same backward, 8 consecutive channels per lane (16-B accesses; C % 8 == 0, aligned rows):
+// lane covers channels 8 * lane + 512 * i, i < V.
+template <typename T, int V>
+__global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_t ldx, RowMap xm,
+                                                 const float* __restrict__ st, const float* __restrict__ g,
+                                                 const T* __restrict__ DY, int64_t lddy, RowMap dym,
+                                                 const T* __restrict__ ADD, int64_t ldadd, RowMap am,
+                                                 T* __restrict__ DX, int64_t lddx, RowMap dxm, int M, int C,
+                                                 float* __restrict__ part) {
+  extern __shared__ float red[];  // [2][4][C]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float dg[V][8], db[V][8];
+#pragma unroll
+  for (int i = 0; i < V; ++i)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dg[i][q] = db[i][q] = 0.f;
+  for (int64_t m = (int64_t)blockIdx.x * 4 + w; m < M; m += (int64_t)gridDim.x * 4) {
+    const float mean = st[2 * m], rstd = st[2 * m + 1];
+    const T* xp = X + xm(m) * ldx;
+    const T* dyp = DY + dym(m) * lddy;
+    V8<T> xh[V], gd[V];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int c = 8 * lane + 512 * i;
+      if (c < C) {
+        V8<T> dy;
+        dy.load(dyp + c);
+        xh[i].load(xp + c);
+        const f32x4 g0 = *(const f32x4*)(g + c), g1 = *(const f32x4*)(g + c + 4);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float x_ = (xh[i].v[q] - mean) * rstd;
+          xh[i].v[q] = x_;
+          gd[i].v[q] = dy.v[q] * (q < 4 ? g0[q] : g1[q - 4]);
+          dg[i][q] = fmaf(dy.v[q], x_, dg[i][q]);
+          db[i][q] += dy.v[q];
+          s1 += gd[i].v[q];
+          s2 = fmaf(gd[i].v[q], x_, s2);
+        }
+      }
+    }
+    s1 = wave_sum(s1) / (float)C;
+    s2 = wave_sum(s2) / (float)C;
+    T* dxp = DX + dxm(m) * lddx;
+    const T* ap = ADD ? ADD + am(m) * ldadd : nullptr;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int c = 8 * lane + 512 * i;
+      if (c < C) {
+        V8<T> o;
+        if (ap) o.load(ap + c);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float v = rstd * (gd[i].v[q] - s1 - xh[i].v[q] * s2);
+          o.v[q] = ap ? o.v[q] + v : v;
+        }
+        o.store(dxp + c);
+      }
+    }
+  }
+  if (!part) return;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int c = 8 * lane + 512 * i;
+    if (c < C) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        red[(0 * 4 + w) * C + c + q] = dg[i][q];
+        red[(1 * 4 + w) * C + c + q] = db[i][q];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    part[(int64_t)blockIdx.x * 2 * C + c] = red[0 * C + c] + red[1 * C + c] + red[2 * C + c] + red[3 * C + c];
+    part[(int64_t)blockIdx.x * 2 * C + C + c] =
+        red[4 * C + c] + red[5 * C + c] + red[6 * C + c] + red[7 * C + c];
+  }
+}
+
+// LayerNorm forward that also writes its statistics (training forward keeps them for the
+// backward): one wave per row, 8 consecutive channels per lane (C % 8 == 0, <= 2048).
+template <typename T, int V>
+__global__ __launch_bounds__(256) void ln_fwd_v8(const T* __restrict__ X, int64_t ldx, RowMap xm, float eps,
+                                                 const float* __restrict__ g, const float* __restrict__ b,
+                                                 float* __restrict__ st, T* __restrict__ Y, int64_t ldy, RowMap ym,
+                                                 int M, int C) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const T* xp = X + xm(m) * ldx;
+  V8<T> x[V];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int c = 8 * lane + 512 * i;
+    if (c < C) {
+      x[i].load(xp + c);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += x[i].v[q];
+    }
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int c = 8 * lane + 512 * i;
+    if (c < C) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ss = fmaf(x[i].v[q] - mean, x[i].v[q] - mean, ss);
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)C + eps);
+  if (lane == 0) *(float2*)(st + 2 * m) = float2{mean, rstd};
+  T* yp = Y + ym(m) * ldy;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int c = 8 * lane + 512 * i;
+    if (c < C) {
+      const f32x4 g0 = *(const f32x4*)(g + c), g1 = *(const f32x4*)(g + c + 4);
+      const f32x4 b0 = *(const f32x4*)(b + c), b1 = *(const f32x4*)(b + c + 4);
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        x[i].v[q] = (x[i].v[q] - mean) * rstd * (q < 4 ? g0[q] : g1[q - 4]) + (q < 4 ? b0[q] : b1[q - 4]);
+      x[i].store(yp + c);
+    }
+  }
+}
+
+extern "C" int sdp_ln_fwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, float eps,
+                          const float* gamma, const float* beta, float* stats, void* Y, int64_t ldy, int y_grp,
+                          int64_t y_gstride, int y_off, int M, int C, void* stream) {
+  if (!X || !Y || !stats || !gamma || !beta || M < 0 || C <= 0 || C > 2048 || C % 8) return (int)hipErrorInvalidValue;
+  if (ldx % 8 || ldy % 8 || (uintptr_t)X % 16 || (uintptr_t)Y % 16 || (uintptr_t)gamma % 16 || (uintptr_t)beta % 16 ||
+      (uintptr_t)stats % 8)
+    return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), ym = mk_tmap(y_grp, y_gstride, y_off);
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((M + 3) / 4);
+  const int v8 = (C + 511) / 512;
+#define SDP_LNF(TT, VV)                                                                                       \
+  hipLaunchKernelGGL((ln_fwd_v8<TT, VV>), grid, dim3(256), 0, s, (const TT*)X, ldx, xm, eps, gamma, beta, stats, \
+                     (TT*)Y, ldy, ym, M, C)
+  if (dtype == 1) {
+    if (v8 <= 1) SDP_LNF(bf16_t, 1); else if (v8 <= 2) SDP_LNF(bf16_t, 2); else SDP_LNF(bf16_t, 4);
+  } else if (dtype == 0) {
+    if (v8 <= 1) SDP_LNF(float, 1); else if (v8 <= 2) SDP_LNF(float, 2); else SDP_LNF(float, 4);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+#undef SDP_LNF
+  return SDP_CHECK_LAUNCH();
+}
+
 extern "C" int sdp_ln_apply(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
                             const float* stats, const float* gamma, const float* beta, void* Y, int64_t ldy, int y_grp,
                             int64_t y_gstride, int y_off, int M, int C, void* stream) {
@@ -799,6 +955,26 @@ extern "C" int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int6
   dim3 grid(sdp_ln_bwd_blocks(M));
   const size_t lds = (size_t)8 * C * sizeof(float);
   const int v = (C + 63) / 64;
+  const int es = dtype == 1 ? 2 : 4;
+  const bool vec = C % 8 == 0 && ldx % 8 == 0 && lddy % 8 == 0 && lddx % 8 == 0 && (!ADD || ldadd % 8 == 0) &&
+                   (uintptr_t)X % 16 == 0 && (uintptr_t)DY % 16 == 0 && (uintptr_t)DX % 16 == 0 &&
+                   (!ADD || (uintptr_t)ADD % 16 == 0) && (uintptr_t)gamma % 16 == 0 && C <= 2048;
+  (void)es;
+  if (vec) {
+#define SDP_LNV(TT, VV)                                                                                          \
+  hipLaunchKernelGGL((ln_bwd_v8<TT, VV>), grid, dim3(256), lds, s, (const TT*)X, ldx, xm, stats, gamma, (const TT*)DY, \
+                     lddy, dym, (const TT*)ADD, ldadd, am, (TT*)DX, lddx, dxm, M, C, part)
+    const int v8 = (C + 511) / 512;
+    if (dtype == 1) {
+      if (v8 <= 1) SDP_LNV(bf16_t, 1); else if (v8 <= 2) SDP_LNV(bf16_t, 2); else SDP_LNV(bf16_t, 4);
+    } else if (dtype == 0) {
+      if (v8 <= 1) SDP_LNV(float, 1); else if (v8 <= 2) SDP_LNV(float, 2); else SDP_LNV(float, 4);
+    } else {
+      return (int)hipErrorInvalidValue;
+    }
+#undef SDP_LNV
+    return SDP_CHECK_LAUNCH();
+  }
 #define SDP_LNB(TT, VV)                                                                                          \
   hipLaunchKernelGGL((ln_bwd_k<TT, VV>), grid, dim3(256), lds, s, (const TT*)X, ldx, xm, stats, gamma, (const TT*)DY, \
                      lddy, dym, (const TT*)ADD, ldadd, am, (TT*)DX, lddx, dxm, M, C, part)
@@ -875,12 +1051,141 @@ __global__ __launch_bounds__(256) void softmax_bwd_k(const T* __restrict__ P, in
   }
 }
 
+// Register-resident rows (Npad <= 512, Npad % 4 == 0): lane holds 4-column chunks lane and
+// lane + 64; one read of S, one write of P / Pd.
+template <typename T>
+SDP_DEV void store4(T* p, const float (&v)[4]) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x4 t;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = (short)f2bf(v[q]);
+    *(bf16x4*)p = t;
+  } else {
+    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  }
+}
+template <typename T>
+SDP_DEV void load4(const T* p, float (&v)[4]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x4 t = *(const bf16x4*)p;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = bf2f((bf16_t)t[q]);
+  } else {
+    const f32x4 t = *(const f32x4*)p;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = t[q];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_fwd_r(const float* __restrict__ S, int64_t lds, T* __restrict__ P,
+                                                     T* __restrict__ Pd, int64_t ldp, int rows, int N, int Npad,
+                                                     float scale, float p, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* sp_ = S + r * lds;
+  float v[2][4];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = 4 * (lane + 64 * i);
+    if (c < Npad) {
+      const f32x4 t = *(const f32x4*)(sp_ + c);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[i][q] = c + q < N ? t[q] * scale : -INFINITY;
+        mx = fmaxf(mx, v[i][q]);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[i][q] = -INFINITY;
+    }
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[i][q] = v[i][q] == -INFINITY ? 0.f : expf(v[i][q] - mx);
+      sum += v[i][q];
+    }
+  const float inv = 1.0f / wave_sum(sum), kp = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = 4 * (lane + 64 * i);
+    if (c < Npad) {
+      float o[4], d[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        o[q] = v[i][q] * inv;
+        d[q] = o[q];
+        if (p > 0.f && c + q < N) d[q] = uniform01(seed, (uint64_t)r * N + c + q) >= p ? o[q] * kp : 0.f;
+      }
+      store4<T>(P + r * ldp + c, o);
+      if (Pd) store4<T>(Pd + r * ldp + c, d);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_bwd_r(const T* __restrict__ P, int64_t ldp, const T* __restrict__ DPd,
+                                                     int64_t lddp, T* __restrict__ DS, int64_t ldds, int rows, int N,
+                                                     int Npad, float p, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float kp = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  float pv[2][4], g[2][4];
+  float dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = 4 * (lane + 64 * i);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pv[i][q] = g[i][q] = 0.f;
+    if (c < Npad) {
+      load4<T>(P + r * ldp + c, pv[i]);
+      load4<T>(DPd + r * lddp + c, g[i]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (c + q >= N) { g[i][q] = 0.f; pv[i][q] = 0.f; }
+        else if (p > 0.f) g[i][q] = uniform01(seed, (uint64_t)r * N + c + q) >= p ? g[i][q] * kp : 0.f;
+        dot = fmaf(g[i][q], pv[i][q], dot);
+      }
+    }
+  }
+  dot = wave_sum(dot);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = 4 * (lane + 64 * i);
+    if (c < Npad) {
+      float o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = pv[i][q] * (g[i][q] - dot);
+      store4<T>(DS + r * ldds + c, o);
+    }
+  }
+}
+
 extern "C" int sdp_softmax_fwd(int dtype, const float* S, int64_t lds, void* P, void* Pd, int64_t ldp, int rows, int N,
                                int Npad, float scale, float p, uint64_t seed, void* stream) {
   if (!S || !P || rows < 0 || N <= 0 || Npad < N || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;
   if (rows == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((rows + 3) / 4);
+  if (Npad <= 512 && Npad % 4 == 0 && lds % 4 == 0 && ldp % 4 == 0 && (uintptr_t)S % 16 == 0 && (uintptr_t)P % 16 == 0 &&
+      (!Pd || (uintptr_t)Pd % 16 == 0)) {
+    if (dtype == 1)
+      hipLaunchKernelGGL(softmax_fwd_r<bf16_t>, grid, dim3(256), 0, s, S, lds, (bf16_t*)P, (bf16_t*)Pd, ldp, rows, N,
+                         Npad, scale, p, seed);
+    else if (dtype == 0)
+      hipLaunchKernelGGL(softmax_fwd_r<float>, grid, dim3(256), 0, s, S, lds, (float*)P, (float*)Pd, ldp, rows, N,
+                         Npad, scale, p, seed);
+    else
+      return (int)hipErrorInvalidValue;
+    return SDP_CHECK_LAUNCH();
+  }
   if (dtype == 1)
     hipLaunchKernelGGL(softmax_fwd_k<bf16_t>, grid, dim3(256), 0, s, S, lds, (bf16_t*)P, (bf16_t*)Pd, ldp, rows, N,
                        Npad, scale, p, seed);
@@ -898,6 +1203,18 @@ extern "C" int sdp_softmax_bwd(int dtype, const void* P, int64_t ldp, const void
   if (rows == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((rows + 3) / 4);
+  if (Npad <= 512 && Npad % 4 == 0 && ldp % 4 == 0 && lddp % 4 == 0 && ldds % 4 == 0 && (uintptr_t)P % 16 == 0 &&
+      (uintptr_t)DPd % 16 == 0 && (uintptr_t)DS % 16 == 0) {
+    if (dtype == 1)
+      hipLaunchKernelGGL(softmax_bwd_r<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)P, ldp, (const bf16_t*)DPd, lddp,
+                         (bf16_t*)DS, ldds, rows, N, Npad, p, seed);
+    else if (dtype == 0)
+      hipLaunchKernelGGL(softmax_bwd_r<float>, grid, dim3(256), 0, s, (const float*)P, ldp, (const float*)DPd, lddp,
+                         (float*)DS, ldds, rows, N, Npad, p, seed);
+    else
+      return (int)hipErrorInvalidValue;
+    return SDP_CHECK_LAUNCH();
+  }
   if (dtype == 1)
     hipLaunchKernelGGL(softmax_bwd_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)P, ldp, (const bf16_t*)DPd, lddp,
                        (bf16_t*)DS, ldds, rows, N, Npad, p, seed);

@@ -77,6 +77,7 @@ _SIGS = {
                           _vp], _i32),
     "sdp_ln_apply": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_ln_bwd_blocks": ([_i32], _i32),
+    "sdp_ln_fwd": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_ln_bwd": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _vp, _i64,
                     *_ROWMAP, _i32, _i32, _vp, _vp], _i32),
     "sdp_softmax_fwd": ([_i32, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _f32, _f32, _u64, _vp], _i32),
@@ -542,7 +543,16 @@ def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows
     if part is None:
         return None
     out = torch.empty(2, C, dtype=torch.float32, device=dx.t.device)
-    seg_colsum(part.view(nb, 2 * C), out.view(1, 2 * C), 1, nb, 0, 1, 2 * C)
+    if nb >= 128:  # two levels: 32-row chunk sums in parallel, then the chunk sums
+        g = nb // 32
+        tmp = torch.empty(g + 1, 2 * C, dtype=torch.float32, device=dx.t.device)
+        seg_colsum(part.view(nb, 2 * C), tmp, g, 32, 32, 1, 2 * C)
+        rest = nb - 32 * g
+        if rest:
+            seg_colsum(part.view(nb, 2 * C), tmp[g:], 1, rest, 0, 1, 2 * C, x_off=32 * g * 2 * C)
+        seg_colsum(tmp, out.view(1, 2 * C), 1, g + (1 if rest else 0), 0, 1, 2 * C)
+    else:
+        seg_colsum(part.view(nb, 2 * C), out.view(1, 2 * C), 1, nb, 0, 1, 2 * C)
     return out[0], out[1]
 
 
@@ -596,3 +606,12 @@ def transpose(x: torch.Tensor) -> torch.Tensor:
     rc = lib().sdp_transpose(dcode(x.dtype), x.data_ptr(), x.stride(0), y.data_ptr(), R, R, C, _stream(y))
     _check(rc, "transpose")
     return y
+
+
+def ln_fwd(x: Rows, eps: float, gamma: torch.Tensor, beta: torch.Tensor, stats: torch.Tensor, y: Rows, M: int, C: int):
+    """One-pass LayerNorm that also writes its (mean, rstd) statistics (training forward)."""
+    _need_cuda(x.t, y.t, gamma, beta, stats)
+    _req(stats.dtype == gamma.dtype == beta.dtype == torch.float32, "ln_fwd fp32 params")
+    rc = lib().sdp_ln_fwd(dcode(x.t.dtype), *x.args(), float(eps), gamma.data_ptr(), beta.data_ptr(),
+                          stats.data_ptr(), *y.args(), M, C, _stream(y.t))
+    _check(rc, "ln_fwd")

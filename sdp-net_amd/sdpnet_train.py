@@ -163,11 +163,23 @@ def _branch_grad(d: torch.Tensor, T: int, C: int, dt, dp: Optional[torch.Tensor]
     return out
 
 
+def _with_regs(src: torch.Tensor, B: int, R: int, N: int, C: int) -> torch.Tensor:
+    """A new token buffer whose register rows are copied from ``src`` (the image rows are
+    about to be written in full by the caller)."""
+    out = torch.empty_like(src)
+    if R:
+        sp.copy_rows(src, C, N * C, out, C, N * C, B, R, C)
+    return out
+
+
 def _ln_fwd(x: Rows, M: int, C: int, g: torch.Tensor, b: torch.Tensor, eps: float, dt):
     st = _empty((M, 2), torch.float32, x.t.device)
-    sp.rowstats(x, eps, st, M, C)
     a = _empty((M, C), dt, x.t.device)
-    sp.ln_apply(x, st, g, b, _dense(a), M, C)
+    if C % 8 == 0 and C <= 2048 and x.ld % 8 == 0:
+        sp.ln_fwd(x, eps, g, b, st, _dense(a), M, C)      # one pass: stats + normalized rows
+    else:
+        sp.rowstats(x, eps, st, M, C)
+        sp.ln_apply(x, st, g, b, _dense(a), M, C)
     return a, st
 
 
@@ -209,7 +221,7 @@ class _MixerFn(torch.autograd.Function):
         z1 = _linear(d, W_["ccw"], W_["ccb"], dt)
         h1 = _empty((M, C), dt, dev)
         sp.act_fwd(z1, h1, M, C, act)
-        mid = tok.clone()
+        mid = _with_regs(tok, B, R, N, C)
         imid = Rows(mid, C, P, N, R)
         sp.rowscale_add(_dense(h1), imid, M, C, scale=dp2, sgrp=P, resid=img)
         # x = drop_path_1(PW_down(act(PW_up(LN2 x_)))) + x_
@@ -218,7 +230,7 @@ class _MixerFn(torch.autograd.Function):
         h = _empty((M, 4 * C), dt, dev)
         sp.act_fwd(z2, h, M, 4 * C, act)
         z3 = _linear(h, W_["dnw"], W_["dnb"], dt)
-        out = mid.clone()
+        out = _with_regs(mid, B, R, N, C)
         sp.rowscale_add(_dense(z3), Rows(out, C, P, N, R), M, C, scale=dp1, sgrp=P, resid=imid)
         ctx.st = dict(tok=tok, mid=mid, a1=a1, s1=s1, d=d, z1=z1, a2=a2, s2=s2, z2=z2, h=h, W=W_, dp1=dp1, dp2=dp2,
                       geo=(B, R, H, W, C, k), act=act, dt=dt, has=[p is not None for p in params])
@@ -243,9 +255,9 @@ class _MixerFn(torch.autograd.Function):
         sp.act_bwd(S["z2"], dh, dz2, M, 4 * C, act)
         da2 = _dgrad(dz2, W_["upw"])
         gup, gupb = _wgrad(dz2, S["a2"]), _colsum(dz2)
-        dmid = dout.clone()
+        dmid = _with_regs(dout, B, R, N, C)
         imid = Rows(dmid, C, P, N, R)
-        gg2, gb2 = sp.ln_bwd(Rows(S["mid"], C, P, N, R), S["s2"], W_["g2"], _dense(da2), imid, M, C, add=imid)
+        gg2, gb2 = sp.ln_bwd(Rows(S["mid"], C, P, N, R), S["s2"], W_["g2"], _dense(da2), imid, M, C, add=iout)
         # branch 2
         dh1 = _dense_copy(imid, M, C, dt, S["dp2"], P)
         dz1 = _empty((M, C), dt, dev)
@@ -301,7 +313,8 @@ class _EncoderFn(torch.autograd.Function):
         qkv = _linear(a1, W_["wqkv"], None, dt)                          # :282-284
         qkvn, sq, sk = qkv, None, None
         if qn:                                                          # :286
-            qkvn = qkv.clone()
+            qkvn = _empty((T, 3 * C), dt, dev)
+            sp.copy_rows(qkv[:, 2 * C:], 3 * C, 0, qkvn[:, 2 * C:], 3 * C, 0, 1, T, C)  # v third
             rq = Rows(qkv, hd, Hn, 3 * Hn, 0)
             rk = Rows(qkv, hd, Hn, 3 * Hn, Hn)
             sq = _empty((T * Hn, 2), torch.float32, dev)
@@ -367,8 +380,8 @@ class _EncoderFn(torch.autograd.Function):
         del dh
         da2 = _dgrad(dz1, W_["w1"])
         gw1, gb1 = _wgrad(dz1, S["a2"]), _colsum(dz1)
-        dt2 = dout.clone()
-        gn2g, gn2b = sp.ln_bwd(_dense(S["t2"]), S["s2"], W_["n2g"], _dense(da2), _dense(dt2), T, C, add=_dense(dt2))
+        dt2 = _empty((T, C), dt, dev)
+        gn2g, gn2b = sp.ln_bwd(_dense(S["t2"]), S["s2"], W_["n2g"], _dense(da2), _dense(dt2), T, C, add=_dense(dout))
         # attention branch
         dzo = _branch_grad(dt2, T, C, dt, S["dp1"], N, p_ff, seeds[1])
         do = _dgrad(dzo, W_["wo"])

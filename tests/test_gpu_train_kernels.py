@@ -235,3 +235,17 @@ def test_transpose(dtype, R, C):
     assert torch.equal(sp.transpose(x), x.t().contiguous())
     y = rnd(R, C + 6, seed=26, dtype=dtype)[:, 3:3 + C]  # strided rows
     assert torch.equal(sp.transpose(y), y.t().contiguous())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("M,C", [(300, 768), (77, 96), (5, 1024), (9, 2048)])
+def test_ln_fwd_one_pass(dtype, M, C):
+    x = (rnd(M, C, seed=27, scale=1.5) + rnd(M, 1, seed=28, scale=2)).to(dtype)
+    g, b = rnd(C, seed=29) * 0.2 + 1, rnd(C, seed=30) * 0.2
+    st = torch.empty(M, 2, device=DEV)
+    y = torch.empty_like(x)
+    sp.ln_fwd(sp.dense(x), 1e-5, g, b, st, sp.dense(y), M, C)
+    xf = x.float()
+    close(st[:, 0], xf.mean(1), 1e-5, "mean")
+    close(st[:, 1], 1 / torch.sqrt(xf.var(1, unbiased=False) + 1e-5), 1e-4, "rstd")
+    close(y, F.layer_norm(xf, (C,), g, b, 1e-5), 2e-5 if dtype == torch.float32 else 2e-2, "ln_fwd")
