@@ -239,7 +239,7 @@ def train_bench(args, C, world, rank, local):
                    "parallelism": f"dp{world}" + (" DDP bucketed grad all-reduce over RCCL" if world > 1 else "")},
         "model_flops_per_image_gf": round(gf, 3),
         "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
-        "loss": round(float(loss), 4), "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
+        "loss": round(float(loss.detach()), 4), "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
