@@ -74,9 +74,14 @@ def main():
                 for s in streams:
                     cur.wait_stream(s)
 
-            for _ in range(3):
-                run()
-            torch.cuda.synchronize()
+            # warm up for ~0.5 s of GPU time so every variant is timed at the loaded clock
+            # (the host-side tensor set-up leaves the GPU idle and down-clocked)
+            import time
+            t_end = time.time() + 0.5
+            while time.time() < t_end:
+                for _ in range(5):
+                    run()
+                torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(args.reps):
