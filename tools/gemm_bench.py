@@ -45,6 +45,7 @@ def main():
     bf = torch.bfloat16
     g = torch.Generator(device="cpu").manual_seed(0)
     total_us = {}
+    ref_out = {}
     for name in args.shapes.split(","):
         M, N, K, has_b, act, has_r = SHAPES[name]
         x = (torch.rand(M, K, generator=g) * 2 - 1).to(bf).to(dev)
@@ -89,10 +90,12 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             us = 1e3 * e0.elapsed_time(e1) / args.reps
+            ref_y = ref_out.setdefault(name, y.clone())  # outputs must agree across kernels
+            diff = float((y.float() - ref_y.float()).abs().max())
             tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
             total_us[(name, kern, ns, dsy)] = us
             print(f"{name:11s} M={M:6d} N={N:5d} K={K:5d} kern={kern} streams={ns} exact_gelu={dsy} variant={sp.gemm_variant(bf, M, N, K)} "
-                  f"{us:9.1f} us  {tf:7.1f} TF/s  ({100 * tf / 2516.6:4.1f}% of bf16 peak)", flush=True)
+                  f"{us:9.1f} us  {tf:7.1f} TF/s  ({100 * tf / 2516.6:4.1f}% of bf16 peak)  max|diff vs first| {diff:.3g}", flush=True)
         if args.torch:  # vendor-library yardstick (plain GEMM, no epilogue) -- not used by the product
             import torch.nn.functional as F
             f = lambda: F.linear(x, w)  # noqa: E731
