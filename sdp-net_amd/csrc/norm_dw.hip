@@ -972,7 +972,10 @@ static int launch_dw3(int variant, int k, const void* X, int64_t ldx, RowMap xm,
   (void)hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   const int npairs = (ncg + 1) / 2;
-  int nchunk = (ncu + ncg - 1) / ncg;  // about one workgroup per CU
+  // one workgroup per CU (16 waves at ~122 VGPRs fill a CU): at most ncu workgroups, or
+  // the few left over would run as a second round after the rest had finished
+  int nchunk = (ncu / 2) / npairs;
+  if (nchunk < 1) nchunk = 1;
   if (nchunk > B) nchunk = B;
   const int ipb = (B + nchunk - 1) / nchunk;
   nchunk = (B + ipb - 1) / ipb;
