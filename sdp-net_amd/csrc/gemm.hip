@@ -808,7 +808,9 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
     e.nt_store = g_nt_store;
     {
       const int tiles_n_ = (N + fast::BN - 1) / fast::BN;
-      e.group_m = g_group_m >= 1 ? g_group_m : (tiles_n_ >= 8 ? 4 : 1);
+      // auto raster (tools/raster_traffic.py, profiles/r02_gemm_probes.md): row-major up to
+      // 9 N-tiles (N = 2304: fewest L2 misses and fastest), groups of 8 M-blocks from 12
+      e.group_m = g_group_m >= 1 ? g_group_m : (tiles_n_ >= 12 ? 8 : 1);
     }
     const bool aligned = (ldy % 4 == 0) && ((uintptr_t)Y % 8 == 0) && (!R || ((ldr % 4 == 0) && ((uintptr_t)R % 8 == 0))) &&
                          (!bias || ((uintptr_t)bias % 16 == 0)) && (ldx % 8 == 0) && ((uintptr_t)X % 16 == 0) &&
