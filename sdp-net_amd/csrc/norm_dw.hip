@@ -800,7 +800,10 @@ SDP_DEV uint32_t pack_bf16x2(float a, float b) {
   const bf16x2v v = __builtin_convertvector((f32x2){a, b}, bf16x2v);
   return __builtin_bit_cast(uint32_t, v);
 }
-constexpr int DW3_CB = 32, DW3_ROWS = 22, DW3_RS = 32;
+// plane rows are 48 elements (96 B) apart although only 32 are used: with 64-B rows a
+// ds_read_b128 lane group (16 rows of one 16-B chunk) hit every bank twice
+// (SQ_LDS_BANK_CONFLICT was 42 % of the kernel's LDS cycles)
+constexpr int DW3_CB = 32, DW3_ROWS = 22, DW3_RS = 48;
 constexpr int DW3_PLANE = DW3_ROWS * DW3_RS;  // elements per channel plane
 
 
@@ -815,7 +818,7 @@ __global__ __launch_bounds__(NT) void dwconv3_mfma(
   constexpr int NIT = 1024 / NT;            // staging items per thread (256 pixels x 4 parts)
   // channel plane cl at cl * DW3_PLANE + 16 * (cl >> 3): the +32 B skew per group of 8
   // puts the 4 planes a staging instruction writes (channels 8q + e) on distinct banks
-  __shared__ __attribute__((aligned(16))) bf16_t planes[DW3_CB * DW3_PLANE + 48];  // 45,152 B
+  __shared__ __attribute__((aligned(16))) bf16_t planes[DW3_CB * DW3_PLANE + 48];  // 67,680 B
   __shared__ __attribute__((aligned(16))) bf16_t outs[256 * DW3_CB];          // [pixel][32]  16,384 B
   __shared__ __attribute__((aligned(16))) float lnp[2 * DW3_CB];              // gamma | beta of the block's channels
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
