@@ -891,6 +891,132 @@ __global__ __launch_bounds__(256) void ln_fwd_v8(const T* __restrict__ X, int64_
   }
 }
 
+// Short rows (C <= 128, the per-head q/k LayerNorm of hd = 64..128): L = pow2 >= C / 8
+// lanes per row, 64 / L rows per wave (one wave per row would leave 52 of 64 lanes idle
+// at hd = 96); reductions stay inside each L-lane segment.
+template <int L>
+SDP_DEV float seg_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < L; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, int L>
+__global__ __launch_bounds__(256) void ln_fwd_sm(const T* __restrict__ X, int64_t ldx, RowMap xm, float eps,
+                                                 const float* __restrict__ g, const float* __restrict__ b,
+                                                 float* __restrict__ st, T* __restrict__ Y, int64_t ldy, RowMap ym,
+                                                 int M, int C) {
+  constexpr int R = 64 / L;
+  const int lane = threadIdx.x & 63, seg = lane / L, sl = lane % L;
+  const int64_t m = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * R + seg;
+  const int c = 8 * sl;
+  const bool act = m < M && c < C;
+  V8<T> x;
+  float s = 0.f;
+  if (act) {
+    x.load(X + xm(m) * ldx + c);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += x.v[q];
+  }
+  const float mean = seg_sum<L>(s) / (float)C;
+  float ss = 0.f;
+  if (act) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ss = fmaf(x.v[q] - mean, x.v[q] - mean, ss);
+  }
+  const float rstd = 1.0f / sqrtf(seg_sum<L>(ss) / (float)C + eps);
+  if (m < M && sl == 0) *(float2*)(st + 2 * m) = float2{mean, rstd};
+  if (act) {
+    const f32x4 g0 = *(const f32x4*)(g + c), g1 = *(const f32x4*)(g + c + 4);
+    const f32x4 b0 = *(const f32x4*)(b + c), b1 = *(const f32x4*)(b + c + 4);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      x.v[q] = (x.v[q] - mean) * rstd * (q < 4 ? g0[q] : g1[q - 4]) + (q < 4 ? b0[q] : b1[q - 4]);
+    x.store(Y + ym(m) * ldy + c);
+  }
+}
+
+template <typename T, int L>
+__global__ __launch_bounds__(256) void ln_bwd_sm(const T* __restrict__ X, int64_t ldx, RowMap xm,
+                                                 const float* __restrict__ st, const float* __restrict__ g,
+                                                 const T* __restrict__ DY, int64_t lddy, RowMap dym,
+                                                 const T* __restrict__ ADD, int64_t ldadd, RowMap am,
+                                                 T* __restrict__ DX, int64_t lddx, RowMap dxm, int M, int C,
+                                                 float* __restrict__ part) {
+  extern __shared__ float red[];  // [2][4][C]
+  constexpr int R = 64 / L;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, seg = lane / L, sl = lane % L;
+  const int c = 8 * sl;
+  float dg[8], db[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dg[q] = db[q] = 0.f;
+  f32x4 g0 = {0.f, 0.f, 0.f, 0.f}, g1 = g0;
+  if (c < C) {
+    g0 = *(const f32x4*)(g + c);
+    g1 = *(const f32x4*)(g + c + 4);
+  }
+  // the wave's first row decides the trip count (uniform: the segment sums shuffle)
+  for (int64_t mb = ((int64_t)blockIdx.x * 4 + w) * R; mb < M; mb += (int64_t)gridDim.x * 4 * R) {
+    const int64_t m = mb + seg;
+    const bool act = m < M && c < C;
+    float mean = 0.f, rstd = 0.f;
+    V8<T> xh, gd;
+    float s1 = 0.f, s2 = 0.f;
+    if (act) {
+      mean = st[2 * m];
+      rstd = st[2 * m + 1];
+      V8<T> dy;
+      dy.load(DY + dym(m) * lddy + c);
+      xh.load(X + xm(m) * ldx + c);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float x_ = (xh.v[q] - mean) * rstd;
+        xh.v[q] = x_;
+        gd.v[q] = dy.v[q] * (q < 4 ? g0[q] : g1[q - 4]);
+        dg[q] = fmaf(dy.v[q], x_, dg[q]);
+        db[q] += dy.v[q];
+        s1 += gd.v[q];
+        s2 = fmaf(gd.v[q], x_, s2);
+      }
+    }
+    s1 = seg_sum<L>(s1) / (float)C;
+    s2 = seg_sum<L>(s2) / (float)C;
+    if (act) {
+      V8<T> o;
+      const T* ap = ADD ? ADD + am(m) * ldadd : nullptr;
+      if (ap) o.load(ap + c);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float v = rstd * (gd.v[q] - s1 - xh.v[q] * s2);
+        o.v[q] = ap ? o.v[q] + v : v;
+      }
+      o.store(DX + dxm(m) * lddx + c);
+    }
+  }
+  if (!part) return;
+  // the R row segments of a wave hold the same channels: fold them onto segment 0
+#pragma unroll
+  for (int o = L; o < 64; o <<= 1)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      dg[q] += __shfl_xor(dg[q], o, 64);
+      db[q] += __shfl_xor(db[q], o, 64);
+    }
+  if (seg == 0 && c < C) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      red[(0 * 4 + w) * C + c + q] = dg[q];
+      red[(1 * 4 + w) * C + c + q] = db[q];
+    }
+  }
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < C; cc += 256) {
+    part[(int64_t)blockIdx.x * 2 * C + cc] = red[0 * C + cc] + red[1 * C + cc] + red[2 * C + cc] + red[3 * C + cc];
+    part[(int64_t)blockIdx.x * 2 * C + C + cc] =
+        red[4 * C + cc] + red[5 * C + cc] + red[6 * C + cc] + red[7 * C + cc];
+  }
+}
+
 extern "C" int sdp_ln_fwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, float eps,
                           const float* gamma, const float* beta, float* stats, void* Y, int64_t ldy, int y_grp,
                           int64_t y_gstride, int y_off, int M, int C, void* stream) {
@@ -901,6 +1027,18 @@ extern "C" int sdp_ln_fwd(int dtype, const void* X, int64_t ldx, int x_grp, int6
   if (M == 0) return 0;
   const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), ym = mk_tmap(y_grp, y_gstride, y_off);
   hipStream_t s = (hipStream_t)stream;
+  if (C <= 128) {  // several rows per wave
+    const int L = C <= 64 ? 8 : 16, R = 64 / L;
+    dim3 gs((M + 4 * R - 1) / (4 * R));
+#define SDP_LNFS(TT, LL)                                                                                      \
+  hipLaunchKernelGGL((ln_fwd_sm<TT, LL>), gs, dim3(256), 0, s, (const TT*)X, ldx, xm, eps, gamma, beta, stats, \
+                     (TT*)Y, ldy, ym, M, C)
+    if (dtype == 1) { if (L == 8) SDP_LNFS(bf16_t, 8); else SDP_LNFS(bf16_t, 16); }
+    else if (dtype == 0) { if (L == 8) SDP_LNFS(float, 8); else SDP_LNFS(float, 16); }
+    else return (int)hipErrorInvalidValue;
+#undef SDP_LNFS
+    return SDP_CHECK_LAUNCH();
+  }
   dim3 grid((M + 3) / 4);
   const int v8 = (C + 511) / 512;
 #define SDP_LNF(TT, VV)                                                                                       \
@@ -965,6 +1103,17 @@ extern "C" int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int6
   hipLaunchKernelGGL((ln_bwd_v8<TT, VV>), grid, dim3(256), lds, s, (const TT*)X, ldx, xm, stats, gamma, (const TT*)DY, \
                      lddy, dym, (const TT*)ADD, ldadd, am, (TT*)DX, lddx, dxm, M, C, part)
     const int v8 = (C + 511) / 512;
+    if (C <= 128) {  // several rows per wave
+#define SDP_LNVS(TT, LL)                                                                                         \
+  hipLaunchKernelGGL((ln_bwd_sm<TT, LL>), grid, dim3(256), lds, s, (const TT*)X, ldx, xm, stats, gamma, (const TT*)DY, \
+                     lddy, dym, (const TT*)ADD, ldadd, am, (TT*)DX, lddx, dxm, M, C, part)
+      const bool l8 = C <= 64;
+      if (dtype == 1) { if (l8) SDP_LNVS(bf16_t, 8); else SDP_LNVS(bf16_t, 16); }
+      else if (dtype == 0) { if (l8) SDP_LNVS(float, 8); else SDP_LNVS(float, 16); }
+      else return (int)hipErrorInvalidValue;
+#undef SDP_LNVS
+      return SDP_CHECK_LAUNCH();
+    }
     if (dtype == 1) {
       if (v8 <= 1) SDP_LNV(bf16_t, 1); else if (v8 <= 2) SDP_LNV(bf16_t, 2); else SDP_LNV(bf16_t, 4);
     } else if (dtype == 0) {

@@ -319,10 +319,14 @@ class _EncoderFn(torch.autograd.Function):
             rk = Rows(qkv, hd, Hn, 3 * Hn, Hn)
             sq = _empty((T * Hn, 2), torch.float32, dev)
             sk = _empty((T * Hn, 2), torch.float32, dev)
-            sp.rowstats(rq, e.q_norm.eps, sq, T * Hn, hd)
-            sp.rowstats(rk, e.k_norm.eps, sk, T * Hn, hd)
-            sp.ln_apply(rq, sq, W_["qg"], W_["qb"], Rows(qkvn, hd, Hn, 3 * Hn, 0), T * Hn, hd)
-            sp.ln_apply(rk, sk, W_["kg"], W_["kb"], Rows(qkvn, hd, Hn, 3 * Hn, Hn), T * Hn, hd)
+            if hd % 8 == 0:  # one pass, several heads per wave (ln_fwd_sm)
+                sp.ln_fwd(rq, e.q_norm.eps, W_["qg"], W_["qb"], sq, Rows(qkvn, hd, Hn, 3 * Hn, 0), T * Hn, hd)
+                sp.ln_fwd(rk, e.k_norm.eps, W_["kg"], W_["kb"], sk, Rows(qkvn, hd, Hn, 3 * Hn, Hn), T * Hn, hd)
+            else:
+                sp.rowstats(rq, e.q_norm.eps, sq, T * Hn, hd)
+                sp.rowstats(rk, e.k_norm.eps, sk, T * Hn, hd)
+                sp.ln_apply(rq, sq, W_["qg"], W_["qb"], Rows(qkvn, hd, Hn, 3 * Hn, 0), T * Hn, hd)
+                sp.ln_apply(rk, sk, W_["kg"], W_["kb"], Rows(qkvn, hd, Hn, 3 * Hn, Hn), T * Hn, hd)
         # attention (:289-298): S = QK^T, P = softmax(S / sqrt(hd)), Pd = dropout(P), O = Pd V
         Np = (N + 7) // 8 * 8
         Z = B * Hn

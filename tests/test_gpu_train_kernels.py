@@ -141,7 +141,8 @@ def test_dropout_mask_consistent():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
-@pytest.mark.parametrize("M,C,eps", [(300, 768, 1e-6), (77, 96, 1e-5), (5, 64, 1e-5)])
+@pytest.mark.parametrize("M,C,eps", [(300, 768, 1e-6), (77, 96, 1e-5), (5, 64, 1e-5), (20011, 96, 1e-5),
+                                     (333, 128, 1e-5), (70, 32, 1e-5)])
 def test_layernorm_fwd_bwd(dtype, M, C, eps):
     x = (rnd(M, C, seed=13, scale=1.5) + rnd(M, 1, seed=14, scale=2)).to(dtype)
     g = rnd(C, seed=15) * 0.2 + 1
@@ -238,7 +239,7 @@ def test_transpose(dtype, R, C):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
-@pytest.mark.parametrize("M,C", [(300, 768), (77, 96), (5, 1024), (9, 2048)])
+@pytest.mark.parametrize("M,C", [(300, 768), (77, 96), (5, 1024), (9, 2048), (61, 64), (1, 128), (130, 16)])
 def test_ln_fwd_one_pass(dtype, M, C):
     x = (rnd(M, C, seed=27, scale=1.5) + rnd(M, 1, seed=28, scale=2)).to(dtype)
     g, b = rnd(C, seed=29) * 0.2 + 1, rnd(C, seed=30) * 0.2
@@ -249,3 +250,32 @@ def test_ln_fwd_one_pass(dtype, M, C):
     close(st[:, 0], xf.mean(1), 1e-5, "mean")
     close(st[:, 1], 1 / torch.sqrt(xf.var(1, unbiased=False) + 1e-5), 1e-4, "rstd")
     close(y, F.layer_norm(xf, (C,), g, b, 1e-5), 2e-5 if dtype == torch.float32 else 2e-2, "ln_fwd")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+def test_head_layernorm_on_qkv_rows(dtype):
+    """The training q/k LayerNorm: per-head rows of hd = 96 inside a [T, 3C] QKV buffer
+    (Rows(qkv, hd, H, 3H, off)), several heads per wave (ln_fwd_sm / ln_bwd_sm)."""
+    T, H, hd, eps = 1001, 8, 96, 1e-5
+    C = H * hd
+    qkv = rnd(T, 3 * C, seed=31, dtype=dtype, scale=1.5)
+    g, b = rnd(hd, seed=32) * 0.2 + 1, rnd(hd, seed=33) * 0.2
+    out = torch.zeros_like(qkv)
+    st = torch.empty(T * H, 2, device=DEV)
+    sp.ln_fwd(sp.Rows(qkv, hd, H, 3 * H, H), eps, g, b, st, sp.Rows(out, hd, H, 3 * H, H), T * H, hd)
+    k = qkv[:, C:2 * C].float().reshape(T, H, hd)
+    kr = k.clone().requires_grad_(True)
+    ref = F.layer_norm(kr, (hd,), g, b, eps)
+    close(out[:, C:2 * C].reshape(T, H, hd), ref.detach(), 2e-5 if dtype == torch.float32 else 2e-2, "head ln fwd")
+    assert (out[:, :C] == 0).all() and (out[:, 2 * C:] == 0).all()
+    dy = torch.zeros_like(qkv)
+    dy[:, C:2 * C] = rnd(T, C, seed=34, dtype=dtype)
+    dx = torch.zeros_like(qkv)
+    dg, db = sp.ln_bwd(sp.Rows(qkv, hd, H, 3 * H, H), st, g, sp.Rows(dy, hd, H, 3 * H, H),
+                       sp.Rows(dx, hd, H, 3 * H, H), T * H, hd)
+    gx, = torch.autograd.grad(ref, kr, dy[:, C:2 * C].float().reshape(T, H, hd))
+    tol = 8e-5 if dtype == torch.float32 else 8e-2
+    close(dx[:, C:2 * C].reshape(T, H, hd), gx, tol, "head ln dx")
+    xh = (k - k.mean(-1, keepdim=True)) / torch.sqrt(k.var(-1, unbiased=False, keepdim=True) + eps)
+    close(dg, (dy[:, C:2 * C].float().reshape(T, H, hd) * xh).sum((0, 1)), tol * 10, "head ln dgamma")
+    close(db, dy[:, C:2 * C].float().reshape(T, H, hd).sum((0, 1)), tol * 10, "head ln dbeta")
