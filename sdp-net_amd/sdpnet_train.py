@@ -250,11 +250,12 @@ class _MixerFn(torch.autograd.Function):
         # branch 1
         dz3 = _dense_copy(iout, M, C, dt, S["dp1"], P)
         dh = _dgrad(dz3, W_["dnw"])
-        gdn, gdnb = _wgrad(dz3, S["h"]), _colsum(dz3)
+        has = S["has"]  # [g1, b1, dww, dwb, ccw, ccb, g2, b2, upw, upb, dnw, dnb]: bias grads only if the bias exists
+        gdn, gdnb = _wgrad(dz3, S["h"]), (_colsum(dz3) if has[11] else None)
         dz2 = _empty((M, 4 * C), dt, dev)
         sp.act_bwd(S["z2"], dh, dz2, M, 4 * C, act)
         da2 = _dgrad(dz2, W_["upw"])
-        gup, gupb = _wgrad(dz2, S["a2"]), _colsum(dz2)
+        gup, gupb = _wgrad(dz2, S["a2"]), (_colsum(dz2) if has[9] else None)
         dmid = _with_regs(dout, B, R, N, C)
         imid = Rows(dmid, C, P, N, R)
         gg2, gb2 = sp.ln_bwd(Rows(S["mid"], C, P, N, R), S["s2"], W_["g2"], _dense(da2), imid, M, C, add=iout)
@@ -263,12 +264,12 @@ class _MixerFn(torch.autograd.Function):
         dz1 = _empty((M, C), dt, dev)
         sp.act_bwd(S["z1"], dh1, dz1, M, C, act)
         dd = _dgrad(dz1, W_["ccw"])
-        gcc, gccb = _wgrad(dz1, S["d"]), _colsum(dz1)
+        gcc, gccb = _wgrad(dz1, S["d"]), (_colsum(dz1) if has[5] else None)
         da1 = _empty((M, C), dt, dev)
         wflip = W_["dww"].view(C, k, k).flip(1, 2).reshape(C, k * k).contiguous()
         sp.dwconv(_dense(dd), wflip, None, _dense(da1), B, H, W, C, k)
         gdw = sp.dw_wgrad(_dense(S["a1"]), _dense(dd), B, H, W, C, k)
-        gdwb = _colsum(dd)
+        gdwb = _colsum(dd) if has[3] else None
         dx = dmid  # residual; LN1's input gradient is added in place on the image rows
         idx = Rows(dx, C, P, N, R)
         gg1, gb1 = sp.ln_bwd(Rows(S["tok"], C, P, N, R), S["s1"], W_["g1"], _dense(da1), idx, M, C, add=idx)
