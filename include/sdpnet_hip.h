@@ -87,7 +87,7 @@ int sdp_gemm_set_fast_kernel(int k);
 int sdp_gemm_set_store_policy(int nt);
 
 /* Tile raster of the 8-phase GEMM: M-blocks per group (consecutive blocks walk a group of
- * gm M-blocks before the next N-tile).  1 = row-major, -1 = auto (4 when N spans >= 8
+ * gm M-blocks before the next N-tile).  1 = row-major, -1 = auto (8 when N spans >= 12
  * tiles, else 1).  Results do not depend on it.  Returns the previous value. */
 int sdp_gemm_set_group_m(int gm);
 
