@@ -298,6 +298,13 @@ int sdp_act_bwd(int dtype, const void* Z, int64_t ldz, const void* DY, int64_t l
 int sdp_rowscale_add(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
                      const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp, int64_t r_gstride, int r_off,
                      void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int M, int N, void* stream);
+/* Y[m] = act(X[m]) * scale[m / sgrp] + R[m] (act's output rounded to dtype first, as sdp_act_fwd
+ * stores it): the activation + drop path + residual add of a ConvMixer branch
+ * (layers.py:83-104, utility_layers.py:16-27) in one pass, without the activation buffer. */
+int sdp_act_rowscale_add(int dtype, int act, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                         const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp, int64_t r_gstride,
+                         int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int M, int N,
+                         void* stream);
 
 /* LayerNorm from given statistics (stats[2m] = mean, stats[2m+1] = rstd, from sdp_rowstats):
  * Y = (X - mean) * rstd * gamma + beta; and its backward

@@ -511,7 +511,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void rowscale_v8(const T* __restrict__ X, int64_t ldx, RowMap xm,
                                                    const float* __restrict__ sc, int sgrp, const T* __restrict__ R,
                                                    int64_t ldr, RowMap rm, T* __restrict__ Y, int64_t ldy, RowMap ym,
-                                                   int M, int N) {
+                                                   int M, int N, int act) {
   const int n8 = N >> 3;
   const int64_t total = (int64_t)M * n8;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
@@ -519,6 +519,10 @@ __global__ __launch_bounds__(256) void rowscale_v8(const T* __restrict__ X, int6
     const int n = (int)(e - m * n8) * 8;
     V8<T> x;
     x.load(X + xm(m) * ldx + n);
+    if (act != ACT_NONE) {  // = sdp_act_fwd's stored output (rounded to T) without the round trip
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x.v[q] = to_f<T>(from_f<T>(apply_act(act, x.v[q])));
+    }
     const float s_ = sc ? sc[m / sgrp] : 1.0f;
     if (R) {
       V8<T> r;
@@ -629,21 +633,23 @@ template <typename T>
 __global__ __launch_bounds__(256) void rowscale_k(const T* __restrict__ X, int64_t ldx, RowMap xm,
                                                   const float* __restrict__ sc, int sgrp, const T* __restrict__ R,
                                                   int64_t ldr, RowMap rm, T* __restrict__ Y, int64_t ldy, RowMap ym,
-                                                  int M, int N) {
+                                                  int M, int N, int act) {
   const int64_t total = (int64_t)M * N;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     const int64_t m = e / N, n = e % N;
-    float v = to_f<T>(X[xm(m) * ldx + n]) * (sc ? sc[m / sgrp] : 1.0f);
+    float x = to_f<T>(X[xm(m) * ldx + n]);
+    if (act != ACT_NONE) x = to_f<T>(from_f<T>(apply_act(act, x)));
+    float v = x * (sc ? sc[m / sgrp] : 1.0f);
     if (R) v += to_f<T>(R[rm(m) * ldr + n]);
     Y[ym(m) * ldy + n] = from_f<T>(v);
   }
 }
 
-extern "C" int sdp_rowscale_add(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
-                                const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp, int64_t r_gstride,
-                                int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int M, int N,
-                                void* stream) {
-  if (!X || !Y || M < 0 || N < 0 || (scale && sgrp <= 0)) return (int)hipErrorInvalidValue;
+static int rowscale_impl(int dtype, int act, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                         const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp, int64_t r_gstride,
+                         int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int M, int N,
+                         void* stream) {
+  if (!X || !Y || M < 0 || N < 0 || (scale && sgrp <= 0) || act < 0 || act > ACT_KELU) return (int)hipErrorInvalidValue;
   if ((int64_t)M * N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), rm = mk_tmap(r_grp, r_gstride, r_off),
@@ -653,10 +659,10 @@ extern "C" int sdp_rowscale_add(int dtype, const void* X, int64_t ldx, int x_grp
     const int gv = ew_grid((int64_t)M * (N / 8));
     if (dtype == 1)
       hipLaunchKernelGGL(rowscale_v8<bf16_t>, dim3(gv), dim3(256), 0, s, (const bf16_t*)X, ldx, xm, scale, sgrp,
-                         (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, M, N);
+                         (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, M, N, act);
     else if (dtype == 0)
       hipLaunchKernelGGL(rowscale_v8<float>, dim3(gv), dim3(256), 0, s, (const float*)X, ldx, xm, scale, sgrp,
-                         (const float*)R, ldr, rm, (float*)Y, ldy, ym, M, N);
+                         (const float*)R, ldr, rm, (float*)Y, ldy, ym, M, N, act);
     else
       return (int)hipErrorInvalidValue;
     return SDP_CHECK_LAUNCH();
@@ -664,13 +670,31 @@ extern "C" int sdp_rowscale_add(int dtype, const void* X, int64_t ldx, int x_grp
   const int g = ew_grid((int64_t)M * N);
   if (dtype == 1)
     hipLaunchKernelGGL(rowscale_k<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)X, ldx, xm, scale, sgrp,
-                       (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, M, N);
+                       (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, M, N, act);
   else if (dtype == 0)
     hipLaunchKernelGGL(rowscale_k<float>, dim3(g), dim3(256), 0, s, (const float*)X, ldx, xm, scale, sgrp,
-                       (const float*)R, ldr, rm, (float*)Y, ldy, ym, M, N);
+                       (const float*)R, ldr, rm, (float*)Y, ldy, ym, M, N, act);
   else
     return (int)hipErrorInvalidValue;
   return SDP_CHECK_LAUNCH();
+}
+
+extern "C" int sdp_rowscale_add(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                                const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp, int64_t r_gstride,
+                                int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int M, int N,
+                                void* stream) {
+  return rowscale_impl(dtype, ACT_NONE, X, ldx, x_grp, x_gstride, x_off, scale, sgrp, R, ldr, r_grp, r_gstride, r_off,
+                       Y, ldy, y_grp, y_gstride, y_off, M, N, stream);
+}
+
+// Y = act(X) * scale + R: activation, drop path and residual add of a ConvMixer branch in one
+// pass (the activation output itself is not needed by the backward).
+extern "C" int sdp_act_rowscale_add(int dtype, int act, const void* X, int64_t ldx, int x_grp, int64_t x_gstride,
+                                    int x_off, const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp,
+                                    int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride,
+                                    int y_off, int M, int N, void* stream) {
+  return rowscale_impl(dtype, act, X, ldx, x_grp, x_gstride, x_off, scale, sgrp, R, ldr, r_grp, r_gstride, r_off, Y,
+                       ldy, y_grp, y_gstride, y_off, M, N, stream);
 }
 
 // ---------------------------------------------------------------------------

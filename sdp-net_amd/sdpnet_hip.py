@@ -75,6 +75,8 @@ _SIGS = {
     "sdp_act_bwd": ([_i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _f32, _u64, _vp], _i32),
     "sdp_rowscale_add": ([_i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _i32, _i32,
                           _vp], _i32),
+    "sdp_act_rowscale_add": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _i32, _i32,
+                          _vp], _i32),
     "sdp_ln_apply": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_ln_bwd_blocks": ([_i32], _i32),
     "sdp_ln_fwd": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
@@ -515,11 +517,16 @@ def act_bwd(Z: torch.Tensor, DY: torch.Tensor, DZ: torch.Tensor, M: int, N: int,
 
 
 def rowscale_add(x: Rows, y: Rows, M: int, N: int, scale: Optional[torch.Tensor] = None, sgrp: int = 1,
-                 resid: Optional[Rows] = None):
+                 resid: Optional[Rows] = None, act: int = 0):
+    """y = act(x) * scale[m / sgrp] (+ resid) over row maps (act 0: sdp_rowscale_add)."""
     _need_cuda(x.t, y.t, scale)
     _req(scale is None or scale.dtype == torch.float32, "rowscale scale fp32")
-    rc = lib().sdp_rowscale_add(dcode(x.t.dtype), *x.args(), _ptr(scale), sgrp, *_rows_args(resid), *y.args(), M, N,
-                                _stream(y.t))
+    if act:
+        rc = lib().sdp_act_rowscale_add(dcode(x.t.dtype), int(act), *x.args(), _ptr(scale), sgrp, *_rows_args(resid),
+                                        *y.args(), M, N, _stream(y.t))
+    else:
+        rc = lib().sdp_rowscale_add(dcode(x.t.dtype), *x.args(), _ptr(scale), sgrp, *_rows_args(resid), *y.args(), M,
+                                    N, _stream(y.t))
     _check(rc, "rowscale_add")
 
 

@@ -219,19 +219,20 @@ class _MixerFn(torch.autograd.Function):
         d = _empty((M, C), dt, dev)
         sp.dwconv(_dense(a1), W_["dww"], W_["dwb"], _dense(d), B, H, W, C, k)
         z1 = _linear(d, W_["ccw"], W_["ccb"], dt)
-        h1 = _empty((M, C), dt, dev)
-        sp.act_fwd(z1, h1, M, C, act)
         mid = _with_regs(tok, B, R, N, C)
         imid = Rows(mid, C, P, N, R)
-        sp.rowscale_add(_dense(h1), imid, M, C, scale=dp2, sgrp=P, resid=img)
+        sp.rowscale_add(_dense(z1), imid, M, C, scale=dp2, sgrp=P, resid=img, act=act)   # act + drop path + residual
         # x = drop_path_1(PW_down(act(PW_up(LN2 x_)))) + x_
         a2, s2 = _ln_fwd(imid, M, C, W_["g2"], W_["b2"], m.layer_norm_2.eps, dt)
         z2 = _linear(a2, W_["upw"], W_["upb"], dt)
         h = _empty((M, 4 * C), dt, dev)
         sp.act_fwd(z2, h, M, 4 * C, act)
-        z3 = _linear(h, W_["dnw"], W_["dnb"], dt)
         out = _with_regs(mid, B, R, N, C)
-        sp.rowscale_add(_dense(z3), Rows(out, C, P, N, R), M, C, scale=dp1, sgrp=P, resid=imid)
+        if dp1 is None:  # residual add in the GEMM epilogue, straight into the token rows
+            sp.gemm(_dense(h), W_["dnw"], Rows(out, C, P, N, R), M, C, 4 * C, bias=W_["dnb"], resid=imid)
+        else:
+            z3 = _linear(h, W_["dnw"], W_["dnb"], dt)
+            sp.rowscale_add(_dense(z3), Rows(out, C, P, N, R), M, C, scale=dp1, sgrp=P, resid=imid)
         ctx.st = dict(tok=tok, mid=mid, a1=a1, s1=s1, d=d, z1=z1, a2=a2, s2=s2, z2=z2, h=h, W=W_, dp1=dp1, dp2=dp2,
                       geo=(B, R, H, W, C, k), act=act, dt=dt, has=[p is not None for p in params])
         ctx.shapes = [None if p is None else p.shape for p in params]

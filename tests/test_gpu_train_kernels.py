@@ -279,3 +279,23 @@ def test_head_layernorm_on_qkv_rows(dtype):
     xh = (k - k.mean(-1, keepdim=True)) / torch.sqrt(k.var(-1, unbiased=False, keepdim=True) + eps)
     close(dg, (dy[:, C:2 * C].float().reshape(T, H, hd) * xh).sum((0, 1)), tol * 10, "head ln dgamma")
     close(db, dy[:, C:2 * C].float().reshape(T, H, hd).sum((0, 1)), tol * 10, "head ln dbeta")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("act", [1, 2, 7])
+@pytest.mark.parametrize("C", [64, 36])   # 8-wide kernel / scalar kernel
+def test_act_rowscale_add_matches_two_passes(dtype, act, C):
+    """sdp_act_rowscale_add == sdp_act_fwd then sdp_rowscale_add, bit for bit (token row maps)."""
+    B, R, P = 3, 2, 49
+    N = R + P
+    z = rnd(B * P, C, seed=50, dtype=dtype)
+    tok = rnd(B * N, C, seed=51, dtype=dtype)
+    scale = torch.rand(B, generator=torch.Generator().manual_seed(52)).to(DEV) + 0.5
+    h = torch.empty_like(z)
+    sp.act_fwd(z, h, B * P, C, act)
+    ref = torch.zeros(B * N, C, dtype=dtype, device=DEV)
+    sp.rowscale_add(sp.dense(h), sp.Rows(ref, C, P, N, R), B * P, C, scale=scale, sgrp=P, resid=sp.Rows(tok, C, P, N, R))
+    got = torch.zeros_like(ref)
+    sp.rowscale_add(sp.dense(z), sp.Rows(got, C, P, N, R), B * P, C, scale=scale, sgrp=P,
+                    resid=sp.Rows(tok, C, P, N, R), act=act)
+    assert torch.equal(got, ref)
