@@ -130,14 +130,39 @@ __global__ void broadcast_rows_k(const TI* __restrict__ src, int64_t lds, int64_
   }
 }
 
+// Same-dtype copy, 16 B per work item (rows of 16-B multiples, 16-B aligned bases / strides).
+__global__ void copy_rows16_k(const uint4* __restrict__ src, int64_t lds, int64_t sgstride, uint4* __restrict__ dst,
+                              int64_t ldd, int64_t gstride, int B, int R, int C16) {
+  const int64_t total = (int64_t)B * R * C16;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(idx % C16);
+    const int64_t br = idx / C16;
+    const int r = (int)(br % R), b = (int)(br / R);
+    dst[b * gstride + (int64_t)r * ldd + c] = src[b * sgstride + (int64_t)r * lds + c];
+  }
+}
+
 // dst[b*gstride + r*ldd + c] = src[b*sgstride + r*lds + c]  (sgstride 0 = broadcast)
 extern "C" int sdp_copy_rows(int dtype_src, const void* src, int64_t lds, int64_t sgstride, int dtype_dst, void* dst,
                              int64_t ldd, int64_t gstride, int B, int R, int C, void* stream) {
   if (!src || !dst || B < 0 || R < 0 || C <= 0) return (int)hipErrorInvalidValue;
   const int64_t total = (int64_t)B * R * C;
   if (total == 0) return 0;
-  dim3 grid((unsigned)std::min<int64_t>((total + 255) / 256, 4096));
   hipStream_t s = (hipStream_t)stream;
+  if (dtype_src == dtype_dst && (dtype_src == 0 || dtype_src == 1)) {
+    const int64_t es = dtype_src == 1 ? 2 : 4, per = 16 / es;  // elements per 16 B
+    if (C % per == 0 && lds % per == 0 && ldd % per == 0 && sgstride % per == 0 && gstride % per == 0 &&
+        (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0) {
+      const int C16 = (int)(C / per);
+      const int64_t t16 = (int64_t)B * R * C16;
+      dim3 g16((unsigned)std::min<int64_t>((t16 + 255) / 256, 8192));
+      hipLaunchKernelGGL(copy_rows16_k, g16, dim3(256), 0, s, (const uint4*)src, lds / per, sgstride / per,
+                         (uint4*)dst, ldd / per, gstride / per, B, R, C16);
+      return SDP_CHECK_LAUNCH();
+    }
+  }
+  dim3 grid((unsigned)std::min<int64_t>((total + 255) / 256, 4096));
   if (dtype_src == 0 && dtype_dst == 1)
     hipLaunchKernelGGL((broadcast_rows_k<float, bf16_t>), grid, dim3(256), 0, s, (const float*)src, lds, sgstride, (bf16_t*)dst, ldd, gstride, B, R, C);
   else if (dtype_src == 0 && dtype_dst == 0)

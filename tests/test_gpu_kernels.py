@@ -309,8 +309,9 @@ def test_patchify(p, img, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
-def test_transposes_and_row_copies(dtype):
-    B, C, H, W, R = 3, 130, 7, 9, 4
+@pytest.mark.parametrize("C", [130, 128])   # scalar / 16-B row-copy kernels
+def test_transposes_and_row_copies(dtype, C):
+    B, H, W, R = 3, 7, 9, 4
     N = R + H * W
     x = rnd(B, C, H, W, dtype=dtype, seed=51)
     tok = torch.zeros(B * N, C, dtype=dtype, device=DEV)
