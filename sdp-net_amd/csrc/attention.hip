@@ -777,7 +777,7 @@ SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8
 // Needs hd % 32 == 0 (whole 4-chunk swizzle groups).
 // ---------------------------------------------------------------------------
 template <int HDT>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDT <= 3 ? 4 : 2))) void attn_fa2_bf16(
+__global__ __launch_bounds__(576) __attribute__((amdgpu_waves_per_eu(HDT <= 3 ? 4 : 2))) void attn_fa2_bf16(
     const bf16_t* __restrict__ QKV, int64_t ldq, bf16_t* __restrict__ O, int64_t ldo, int B, int N, int H,
     const float* __restrict__ gq, const float* __restrict__ bq, const float* __restrict__ gk,
     const float* __restrict__ bk, float eps, float scale_log2) {
@@ -879,8 +879,10 @@ static int launch_attn_fa2(const void* QKV, int64_t ldq, void* O, int64_t ldo, i
                                        (int)bytes);
     if (e != hipSuccess) return (int)e;
   }
+  // one query tile per wave up to 9 tiles (N <= 288: XL's 260 tokens are 8 full tiles + 4 rows;
+  // with 8 waves one wave did two tiles and set the block's time), else 8 waves looping
   int waves = (N + 31) / 32;
-  if (waves > 8) waves = 8;
+  if (waves > 9) waves = 8;
   hipLaunchKernelGGL(attn_fa2_bf16<HDT>, dim3(B * H), dim3(64 * waves), bytes, s, (const bf16_t*)QKV, ldq,
                      (bf16_t*)O, ldo, B, N, H, gq, bq, gk, bk, eps, scale * 1.4426950408889634f);
   return SDP_CHECK_LAUNCH();
