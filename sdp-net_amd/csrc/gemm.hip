@@ -701,6 +701,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                                        (AS3 void*)(buf + lds_op + ((wave & 1) * 16 + s) * 1024), 16, 0, 0);
   };
 
+  auto dma_piece = [&](int kt, char* buf, int s) {
+    __builtin_amdgcn_global_load_lds((const AS1 void*)(gbase + (int64_t)kt * (BK * 2) + voff[s]),
+                                     (AS3 void*)(buf + lds_op + ((wave & 1) * 16 + s) * 1024), 16, 0, 0);
+  };
   f32x4 acc[8][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -758,30 +762,27 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
     }
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr (MORE1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // builtin (not inline-asm) waits, so the compiler's counter model sees them
+    __builtin_amdgcn_s_waitcnt(MORE1 ? 0x0070 : 0xC07F);  // lgkmcnt(0) [+ vmcnt(0)]
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    // half 1: 64 MFMA on ks1 || 16 ds_read of ks0 of t+1 || 16 LDS-DMA pieces of t+2
-    if constexpr (MORE1) rd(nxt, 0, xa, wa);
-    if constexpr (MORE2) dma_tile(t + 2, cur);
-    mm(xb, wb);
-    if constexpr (MORE1 && MORE2) {
+    // half 1: 64 MFMA on ks1 || 16 ds_read of ks0 of t+1 || 16 LDS-DMA pieces of t+2,
+    // pinned in 16 chunks of {1 read, 1 DMA, 4 MFMA} (the scheduler otherwise clusters
+    // every read and DMA ahead of the MFMAs)
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);  // DS read
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);  // VMEM (LDS-DMA)
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);  // MFMA
+    for (int g = 0; g < 16; ++g) {
+      if constexpr (MORE1) {
+        if (g < 8) wa[g] = lds_frag(nxt + TILE_BYTES, wn * 128 + g * 16 + fr, fq);
+        else xa[g - 8] = lds_frag(nxt, wm * 128 + (g - 8) * 16 + fr, fq);
       }
-    } else if constexpr (MORE1) {
+      if constexpr (MORE2) dma_piece(t + 2, cur, g);
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
+      for (int e = 0; e < 4; ++e) {
+        const int q = 4 * g + e, i = q >> 3, j = q & 7;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[i], xb[j], acc[i][j], 0, 0, 0);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_sched_barrier(0);
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
