@@ -28,7 +28,6 @@
 // accumulator holds D[n][m] with 4 consecutive n per lane: every epilogue
 // access (bias, residual, output) is an 8/16-byte vector per lane.
 #include "common.h"
-#include <type_traits>
 
 
 template <typename T>
@@ -621,185 +620,6 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
 }
 
-// ---------------------------------------------------------------------------
-// 4-wave kernel (id 20): the same 256x256x64 tile and LDS image, but one wave per
-// SIMD owning a 128(m) x 128(n) quadrant (acc[8][8] = 256 accumulator registers in
-// the AGPR half of the 512-entry file), so a K-tile costs each wave 128 MFMAs
-// against 32 ds_read_b128 (the 8-wave kernel: 64 against 24, 1.5x the LDS reads
-// per FLOP) and ONE barrier instead of eight.
-//
-// K-tile t is consumed in two halves (ks = 0, 1: K 0-31 / 32-63), fragments
-// double-buffered in registers:
-//   half 0: MFMA(ks0 of t)  ||  ds_read ks1 of t
-//           lgkmcnt(0); vmcnt(0) [DMA of t+1 landed]; s_barrier
-//   half 1: MFMA(ks1 of t)  ||  ds_read ks0 of t+1; LDS-DMA of t+2 into t's buffer
-// The barrier proves every wave has read all of buffer t (so t+2 may overwrite
-// it) and that every wave's DMA pieces of t+1 have landed; the DMA of t+2 has one
-// full K-tile of MFMA time to arrive.  Operand pieces: 64 per K-tile (32 X, 32 W,
-// 8 rows x 128 B), 16 per wave, addressed by 32-bit per-lane offsets from a
-// uniform base (host checks the operands' extents).
-// ---------------------------------------------------------------------------
-namespace w4 {
-constexpr int NT = 256;
-constexpr int BUF = 2 * TILE_BYTES;  // X + W image of one K-tile
-
-template <int ACT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_bf16_4w(
-    const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap, const bf16_t* __restrict__ W, int64_t ldw,
-    Epi<bf16_t> epi, int M, int N, int K, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
-  const int nwg = tiles_m * tiles_n;
-  const int b = blockIdx.x;
-  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
-  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
-  int tm, tn;
-  if (epi.group_m > 1) {
-    const int gsz_full = epi.group_m * tiles_n;
-    const int g = wgid / gsz_full, r = wgid - g * gsz_full;
-    const int first = g * epi.group_m;
-    const int gm = min(tiles_m - first, epi.group_m);
-    tm = first + r % gm;
-    tn = r / gm;
-  } else {
-    tm = wgid / tiles_n;
-    tn = wgid % tiles_n;
-  }
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int nk = K / BK;
-
-  // pieces of wave w: 16w .. 16w+15 (0-31: X rows 8p.., 32-63: W rows 8(p-32)..)
-  const bool isx = wave < 2;
-  const char* gbase = isx ? (const char*)X : (const char*)W;
-  uint32_t voff[16];
-  {
-    const int rr = lane >> 3, pc = lane & 7;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int piece = (wave & 1) * 16 + s;  // within the operand
-      const int r = piece * 8 + rr;
-      const int c = swz(r, pc);
-      int64_t off;
-      if (isx) {
-        const int g = min(m0 + r, M - 1);
-        off = (xmap(g) * ldx + c * 8) * 2;
-      } else {
-        const int g = min(n0 + r, N - 1);
-        off = ((int64_t)g * ldw + c * 8) * 2;
-      }
-      voff[s] = (uint32_t)off;
-    }
-  }
-  const int lds_op = isx ? 0 : TILE_BYTES;
-  auto dma_tile = [&](int kt, char* buf) {
-    const char* gk = gbase + (int64_t)kt * (BK * 2);
-#pragma unroll
-    for (int s = 0; s < 16; ++s)
-      __builtin_amdgcn_global_load_lds((const AS1 void*)(gk + voff[s]),
-                                       (AS3 void*)(buf + lds_op + ((wave & 1) * 16 + s) * 1024), 16, 0, 0);
-  };
-
-  auto dma_piece = [&](int kt, char* buf, int s) {
-    __builtin_amdgcn_global_load_lds((const AS1 void*)(gbase + (int64_t)kt * (BK * 2) + voff[s]),
-                                     (AS3 void*)(buf + lds_op + ((wave & 1) * 16 + s) * 1024), 16, 0, 0);
-  };
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8 xa[8], wa[8], xb[8], wb[8];
-  auto rd = [&](const char* buf, int ks, bf16x8(&xf)[8], bf16x8(&wf)[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      wf[j] = lds_frag(buf + TILE_BYTES, wn * 128 + j * 16 + fr, ks * 4 + fq);
-      xf[j] = lds_frag(buf, wm * 128 + j * 16 + fr, ks * 4 + fq);
-    }
-#ifdef PIN_V
-#pragma unroll
-    for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(xf[j]), "+v"(wf[j]));
-#endif
-  };
-  auto mm = [&](const bf16x8(&xf)[8], const bf16x8(&wf)[8]) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
-#ifdef PIN_A
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-#endif
-  };
-
-  dma_tile(0, smem);
-  if (nk > 1) {
-    dma_tile(1, smem + BUF);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  rd(smem, 0, xa, wa);
-
-  // one K-tile; MORE1: tile t+1 exists, MORE2: tile t+2 exists (compile-time, so each
-  // half is one straight-line scheduling region)
-  auto ktile = [&](int t, auto more1_c, auto more2_c) {
-    constexpr bool MORE1 = decltype(more1_c)::value, MORE2 = decltype(more2_c)::value;
-    char* cur = smem + (t & 1) * BUF;
-    char* nxt = smem + ((t + 1) & 1) * BUF;
-    // half 0: 64 MFMA on ks0 || 16 ds_read of ks1
-    rd(cur, 1, xb, wb);
-    mm(xa, wa);
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // builtin (not inline-asm) waits, so the compiler's counter model sees them
-    __builtin_amdgcn_s_waitcnt(MORE1 ? 0x0070 : 0xC07F);  // lgkmcnt(0) [+ vmcnt(0)]
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    // half 1: 64 MFMA on ks1 || 16 ds_read of ks0 of t+1 || 16 LDS-DMA pieces of t+2,
-    // pinned in 16 chunks of {1 read, 1 DMA, 4 MFMA} (the scheduler otherwise clusters
-    // every read and DMA ahead of the MFMAs)
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      if constexpr (MORE1) {
-        if (g < 8) wa[g] = lds_frag(nxt + TILE_BYTES, wn * 128 + g * 16 + fr, fq);
-        else xa[g - 8] = lds_frag(nxt, wm * 128 + (g - 8) * 16 + fr, fq);
-      }
-      if constexpr (MORE2) dma_piece(t + 2, cur, g);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int q = 4 * g + e, i = q >> 3, j = q & 7;
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[i], xb[j], acc[i][j], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  int t = 0;
-  for (; t + 2 < nk; ++t) ktile(t, T_{}, T_{});
-  if (t + 1 < nk) ktile(t++, T_{}, F_{});
-  ktile(t, F_{}, F_{});
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // every wave done with the K buffers: they become epilogue slots
-  char* stg = smem + wave * 16384;
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-    tile_epilogue_rows<ACT, 4, true>(epi, *reinterpret_cast<f32x4(*)[4][8]>(&acc[4 * h][0]), m0, n0, M, N, wm,
-                                     2 * wn + h, lane, fr, fq, stg);
-}
-}  // namespace w4
-
 #undef SDP_VMCNT
 
 }  // namespace fast
@@ -913,7 +733,7 @@ extern "C" int sdp_gemm_force_generic(int on) {
 static int g_fast_kernel = 14;
 extern "C" int sdp_gemm_set_fast_kernel(int k) {
   int old = g_fast_kernel;
-  if (k == 9 || k == 14 || k == 20) g_fast_kernel = k;
+  if (k == 9 || k == 14) g_fast_kernel = k;
   return old;
 }
 
@@ -1001,14 +821,8 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
       // and implements resid_pre only without an activation
       const bool rows_ok = (N % 8 == 0) && (ldy % 8 == 0) && ((uintptr_t)Y % 16 == 0) &&
                            (!R || ((ldr % 8 == 0) && ((uintptr_t)R % 16 == 0))) && !(R && resid_pre && act != ACT_NONE);
-      int fk = rows_ok ? g_fast_kernel : 9;
-      if (fk == 20) {  // 32-bit per-lane operand offsets: both extents must stay below 4 GiB
-        const int64_t lm = M - 1;
-        const int64_t xlast = (lm / xm.grp) * xm.gstride + xm.off + lm % xm.grp;
-        const int64_t xbytes = (xlast * ldx + K) * 2, wbytes = ((int64_t)(N - 1) * ldw + K) * 2;
-        if (xbytes >= (int64_t(1) << 32) || wbytes >= (int64_t(1) << 32)) fk = 14;
-      }
-      if ((fk == 14 || fk == 20) && part && N % 64 == 0) {  // the whole-line epilogue emits the row partial statistics
+      const int fk = rows_ok ? g_fast_kernel : 9;
+      if (fk == 14 && part && N % 64 == 0) {  // the whole-line epilogue emits the row partial statistics
         e.part = part;
         if (part_done) *part_done = true;
       }
@@ -1016,14 +830,7 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
                                          (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
       // exact-erf GELU goes through the runtime-activation epilogue (apply_act)
       const int ak = (act == ACT_GELU && g_exact_gelu) ? -1 : act;
-#define SDP_4W(A) hipLaunchKernelGGL((fast::w4::gemm_bf16_4w<A>), dim3(tm * tn), dim3(fast::w4::NT), 0, s, \
-                                   (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
-      if (fk == 20) {
-        if (ak == ACT_NONE) SDP_4W(ACT_NONE);
-        else if (ak == ACT_GELU) SDP_4W(ACT_GELU);
-        else if (ak == ACT_TANH) SDP_4W(ACT_TANH);
-        else SDP_4W(-1);
-      } else if (fk == 14) {
+      if (fk == 14) {
         if (ak == ACT_NONE) SDP_8PH(ACT_NONE, 4);
         else if (ak == ACT_GELU) SDP_8PH(ACT_GELU, 4);
         else if (ak == ACT_TANH) SDP_8PH(ACT_TANH, 4);
@@ -1035,7 +842,6 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
         else SDP_8PH(-1, 1);
       }
 #undef SDP_8PH
-#undef SDP_4W
     } else {
       dim3 grid((M + gen::BM - 1) / gen::BM, (N + gen::BN - 1) / gen::BN);
       hipLaunchKernelGGL(gen::gemm_generic<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)X, ldx, xm,
