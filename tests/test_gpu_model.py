@@ -87,6 +87,24 @@ def test_batch_invariance_full_size_bf16():
         assert torch.equal(y2[0], y[i]), f"image {i}: batch-dependent result"
 
 
+def test_config4_eight_rank_shards_equal_global_batch():
+    """BASELINE configs[3] (M, global batch 2048 over 8 GPUs): the shard each of the 8 ranks
+    runs (sharding.shard_bounds, as bench.py assigns them) gives bit for bit the rows of the
+    whole 2048-image forward, so the 8-rank job computes exactly the global batch."""
+    import model as ours
+    import sharding
+    torch.manual_seed(231424314)
+    m = ours.MainModel(**synth.canonical("M")).to(DEV).eval().to(torch.bfloat16)
+    g = torch.Generator(device="cpu").manual_seed(2048)
+    x = torch.randn(2048, 3, 224, 224, generator=g).to(DEV).to(torch.bfloat16)
+    y = m(x)
+    assert y.shape == (2048, 1000) and torch.isfinite(y.float()).all()
+    for r in range(8):
+        lo, hi = sharding.shard_bounds(2048, 8, r)
+        assert hi - lo == 256
+        assert torch.equal(m(x[lo:hi]), y[lo:hi]), f"rank {r} shard differs from the global batch"
+
+
 def test_xl_full_batch_runs_finite():
     """XL at the BASELINE configs[2] batch (512): finite, and batch-invariant bit for bit."""
     import model as ours
