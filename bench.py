@@ -411,7 +411,7 @@ def main():
         "roofline": {"bound": "mfma", "kernel": kname,
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
-                     "traffic_unit": "bytes per launch (HBM-side, PMC)", "traffic_source": traffic_src,
+                     "traffic_unit": "bytes per launch, L2-to-fabric (PMC 2*FETCH_SIZE+WRITE_SIZE; Infinity Cache hits included)", "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": int(fast_by / max(1, fast_n)),
                      "launches_per_step": fast_n // max(1, args.prof_steps),
                      "avg_launch_us": round(1e3 * fast_ms / max(1, fast_n), 2),
