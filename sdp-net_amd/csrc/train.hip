@@ -146,8 +146,20 @@ __global__ __launch_bounds__(NT) void gemm_flex_bf16(Op A, Op B, Op Cc, int Mi, 
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wi = wave >> 1, wj = wave & 1;
-  const int i0 = blockIdx.y * BI, j0 = blockIdx.x * BJ;
-  const int z = blockIdx.z / splits, sk = blockIdx.z % splits;
+  // XCD-contiguous tile order (consecutive block ids go to different XCDs): the tiles one XCD
+  // runs together share their column blocks in its L2 (XL training step +1 %)
+  int bx, by, bz;
+  {
+    const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy * gridDim.z;
+    const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+    const int w = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+    bx = w % gx;
+    by = (w / gx) % gy;
+    bz = w / (gx * gy);
+  }
+  const int i0 = by * BI, j0 = bx * BJ;
+  const int z = bz / splits, sk = bz % splits;
   const int kb = sk * kchunk, ke = min(K, kb + kchunk);
   const bf16_t* Ap = (const bf16_t*)A.p + zoff(A, z, zdiv);
   const bf16_t* Bp = (const bf16_t*)B.p + zoff(B, z, zdiv);
