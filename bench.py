@@ -202,15 +202,14 @@ def train_bench(args, C, world, rank, local):
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     x = torch.randn(B, 3, 224, 224, generator=g).to(dev)
     y = torch.randint(0, cfg["output_classes"], (B,), generator=g).to(dev)
-    scale = 65536.0
 
     def step():
         opt.zero_grad(set_to_none=True)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = net(x)
             loss = sdpnet_train.cross_entropy(out, y, 0.1)
-        (loss * scale).backward()
-        opt.step(grad_scale=scale, max_norm=5.0)
+        opt.scale(loss).backward()              # GradScaler.scale on the device scale (no sync)
+        opt.step(grad_scale=None, max_norm=5.0)  # unscale / inf check / clip / AdamW / scale update
         return loss
 
     for _ in range(max(1, args.warmup)):
@@ -219,6 +218,7 @@ def train_bench(args, C, world, rank, local):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    taken0 = float(opt._steps[0])
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -228,6 +228,9 @@ def train_bench(args, C, world, rank, local):
     el = sharding.max_over_ranks(time.perf_counter() - t0, device=dev)
     total = int(sharding.sum_over_ranks(B * args.steps, device=dev))
     assert torch.isfinite(loss).all()
+    # GradScaler skips (inf/nan grads) did no optimizer work: count them, none expected
+    skipped = int(args.steps - (float(opt._steps[0]) - taken0))
+    assert skipped == 0, f"{skipped} optimizer steps skipped by the GradScaler inside the timed region"
     gf = 3 * flops_per_image(cfg) / 1e9   # forward + dX + dW GEMMs (3x forward)
     value = total / el
     out = {
@@ -239,6 +242,7 @@ def train_bench(args, C, world, rank, local):
                    "parallelism": f"dp{world}" + (" DDP bucketed grad all-reduce over RCCL" if world > 1 else "")},
         "model_flops_per_image_gf": round(gf, 3),
         "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
+        "skipped_steps": skipped, "grad_scale": float(opt.scaler[0]),
         "loss": round(float(loss.detach()), 4), "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
     }
     if rank == 0:
@@ -251,14 +255,14 @@ def train_bench(args, C, world, rank, local):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="m",
                     help="m = the BASELINE metric's workload (default); xl = configs[2]")
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = the config's: M 256, XL 512)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--prof-steps", type=int, default=2)
+    ap.add_argument("--prof-steps", type=int, default=1)
     ap.add_argument("--streams", type=int, default=0, help="sub-batch streams per GPU (0 = model default)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of the launch + timing path")
     args = ap.parse_args()
@@ -346,27 +350,55 @@ def main():
     assert torch.isfinite(y.float()).all()
 
     # ---- dominant-kernel roofline: HIP events around every GEMM launch -------------
+    # Same model, same sub-batch streams as the timed graph (events cannot be recorded inside
+    # a replayed graph, so this pass launches eagerly).  Each GEMM is bracketed by events on
+    # its own launch stream; their offsets from one reference event give the launch
+    # intervals, whose UNION per step is the wall time the GEMMs occupy in this schedule
+    # (two streams may overlap GEMMs with each other or with other kernels).
     rec = {}
 
     def timer(name, key, flops, nbytes, e0, e1):
         rec.setdefault(key, []).append((flops, nbytes, e0, e1))
 
     old = sp.set_launch_timer(timer)
-    ns_saved = getattr(m, "num_streams", None)
-    m.num_streams = 1  # per-launch events must not include the other stream's overlap
+    basis = "graph"
     try:
+        # a second graph of the same step with external timing-event nodes around every GEMM,
+        # replayed like the timed one (the timed graph itself stays free of event nodes)
+        ref_ev = torch.cuda.Event(enable_timing=True, external=True)
+        pg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(pg):
+            ref_ev.record()
+            for _ in range(max(1, args.prof_steps)):
+                step()
+        rec.clear()  # keep only the events of the captured launches
+        pg.replay()  # warm replay: events are re-recorded on every replay
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        for _ in range(3):
+            pg.replay()
+        torch.cuda.synchronize()
+        prof_step_ms = 1e3 * (time.perf_counter() - tp) / 3 / max(1, args.prof_steps)
+        ref_ev.elapsed_time(next(iter(rec.values()))[0][2])  # probe: raises if unsupported
+    except Exception as exc:  # noqa: BLE001 -- fall back to an eager pass
+        basis = f"eager ({type(exc).__name__} on graph events)"
+        rec.clear()
+        ref_ev = torch.cuda.Event(enable_timing=True)
+        end_ev = torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(int(2.4e8 * max(1, args.prof_steps)))
+        ref_ev.record()
         for _ in range(max(1, args.prof_steps)):
             step()
+        end_ev.record()
+        torch.cuda.synchronize()
+        prof_step_ms = ref_ev.elapsed_time(end_ev) / max(1, args.prof_steps)
     finally:
         sp.set_launch_timer(old)
-        if ns_saved is None:
-            del m.num_streams
-        else:
-            m.num_streams = ns_saved
     torch.cuda.synchronize()
     fast_fl = fast_ms = fast_by = 0.0
     fast_n = 0
     per_shape = {}
+    intervals = []
     for key, lst in rec.items():
         ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in lst)
         fl = sum(f for f, _, _, _ in lst)
@@ -379,13 +411,32 @@ def main():
             fast_ms += ms
             fast_by += by
             fast_n += len(lst)
-    achieved = fast_fl / (fast_ms * 1e-3) / 1e12 if fast_ms else 0.0
+            intervals += [(ref_ev.elapsed_time(e0), ref_ev.elapsed_time(e1)) for _, _, e0, e1 in lst]
+    intervals.sort()
+    union_ms, cur = 0.0, None
+    for a, b_ in intervals:
+        if cur is None or a > cur[1]:
+            if cur is not None:
+                union_ms += cur[1] - cur[0]
+            cur = [a, b_]
+        else:
+            cur[1] = max(cur[1], b_)
+    if cur is not None:
+        union_ms += cur[1] - cur[0]
+    union_ms_step = union_ms / max(1, args.prof_steps)
+    # achieved = the GEMMs' FLOPs per step / the wall time they occupy per step
+    achieved = fast_fl / max(1, args.prof_steps) / (union_ms_step * 1e-3) / 1e12 if union_ms_step else 0.0
+    per_launch_tf = fast_fl / (fast_ms * 1e-3) / 1e12 if fast_ms else 0.0
     kname = FAST_GEMM_NAMES.get(sp.lib().sdp_gemm_set_fast_kernel(0), "?")
     traffic, traffic_src = measured_traffic(kname) if args.config == "m" else (None, None)
 
     gf = flops_per_image(cfg) / 1e9
     tokens = (224 // cfg["patch_size"]) ** 2 + min(4, cfg["max_num_registers"])
     value = total_imgs / el
+    ms_step = 1e3 * el / args.steps
+    # the GEMM time quoted must fit in the step it was measured in (the event nodes themselves
+    # add a few us per launch over the timed graph, reported as prof_step_ms)
+    assert union_ms_step <= prof_step_ms * 1.001, (union_ms_step, prof_step_ms)
     out = {
         "metric": C["metric"],
         "value": round(value, 2),
@@ -410,6 +461,12 @@ def main():
         "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
         "roofline": {"bound": "mfma", "kernel": kname,
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "achieved_basis": "GEMM FLOPs per step / union of the GEMM launch intervals per step (HIP "
+                                       "events on each launch stream, same sub-batch streams as the timed graph; "
+                                       f"measured in a {basis}-replayed step)",
+                     "gemm_union_ms_per_step": round(union_ms_step, 3),
+                     "events_step_ms": round(prof_step_ms, 3),
+                     "per_launch_tflops": round(per_launch_tf, 1),
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
                      "traffic_unit": "bytes per launch, L2-to-fabric (PMC 2*FETCH_SIZE+WRITE_SIZE; Infinity Cache hits included)", "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": int(fast_by / max(1, fast_n)),

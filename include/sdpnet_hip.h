@@ -97,6 +97,29 @@ int sdp_gemm_set_group_m(int gm);
 int sdp_gemm_set_exact_gelu(int on);
 
 /*
+ * Stream-K schedule of the bf16 fast GEMM.  When a shape's 256x256 tile count T is at
+ * least the CU count G and not a multiple of it, one persistent workgroup per CU takes
+ * an equal contiguous share of the T * K/64 k-iterations; a tile split between two
+ * workgroups is finished by the later one starting from the earlier one's fp32
+ * accumulators, so every output is bit-identical to the data-parallel tile schedule.
+ * The split needs caller-owned scratch per stream:
+ *   sdp_gemm_workspace_bytes()   bytes needed (8 KiB + G x 256 KiB);
+ *   sdp_gemm_set_workspace(stream, ws, bytes)  register ZERO-FILLED device memory (256-B
+ *       aligned) for GEMMs launched on `stream` (ws = NULL unregisters).  The library keeps
+ *       it zero between launches; streams without one use the data-parallel schedule.
+ *   sdp_gemm_set_schedule(mode)  1 = stream-K where it applies (default), 0 = never.
+ *   sdp_gemm_sk_applies(M, N, K) 1 if such a launch takes stream-K (given a workspace).
+ *   sdp_gemm_sk_status(stream, &n) synchronous: bounded-wait give-ups recorded on the
+ *       stream's workspace (0 unless a split tile's producer never published).
+ * Replaces nothing in the reference by itself: it schedules the GEMMs of sdp_gemm.
+ */
+int64_t sdp_gemm_workspace_bytes(void);
+int sdp_gemm_set_workspace(void* stream, void* ws, int64_t bytes);
+int sdp_gemm_set_schedule(int mode);
+int sdp_gemm_sk_applies(int M, int N, int K);
+int sdp_gemm_sk_status(void* stream, unsigned* n);
+
+/*
  * LayerNorm statistics by parts: sdp_row_partials writes {mean, M2} of every
  * 64-column chunk of the logical rows of X to part[(phys_row * ceil(C/64) + c) * 2];
  * sdp_ln_stats combines a row's chunks exactly (pairwise mean / M2 update) into
@@ -356,6 +379,14 @@ int sdp_ce_loss(int dtype, const void* logits, int64_t ldl, const int64_t* label
  *     max_norm / (sqrt(state[0]) * inv_scale + 1e-6)) (clip_grad_norm_, max_norm <= 0: off),
  *     then torch.optim.AdamW (decoupled decay, bias corrections of step);
  *   sdp_scaler_update: GradScaler.update on sc[0] = scale, sc[1] = growth tracker, resets state.
+ *   sdp_adamw_dev: sdp_adamw with the step counts on the device: steps[t] (fp32) = optimizer
+ *     steps tensor t has taken; the bias corrections use steps[t] + 1 (double precision).
+ *     scale != NULL: the grads are unscaled by 1 / scale[0] (device GradScaler scale; the loss
+ *     is multiplied by the same device value, so a backoff needs no host sync).
+ *   sdp_adamw_finish: if the step was taken (state[1] == 0) steps[0..nsteps) += 1; with
+ *     scale_tracker != NULL the GradScaler update as sdp_scaler_update; always resets state.
+ *     Together: torch.amp.GradScaler + torch.optim.AdamW semantics, where a skipped step
+ *     advances neither the parameters, the moments nor the step count.
  * (training_tools.py:91-99, :235.) */
 int sdp_mt_block_bytes(void);
 int sdp_grad_sumsq(float* const* grads, const int64_t* sizes, const void* blocks, int nblocks, float* state,
@@ -364,6 +395,12 @@ int sdp_adamw(float* const* params, float* const* grads, float* const* exp_avg, 
               const int64_t* sizes, const void* blocks, int nblocks, const float* state, float lr, float beta1,
               float beta2, float eps, float weight_decay, int step, float inv_scale, float max_norm, void* stream);
 int sdp_scaler_update(float* state, float* scale_tracker, float growth, float backoff, int interval, void* stream);
+int sdp_adamw_dev(float* const* params, float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                  const int64_t* sizes, const void* blocks, int nblocks, const float* state, float lr, float beta1,
+                  float beta2, float eps, float weight_decay, const float* steps, const float* scale,
+                  float inv_scale, float max_norm, void* stream);
+int sdp_adamw_finish(float* state, float* scale_tracker, float growth, float backoff, int interval, float* steps,
+                     int nsteps, void* stream);
 
 #ifdef __cplusplus
 }

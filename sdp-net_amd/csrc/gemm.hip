@@ -28,6 +28,7 @@
 // accumulator holds D[n][m] with 4 consecutive n per lane: every epilogue
 // access (bias, residual, output) is an 8/16-byte vector per lane.
 #include "common.h"
+#include <mutex>
 
 
 template <typename T>
@@ -298,6 +299,25 @@ SDP_DEV void tile_epilogue16(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0,
 // (v = bf16(act(acc + b)) + R, rounded again), i.e. resid_pre = 0 semantics; the
 // caller routes resid_pre with an activation elsewhere.  Same-wave LDS accesses
 // execute in order, so the slot needs no barrier.
+// Physical rows of a lane's logical rows m, m + 8, m + 16, ... through a RowMap without a
+// division per row: (g, r) = divmod(m, grp) once, then r += 8 with a carry into g.
+struct RowWalk {
+  int g, r, grp, off;
+  int64_t gstride;
+  SDP_DEV RowWalk(const RowMap& rm, int m) : grp(rm.grp), off(rm.off), gstride(rm.gstride) {
+    g = (int)((unsigned)m / (unsigned)rm.grp);
+    r = m - g * rm.grp;
+  }
+  SDP_DEV int64_t phys() const { return (int64_t)g * gstride + off + r; }
+  SDP_DEV void step8() {
+    r += 8;
+    while (r >= grp) {  // one pass unless grp < 8
+      r -= grp;
+      ++g;
+    }
+  }
+};
+
 template <int ACT, int JB = 4, bool ALL = false>
 SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int M, int N, int wm,
                                 int wn, int lane, int fr, int fq, char* stg) {
@@ -327,6 +347,8 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
   const bool col_ok = col < N;
   const int lcol = col_ok ? col : N - 8;
   const int wchunk0 = ((fq & 1) << 1) | (fq >> 1);  // 16-B chunk of pair 0 (pair 1: +4)
+  // the lane's 16 drain rows are mb + 8 i, i = 2 j + q
+  const int mb = m0 + wm * 128 + rlo;
   // stage(j): row group j through the permlane pairing, bias / LN fold / activation, bf16
   // pack, into its LDS slot; drain(j, rr): read the slot back in whole-line order, add the
   // residual, store, emit the row partials.  ALL: every row group gets its own 2 KiB
@@ -375,6 +397,8 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
       *(bf16x8*)(sl + fr * 128 + (((4 * p + wchunk0) ^ (fr & 7)) << 4)) = o;
     }
   };
+  RowWalk ow(epi.cmap, mb);
+  const int64_t part_col = (n0 + wn * 64) >> 6;
   auto drain = [&](int j, const bf16x8(&rr)[2]) {
     const char* sl = slot(j);
 #pragma unroll
@@ -385,9 +409,11 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(bf2f((bf16_t)o[e]) + bf2f((bf16_t)rr[q][e]));
       }
-      const int m = m0 + wm * 128 + j * 16 + r;
+      const int m = mb + j * 16 + 8 * q;
+      const int64_t prow = ow.phys();
+      ow.step8();
       if (m < M && col_ok) {
-        bf16x8* dst = (bf16x8*)(epi.out + epi.cmap(m) * epi.ldc + col);
+        bf16x8* dst = (bf16x8*)(epi.out + (uint64_t)prow * (uint32_t)epi.ldc + col);
         if (epi.nt_store) __builtin_nontemporal_store(o, dst);
         else *dst = o;
       }
@@ -409,30 +435,49 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
         m2 += __shfl_xor(m2, 2, 64);
         m2 += __shfl_xor(m2, 4, 64);
         if (ch == 0 && m < M && col_ok)
-          *(float2*)(epi.part + (epi.cmap(m) * (N >> 6) + ((n0 + wn * 64) >> 6)) * 2) = float2{mean, m2};
+          *(float2*)(epi.part + (prow * (N >> 6) + part_col) * 2) = float2{mean, m2};
       }
     }
   };
-  if constexpr (ALL) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) stage(j);
+  // residual rows: loads for every row group issued before any staging (ALL), so their
+  // latency runs under the staging arithmetic; rows past M re-read the last valid row
+  bf16x8 rres[ALL ? 8 : JB][2];
+  RowWalk rw(epi.rmap, mb);
+  int64_t rlast = 0;
+  if (epi.resid) {
+    const RowWalk rl(epi.rmap, M - 1);
+    rlast = rl.phys();
   }
+  auto load_res = [&](int jj, int j) {
 #pragma unroll
-  for (int j0 = 0; j0 < 8; j0 += JB) {
-    bf16x8 rres[JB][2];
+    for (int q = 0; q < 2; ++q) {
+      const int m = mb + j * 16 + 8 * q;
+      const int64_t prow = m < M ? rw.phys() : rlast;
+      rw.step8();
+      rres[jj][q] = *(const bf16x8*)(epi.resid + (uint64_t)prow * (uint32_t)epi.ldr + lcol);
+    }
+  };
+  if constexpr (ALL) {
     if (epi.resid) {
 #pragma unroll
-      for (int jj = 0; jj < JB; ++jj)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int m = min(m0 + wm * 128 + (j0 + jj) * 16 + rlo + 8 * q, M - 1);
-          rres[jj][q] = *(const bf16x8*)(epi.resid + epi.rmap(m) * epi.ldr + lcol);
-        }
+      for (int j = 0; j < 8; ++j) load_res(j, j);
     }
 #pragma unroll
-    for (int jj = 0; jj < JB; ++jj) {
-      if constexpr (!ALL) stage(j0 + jj);
-      drain(j0 + jj, rres[jj]);
+    for (int j = 0; j < 8; ++j) stage(j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) drain(j, rres[j]);
+  } else {
+#pragma unroll
+    for (int j0 = 0; j0 < 8; j0 += JB) {
+      if (epi.resid) {
+#pragma unroll
+        for (int jj = 0; jj < JB; ++jj) load_res(jj, j0 + jj);
+      }
+#pragma unroll
+      for (int jj = 0; jj < JB; ++jj) {
+        stage(j0 + jj);
+        drain(j0 + jj, rres[jj]);
+      }
     }
   }
 }
@@ -466,37 +511,148 @@ constexpr int BUF8 = 2 * TILE_BYTES;
 
 #define SDP_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
-// EPI: 1 = production epilogue, 2 = timing probe (stores only if a sentinel value
-// appears, i.e. never: measures main loop + prologue alone).
-template <int ACT, int EPI = 1>
-__global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
-                                                         const bf16_t* __restrict__ W, int64_t ldw, Epi<bf16_t> epi,
-                                                         int M, int N, int K, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF8];
-  const int nwg = tiles_m * tiles_n;
-  const int b = blockIdx.x;
-  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
-  const int wgid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
-  // grouped raster (epi.group_m > 1): wgids run down a group of group_m M-blocks before
-  // moving to the next N-tile, so the 32 concurrent tiles of an XCD span ~group_m
-  // X blocks x 32/group_m W slices instead of 32/tiles_n X blocks x every W slice
-  int tm, tn;
-  if (epi.group_m > 1) {
-    const int gsz_full = epi.group_m * tiles_n;
-    const int g = wgid / gsz_full, r = wgid - g * gsz_full;
-    const int first = g * epi.group_m;
-    const int gm = min(tiles_m - first, epi.group_m);
+// ---------------------------------------------------------------------------
+// Stream-K schedule (SK = true): a persistent grid of G workgroups (one per CU)
+// splits the T * nk K-iterations of the whole GEMM into G equal contiguous ranges
+// (T >= G, so a tile is split between at most two ranges).  Range p holds
+//   [tail of tile ts: k in ks..nk) [full tiles] [head of tile te: k in 0..ke)
+// and runs them in the order  head -> full tiles -> tail.  The head's fp32
+// accumulators go to slot p of the workspace (write-through sc1 stores, drained,
+// then a relaxed agent-scope flag); range p+1 finishes that tile LAST, starting its
+// own k-loop from those accumulators.  So every tile accumulates k = 0..nk-1 in
+// order into one fp32 accumulator exactly as the data-parallel kernel does: outputs
+// are bit-identical to it whatever the split (batch invariance survives).  A
+// consumer waits only for a head its producer computed FIRST, so the wait is short
+// and no range waits for work queued behind its own.  Tile boundaries fall at a
+// different time on every CU, so epilogue store bursts are spread over the launch
+// instead of arriving together once per tile round, and the last partial round of
+// the data-parallel grid disappears.
+// Flags return to 0 at the end of every launch (the consumer clears the word it
+// consumed), which keeps graph replays valid; a wait gives up after ~2^22 polls and
+// records it in *status (never expected; checked by the tests).
+// ---------------------------------------------------------------------------
+struct SkArgs {
+  float* part;        // G slots x 64 Ki floats (one 256x256 fp32 tile each)
+  unsigned* flags;    // G words, zero between launches
+  unsigned* status;   // give-up counter
+  int64_t iters;      // T * nk
+  int G;              // persistent grid size (multiple of 8)
+};
+constexpr int SK_SLOT_FLOATS = BM * BN;
+
+// tile index -> (tm, tn).  group_m > 1: indices run down a group of group_m M-blocks
+// before moving to the next N-tile, so the tiles an XCD holds at once span ~group_m
+// X blocks x 32/group_m W slices instead of 32/tiles_n X blocks x every W slice.
+SDP_DEV void tile_coords(int t, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+  if (group_m > 1) {
+    const int gsz_full = group_m * tiles_n;
+    const int g = t / gsz_full, r = t - g * gsz_full;
+    const int first = g * group_m;
+    const int gm = min(tiles_m - first, group_m);
     tm = first + r % gm;
     tn = r / gm;
   } else {
-    tm = wgid / tiles_n;
-    tn = wgid % tiles_n;
+    tm = t / tiles_n;
+    tn = t % tiles_n;
   }
-  const int m0 = tm * BM, n0 = tn * BN;
+}
+
+SDP_DEV __amdgpu_buffer_rsrc_t sk_rsrc(float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, SK_SLOT_FLOATS * 4, 0x00020000);
+}
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+#ifdef SDP_GEMM_STAMPS
+// Diagnostic build only (tools/gemm_stamps.py, a separate library): wall-clock stamps of
+// workgroup events, 64 per workgroup; stamp = event code << 56 | s_memrealtime (100 MHz).
+__device__ unsigned long long g_gemm_stamps[8192 * 64];
+#define SDP_STAMP(code)                                                                            \
+  do {                                                                                             \
+    if (tid == 0 && nstamp < 64)                                                                   \
+      g_gemm_stamps[(int64_t)b * 64 + nstamp++] =                                                  \
+          ((unsigned long long)(code) << 56) | (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffffull); \
+  } while (0)
+#else
+#define SDP_STAMP(code) do {} while (0)
+#endif
+
+// EPI: 1 = permlane-paired register epilogue, 4 = whole-line LDS-staged epilogue.
+template <int ACT, int EPI, bool SK>
+__global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
+                                                         const bf16_t* __restrict__ W, int64_t ldw, Epi<bf16_t> epi,
+                                                         int M, int N, int K, int tiles_m, int tiles_n, SkArgs sk) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF8];
+  const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
   const int nk = K / BK;
+#ifdef SDP_GEMM_STAMPS
+  int nstamp = 0;
+#endif
+  SDP_STAMP(0);
+
+  // ---- segment plan: (tile, first k-tile, k-tiles, mode) per segment
+  enum { SEG_FULL = 0, SEG_HEAD = 1, SEG_TAIL = 2 };
+  int nseg = 1, p = 0, ts = 0, ks = 0, te = 0, ke = nk, f0 = 0;
+  bool has_head = false, has_tail = false;
+  // SK: XCD x = b % 8 owns the raster tiles [a_x, a_x+1) (a_x = x T / 8), ordered column-major
+  // over its Gx = G / 8 workgroups (column j = local tiles j, j + Gx, j + 2 Gx, ...), so the
+  // tiles its workgroups hold at any moment are ~Gx consecutive raster tiles, as in the
+  // data-parallel grid; that stream is cut into Gx equal k-iteration ranges, range j = b / 8.
+  int a_x = 0, gx = 1, qx = 1, rx = 0;
+  if constexpr (SK) {
+    const int T = tiles_m * tiles_n, x = b & 7;
+    gx = sk.G >> 3;
+    a_x = (int)((int64_t)x * T / 8);
+    const int tx = (int)((int64_t)(x + 1) * T / 8) - a_x;
+    qx = tx / gx;
+    rx = tx - qx * gx;
+    const int64_t ix = (int64_t)tx * nk, j = b >> 3;
+    const int64_t s = j * ix / gx, e = (j + 1) * ix / gx;
+    ts = (int)(s / nk);
+    ks = (int)(s - (int64_t)ts * nk);
+    te = (int)((e - 1) / nk);
+    ke = (int)(e - (int64_t)te * nk);
+    has_head = ke < nk;
+    has_tail = ks > 0;
+    f0 = ts + (has_tail ? 1 : 0);
+    const int f1 = te - (has_head ? 1 : 0);
+    nseg = (has_head ? 1 : 0) + max(0, f1 - f0 + 1) + (has_tail ? 1 : 0);
+    p = b;
+  } else {
+    const int nwg = tiles_m * tiles_n;
+    const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+    f0 = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  }
+
+  for (int seg = 0; seg < nseg; ++seg) {
+  int tile = f0, kb = 0, kn = nk, mode = SEG_FULL;
+  if constexpr (SK) {
+    if (has_head && seg == 0) { tile = te; kn = ke; mode = SEG_HEAD; }
+    else if (has_tail && seg == nseg - 1) { tile = ts; kb = ks; kn = nk - ks; mode = SEG_TAIL; }
+    else tile = f0 + seg - (has_head ? 1 : 0);
+    if (seg > 0) {  // the previous segment's epilogue staging (all of LDS) must be read out
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  SDP_STAMP(0x10 + mode);
+  if constexpr (SK) {  // column-major stream position -> raster tile
+    int c, r;
+    if (tile < (qx + 1) * rx) {
+      c = tile / (qx + 1);
+      r = tile - c * (qx + 1);
+    } else {
+      const int t2 = tile - (qx + 1) * rx;
+      c = rx + t2 / qx;
+      r = t2 - (c - rx) * qx;
+    }
+    tile = a_x + r * gx + c;
+  }
+  int tm, tn;
+  tile_coords(tile, tiles_m, tiles_n, epi.group_m, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
 
   // The wave's 8 DMA pieces per K-tile (8 rows x 128 B each): [0,1] S1-X,
   // [2,3] S1-W, [4,5] S2-W, [6,7] S3-X.  Source pointers advance by BK per tile.
@@ -518,12 +674,12 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
       if (isx) {
         int g = m0 + r;
         g = g < M ? g : M - 1;
-        src[s] = X + xmap(g) * ldx + c * 8;
+        src[s] = X + xmap(g) * ldx + kb * BK + c * 8;
         loff[s] = piece * 1024;
       } else {
         int g = n0 + r;
         g = g < N ? g : N - 1;
-        src[s] = W + (int64_t)g * ldw + c * 8;
+        src[s] = W + (int64_t)g * ldw + kb * BK + c * 8;
         loff[s] = TILE_BYTES + piece * 1024;
       }
     }
@@ -537,10 +693,37 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   auto S3 = [&](int kt) { dma(6, kt); dma(7, kt); };
 
   f32x4 acc[4][8];
+  if (SK && mode == SEG_TAIL) {
+    // continue the head's accumulation (range p-1 computed it first, so this rarely waits)
+    const int prev = p - 8;  // range j - 1 of the same XCD
+    SDP_STAMP(2);
+    if (wave == 0) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(sk.flags + prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 22)) {
+          if (lane == 0) __hip_atomic_fetch_add(sk.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the poll
+    SDP_STAMP(3);
+    const __amdgpu_buffer_rsrc_t rs = sk_rsrc(sk.part + (int64_t)prev * SK_SLOT_FLOATS);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((wave * 32 + i * 8 + j) * 64 + lane) * 16, 0, 16));
+    if (tid == 0) __hip_atomic_store(sk.flags + prev, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   bf16x8 xf[8], w0[4], w1[4];
   auto read_x = [&](const char* xt, int jm) {
@@ -582,16 +765,17 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
 
   // prologue: S1(0) S2(0) S3(0) [S1(1) S2(1)]; retire S1(0)
   S1(0); S2(0); S3(0);
-  if (nk > 1) { S1(1); S2(1); SDP_VMCNT(10); }
+  if (kn > 1) { S1(1); S2(1); SDP_VMCNT(10); }
   else SDP_VMCNT(4);
   __builtin_amdgcn_s_barrier();
   if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one barrier
+  SDP_STAMP(4);
   __builtin_amdgcn_sched_barrier(0);
 
-  for (int t = 0; t < nk; ++t) {
+  for (int t = 0; t < kn; ++t) {
     const char* xt = smem + (t & 1) * BUF8;
     const char* wt = xt + TILE_BYTES;
-    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
+    const bool more1 = t + 1 < kn, more2 = t + 2 < kn;
     // phase 0: Q(m0, n0)
     read_w(wt, 0, w0);
     read_x(xt, 0);
@@ -611,13 +795,32 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     mfma_section([&] { quad(1, 0, w0); });
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  SDP_STAMP(5);
+  if (SK && mode == SEG_HEAD) {
+    // publish the head's accumulators to slot p: sc1 (write-through) stores, every wave
+    // drains them, then one lane raises the flag (relaxed agent-scope store)
+    const __amdgpu_buffer_rsrc_t rs = sk_rsrc(sk.part + (int64_t)p * SK_SLOT_FLOATS);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[i][j]), rs,
+                                               ((wave * 32 + i * 8 + j) * 64 + lane) * 16, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (tid == 0) __hip_atomic_store(sk.flags + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    SDP_STAMP(6);
+    continue;
+  }
   if constexpr (EPI == 4) {  // whole-line epilogue, all eight row groups staged first (16 KiB
     // per wave: both K buffers, free once the balancing barrier above has passed); the host
     // routes resid_pre-with-activation and unaligned calls to EPI 1
     tile_epilogue_rows<ACT, 4, true>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + wave * 16384);
-    return;
+  } else {
+    tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
   }
-  tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
+  SDP_STAMP(6);
+  }  // segments
 }
 
 #undef SDP_VMCNT
@@ -758,6 +961,95 @@ extern "C" int sdp_gemm_set_store_policy(int nt) {
   return old;
 }
 
+// ---- stream-K workspaces (caller-owned, registered per stream)
+// layout: [flags: 4 KiB][status: 4 KiB][G slots x 256 KiB fp32]
+static int g_sk_mode = 0;  // 1 = stream-K where it applies and a workspace is registered (measured slower, off)
+struct SkWorkspace {
+  void* stream;
+  char* base;
+};
+static SkWorkspace g_sk_ws[16];
+static std::mutex g_sk_mu;
+static int g_sk_grid = 0;
+
+static int sk_grid() {
+  if (!g_sk_grid) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      g_sk_grid = std::min(1024, cus & ~7);
+    if (g_sk_grid < 8) g_sk_grid = 8;
+  }
+  return g_sk_grid;
+}
+
+extern "C" int64_t sdp_gemm_workspace_bytes(void) {
+  return 8192 + (int64_t)sk_grid() * fast::SK_SLOT_FLOATS * 4;
+}
+
+extern "C" int sdp_gemm_set_workspace(void* stream, void* ws, int64_t bytes) {
+  std::lock_guard<std::mutex> lk(g_sk_mu);
+  for (auto& w : g_sk_ws)
+    if (w.base && w.stream == stream) w.base = nullptr;
+  if (!ws) return 0;
+  if (bytes < sdp_gemm_workspace_bytes() || (uintptr_t)ws % 256) return (int)hipErrorInvalidValue;
+  for (auto& w : g_sk_ws)
+    if (!w.base) {
+      w.stream = stream;
+      w.base = (char*)ws;
+      return 0;
+    }
+  return (int)hipErrorOutOfMemory;
+}
+
+extern "C" int sdp_gemm_set_schedule(int mode) {
+  int old = g_sk_mode;
+  if (mode == 0 || mode == 1) g_sk_mode = mode;
+  return old;
+}
+
+// 1 if a bf16 fast-kernel GEMM of this shape takes the stream-K schedule (given a workspace)
+extern "C" int sdp_gemm_sk_applies(int M, int N, int K) {
+  if (!g_sk_mode || M <= 0 || N <= 0 || K <= 0 || sdp_gemm_variant(1, M, N, K) != 1) return 0;
+  const int64_t T = (int64_t)((M + fast::BM - 1) / fast::BM) * ((N + fast::BN - 1) / fast::BN);
+  const int G = sk_grid();
+  return (T >= G && T % G != 0) ? 1 : 0;
+}
+
+// Give-up count of the stream-K waits on this stream's workspace (tests; synchronous).
+extern "C" int sdp_gemm_sk_status(void* stream, unsigned* out) {
+  char* ws = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_sk_mu);
+    for (auto& w : g_sk_ws)
+      if (w.base && w.stream == stream) ws = w.base;
+  }
+  if (!ws || !out) return (int)hipErrorInvalidValue;
+  hipError_t rc = hipStreamSynchronize((hipStream_t)stream);
+  if (rc == hipSuccess) rc = hipMemcpy(out, ws + 4096, sizeof(unsigned), hipMemcpyDeviceToHost);
+  return (int)rc;
+}
+
+#ifdef SDP_GEMM_STAMPS
+extern "C" int sdp_gemm_stamps(void* dst, int64_t bytes, int clear) {
+  hipError_t rc = hipDeviceSynchronize();
+  if (rc == hipSuccess && dst) rc = hipMemcpyFromSymbol(dst, HIP_SYMBOL(fast::g_gemm_stamps), std::min<int64_t>(bytes, sizeof(fast::g_gemm_stamps)));
+  if (rc == hipSuccess && clear) {
+    void* p = nullptr;
+    rc = hipGetSymbolAddress(&p, HIP_SYMBOL(fast::g_gemm_stamps));
+    if (rc == hipSuccess) rc = hipMemset(p, 0, sizeof(fast::g_gemm_stamps));
+  }
+  return (int)rc;
+}
+#endif
+
+static char* sk_lookup(void* stream) {
+  std::lock_guard<std::mutex> lk(g_sk_mu);
+  for (auto& w : g_sk_ws)
+    if (w.base && w.stream == stream) return w.base;
+  return nullptr;
+}
+
 int sdp_row_partials(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, int M, int C,
                      float* part, void* stream);
 
@@ -826,8 +1118,24 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
         e.part = part;
         if (part_done) *part_done = true;
       }
-#define SDP_8PH(A, E) hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s, \
-                                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
+      fast::SkArgs sk{};
+      char* ws = sdp_gemm_sk_applies(M, N, K) ? sk_lookup(stream) : nullptr;
+      if (ws) {
+        sk.flags = (unsigned*)ws;
+        sk.status = (unsigned*)(ws + 4096);
+        sk.part = (float*)(ws + 8192);
+        sk.G = sk_grid();
+        sk.iters = (int64_t)tm * tn * (K / fast::BK);
+      }
+#define SDP_8PH(A, E)                                                                                               \
+  do {                                                                                                              \
+    if (ws)                                                                                                         \
+      hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, true>), dim3(sk.G), dim3(fast::NTHREADS), 0, s,                 \
+                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);                 \
+    else                                                                                                            \
+      hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,             \
+                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);                 \
+  } while (0)
       // exact-erf GELU goes through the runtime-activation epilogue (apply_act)
       const int ak = (act == ACT_GELU && g_exact_gelu) ? -1 : act;
       if (fk == 14) {

@@ -1622,20 +1622,30 @@ __global__ __launch_bounds__(256) void sumsq_k(float* const* __restrict__ grads,
   }
 }
 
+// steps (optional): per-tensor count of completed optimizer steps (fp32, exact to 2^24); the
+// bias corrections of this step use steps[t] + 1, computed in double (torch AdamW computes
+// 1 - beta ** step on the host in double).  dscale (optional): the device GradScaler scale;
+// the grads are unscaled by 1 / dscale[0] instead of inv_scale.
 __global__ __launch_bounds__(256) void adamw_k(float* const* __restrict__ params, float* const* __restrict__ grads,
                                                float* const* __restrict__ m1, float* const* __restrict__ m2,
                                                const int64_t* __restrict__ sizes, const MTBlock* __restrict__ blocks,
                                                const float* __restrict__ state, float lr, float b1, float b2,
                                                float eps, float wd, float bc1, float bc2, float inv_scale,
-                                               float max_norm) {
+                                               float max_norm, const float* __restrict__ steps,
+                                               const float* __restrict__ dscale) {
   if (((const int*)state)[1] != 0) return;  // inf / nan in the grads: skip the step (GradScaler)
-  float sc = inv_scale;
+  float sc = dscale ? 1.0f / dscale[0] : inv_scale;
   if (max_norm > 0.f) {
-    const float norm = sqrtf(state[0]) * inv_scale;
+    const float norm = sqrtf(state[0]) * sc;
     const float clip = max_norm / (norm + 1e-6f);
     if (clip < 1.f) sc *= clip;
   }
   const MTBlock bl = blocks[blockIdx.x];
+  if (steps) {
+    const double st = (double)steps[bl.tensor] + 1.0;
+    bc1 = (float)(1.0 - pow((double)b1, st));
+    bc2 = (float)(1.0 - pow((double)b2, st));
+  }
   float* p = params[bl.tensor];
   const float* g = grads[bl.tensor];
   float* a = m1[bl.tensor];
@@ -1673,7 +1683,54 @@ extern "C" int sdp_adamw(float* const* params, float* const* grads, float* const
   const float bc1 = 1.0f - powf(beta1, (float)step), bc2 = 1.0f - powf(beta2, (float)step);
   hipLaunchKernelGGL(adamw_k, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg, exp_avg_sq,
                      sizes, (const MTBlock*)blocks, state, lr, beta1, beta2, eps, weight_decay, bc1, bc2, inv_scale,
-                     max_norm);
+                     max_norm, (const float*)nullptr, (const float*)nullptr);
+  return SDP_CHECK_LAUNCH();
+}
+
+extern "C" int sdp_adamw_dev(float* const* params, float* const* grads, float* const* exp_avg,
+                             float* const* exp_avg_sq, const int64_t* sizes, const void* blocks, int nblocks,
+                             const float* state, float lr, float beta1, float beta2, float eps, float weight_decay,
+                             const float* steps, const float* scale, float inv_scale, float max_norm, void* stream) {
+  if (!params || !grads || !exp_avg || !exp_avg_sq || !sizes || !blocks || !state || !steps || nblocks < 0)
+    return (int)hipErrorInvalidValue;
+  if (nblocks == 0) return 0;
+  hipLaunchKernelGGL(adamw_k, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg, exp_avg_sq,
+                     sizes, (const MTBlock*)blocks, state, lr, beta1, beta2, eps, weight_decay, 1.f, 1.f, inv_scale,
+                     max_norm, steps, scale);
+  return SDP_CHECK_LAUNCH();
+}
+
+// End of an optimizer step: when the step was taken (no inf / nan flagged in state[1]) every
+// per-tensor step count advances; with sc != NULL the GradScaler scale updates (backoff on a
+// skipped step, growth every `interval` clean steps); state is reset for the next step.
+__global__ __launch_bounds__(256) void adamw_finish_k(float* __restrict__ state, float* __restrict__ sc, float growth,
+                                                      float backoff, int interval, float* __restrict__ steps, int n) {
+  const bool bad = ((const int*)state)[1] != 0;
+  if (!bad && steps)
+    for (int i = threadIdx.x; i < n; i += 256) steps[i] += 1.0f;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (sc) {
+      int* tr = (int*)(sc + 1);
+      if (bad) {
+        sc[0] *= backoff;
+        *tr = 0;
+      } else if (++*tr >= interval) {
+        sc[0] *= growth;
+        *tr = 0;
+      }
+    }
+    state[0] = 0.f;
+    ((int*)state)[1] = 0;
+  }
+}
+
+extern "C" int sdp_adamw_finish(float* state, float* scale_tracker, float growth, float backoff, int interval,
+                                float* steps, int nsteps, void* stream) {
+  if (!state || nsteps < 0 || (scale_tracker && interval <= 0) || (nsteps > 0 && !steps))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(adamw_finish_k, dim3(1), dim3(256), 0, (hipStream_t)stream, state, scale_tracker, growth,
+                     backoff, interval, steps, nsteps);
   return SDP_CHECK_LAUNCH();
 }
 

@@ -40,6 +40,11 @@ _SIGS = {
     "sdp_gemm_set_store_policy": ([_i32], _i32),
     "sdp_gemm_set_group_m": ([_i32], _i32),
     "sdp_gemm_set_exact_gelu": ([_i32], _i32),
+    "sdp_gemm_workspace_bytes": ([], _i64),
+    "sdp_gemm_set_workspace": ([_vp, _vp, _i64], _i32),
+    "sdp_gemm_set_schedule": ([_i32], _i32),
+    "sdp_gemm_sk_applies": ([_i32, _i32, _i32], _i32),
+    "sdp_gemm_sk_status": ([_vp, _vp], _i32),
     "sdp_layernorm": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _f32, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_qk_headnorm": ([_i32, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp], _i32),
     "sdp_rowstats": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _i32, _i32, _vp], _i32),
@@ -91,6 +96,9 @@ _SIGS = {
     "sdp_grad_sumsq": ([_vp, _vp, _vp, _i32, _vp, _vp], _i32),
     "sdp_adamw": ([_vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _f32, _f32, _f32, _f32, _f32, _i32, _f32, _f32, _vp], _i32),
     "sdp_scaler_update": ([_vp, _vp, _f32, _f32, _i32, _vp], _i32),
+    "sdp_adamw_dev": ([_vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _f32, _f32,
+                       _vp], _i32),
+    "sdp_adamw_finish": ([_vp, _vp, _f32, _f32, _i32, _vp, _i32, _vp], _i32),
 }
 
 _lib = None
@@ -130,6 +138,9 @@ def lib():
         kern = os.environ.get("SDPNET_GEMM_GROUP_M")  # tile raster of the 8-phase GEMM (-1 auto, 1 row-major)
         if kern:
             L.sdp_gemm_set_group_m(int(kern))
+        kern = os.environ.get("SDPNET_GEMM_SCHEDULE")  # 0 data-parallel tiles, 1 stream-K (default)
+        if kern:
+            L.sdp_gemm_set_schedule(int(kern))
         kern = os.environ.get("SDPNET_DW_KERNEL")  # A/B switch for the depthwise conv
         if kern:
             L.sdp_dwconv_set_kernel(int(kern))
@@ -217,9 +228,14 @@ def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Option
         r = [resid.t.data_ptr(), resid.ld, *resid.map()]
     else:
         r = [None, 0, 0, 0, 0]
+    if dt == BF16:
+        _ensure_workspace(y.t, M, N, K)
     timer = _TIMER
     if timer is not None:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # inside a graph capture the events become external event-record nodes of the graph
+        ext = torch.cuda.is_current_stream_capturing()
+        e0 = torch.cuda.Event(enable_timing=True, external=ext)
+        e1 = torch.cuda.Event(enable_timing=True, external=ext)
         e0.record()
     if ln is None and part is None:
         rc = lib().sdp_gemm(dt, *x.args(), w.data_ptr(), w.stride(0), _ptr(bias), *r, *y.args(), M, N, K, act,
@@ -237,6 +253,32 @@ def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Option
         es = x.t.element_size()
         nbytes = es * (M * K + N * K + M * N * (2 if resid is not None else 1)) + (4 * N if bias is not None else 0)
         timer("gemm", (M, N, K, lib().sdp_gemm_variant(dt, M, N, K)), 2.0 * M * N * K, nbytes, e0, e1)
+
+
+# Stream-K workspaces, one per HIP stream that has run a GEMM (caller-owned memory the
+# library only borrows; see sdp_gemm_set_workspace).  A stream first seen while a graph
+# is being captured gets none, and its GEMMs keep the data-parallel tile schedule.
+_WS = {}
+
+
+def _ensure_workspace(t: torch.Tensor, M: int, N: int, K: int):
+    s = torch.cuda.current_stream(t.device)
+    key = (t.device.index, s.cuda_stream)
+    if key in _WS or not lib().sdp_gemm_sk_applies(M, N, K) or torch.cuda.is_current_stream_capturing():
+        return
+    ws = torch.zeros(int(lib().sdp_gemm_workspace_bytes()), dtype=torch.uint8, device=t.device)
+    _check(lib().sdp_gemm_set_workspace(s.cuda_stream, ws.data_ptr(), ws.numel()), "gemm_set_workspace")
+    _WS[key] = ws
+
+
+def gemm_sk_status(t: torch.Tensor) -> int:
+    """Give-up count of the stream-K waits on the current stream's workspace (0 expected)."""
+    key = (t.device.index, torch.cuda.current_stream(t.device).cuda_stream)
+    if key not in _WS:
+        return 0
+    out = ctypes.c_uint(0)
+    _check(lib().sdp_gemm_sk_status(key[1], ctypes.byref(out)), "gemm_sk_status")
+    return int(out.value)
 
 
 def layernorm(x: Rows, gamma: torch.Tensor, beta: torch.Tensor, eps: float, y: Rows, M: int, C: int):

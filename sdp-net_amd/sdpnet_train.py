@@ -649,89 +649,153 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, label_smoothing: f
 
 class AdamW(torch.optim.Optimizer):
     """torch.optim.AdamW (training_tools.py:235; betas (0.9, 0.999), eps 1e-8, decoupled weight
-    decay) as one multi-tensor HIP kernel.  ``step(grad_scale=S, max_norm=M)`` also performs
-    GradScaler.unscale_ (grads / S), the inf/nan check that skips the step, and
-    clip_grad_norm_(M) (training_tools.py:94-99) on device, without a host sync; the
-    scaler state lives in ``self.scaler`` ([scale, growth tracker]) and updates like
-    torch.amp.GradScaler (growth 2, backoff 0.5, interval 2000)."""
+    decay) as one multi-tensor HIP kernel, with torch.amp.GradScaler semantics folded in
+    (training_tools.py:63-64, :91-99).
+
+    ``step(grad_scale=S, max_norm=M)`` performs GradScaler.unscale_ (grads / S), the inf/nan
+    check, clip_grad_norm_(M) and the AdamW update on device without a host sync.  A step
+    whose gradients hold an inf/nan is skipped exactly as ``scaler.step(optimizer)`` skips
+    ``optimizer.step()``: parameters, moments AND step counts stay as they were (the step
+    counts live on the device, ``state[p]["step"]`` is a 0-d view of them).  ``grad_scale=None``
+    unscales by the device scale ``self.scaler[0]``; multiply the loss by the same value with
+    ``opt.scale(loss)`` and a backoff takes effect on the next step without any host sync.
+    The scale updates like torch.amp.GradScaler (growth 2, backoff 0.5, interval 2000) unless
+    ``update_scaler=False``.  Parameters whose ``grad`` is None are left out of the step
+    (no decay, no moment update, no step count), as torch does.  The device work lists are
+    rebuilt whenever a parameter, its state tensors or the set of parameters with gradients
+    change (``load_state_dict``, ``add_param_group``, a reallocated tensor)."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, init_scale=65536.0,
                  growth_interval=2000):
-        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._tables = None
+        self._sig = None
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.growth_interval = growth_interval
         self._init_scale = float(init_scale)
         self.scaler = None
         self.state_buf = None
 
+    def add_param_group(self, param_group):
+        super().add_param_group(param_group)
+        self._tables = None
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._tables = None
+
+    def _ensure_device_state(self, dev):
+        if self.scaler is None:
+            self.state_buf = torch.zeros(2, dtype=torch.float32, device=dev)
+            self.scaler = torch.tensor([self._init_scale, 0.0], dtype=torch.float32, device=dev)
+            self.scaler[1:].view(torch.int32).zero_()
+
+    def scale(self, loss: torch.Tensor) -> torch.Tensor:
+        """GradScaler.scale(loss): loss * the device scale (no host sync)."""
+        self._ensure_device_state(loss.device)
+        return loss * self.scaler[0]
+
+    def _signature(self):
+        sig = []
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is None:
+                    sig.append(None)
+                    continue
+                st = self.state.get(p)
+                if not st:
+                    sig.append(-1)
+                    continue
+                sig.append((p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), id(st["step"])))
+        return sig
+
     def _build(self, dev):
+        import struct
         bb = sp.lib().sdp_mt_block_bytes()
         self._tables = []
-        for group in self.param_groups:
-            ps = [p for p in group["params"] if p.requires_grad]
+        groups = [[p for p in group["params"] if p.grad is not None] for group in self.param_groups]
+        counts = []
+        for ps in groups:
             for p in ps:
-                if p.dtype != torch.float32 or not p.is_contiguous():
-                    raise TypeError("sdpnet AdamW: fp32 contiguous parameters only")
+                if p.dtype != torch.float32 or not p.is_contiguous() or p.device != dev:
+                    raise TypeError("sdpnet AdamW: fp32 contiguous parameters on one device only")
                 st = self.state[p]
                 if not st:
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
+                for k in ("exp_avg", "exp_avg_sq"):  # e.g. a state dict loaded to another device
+                    t = st[k]
+                    if t.device != dev or t.dtype != torch.float32 or not t.is_contiguous():
+                        st[k] = t.to(device=dev, dtype=torch.float32).contiguous()
+                counts.append(float(st["step"]))
+        # one device array of step counts for every table (sdp_adamw_finish advances it in one launch)
+        self._steps = torch.tensor(counts, dtype=torch.float32, device=dev)
+        base = 0
+        for ps in groups:
+            steps = self._steps[base:base + len(ps)]
+            for i, p in enumerate(ps):
+                self.state[p]["step"] = steps[i]
+            base += len(ps)
             blocks = []
             for ti, p in enumerate(ps):
-                for s in range(0, p.numel(), 4096):
-                    blocks.append((ti, s))
+                for s0 in range(0, p.numel(), 4096):
+                    blocks.append((ti, s0))
             raw = bytearray(bb * len(blocks))
-            import struct
-            for i, (t, s) in enumerate(blocks):
-                struct.pack_into("<iiq", raw, i * bb, t, 0, s)
-            btab = torch.frombuffer(raw, dtype=torch.uint8).to(dev) if blocks else torch.empty(0, dtype=torch.uint8,
-                                                                                                 device=dev)
+            for i, (t, s0) in enumerate(blocks):
+                struct.pack_into("<iiq", raw, i * bb, t, 0, s0)
+            btab = (torch.frombuffer(raw, dtype=torch.uint8).to(dev) if blocks
+                    else torch.empty(0, dtype=torch.uint8, device=dev))
             sizes = torch.tensor([p.numel() for p in ps], dtype=torch.int64, device=dev)
 
             def ptrs(ts):
                 return torch.tensor([t.data_ptr() for t in ts], dtype=torch.int64, device=dev)
             self._tables.append(dict(params=ps, blocks=btab, nblocks=len(blocks), sizes=sizes, pp=ptrs(ps),
                                      m1=ptrs([self.state[p]["exp_avg"] for p in ps]),
-                                     m2=ptrs([self.state[p]["exp_avg_sq"] for p in ps])))
-        self.state_buf = torch.zeros(2, dtype=torch.float32, device=dev)
-        self.scaler = torch.tensor([self._init_scale, 0.0], dtype=torch.float32, device=dev)
-        self.scaler[1:].view(torch.int32).zero_()
+                                     m2=ptrs([self.state[p]["exp_avg_sq"] for p in ps]), steps=steps))
+        self._ensure_device_state(dev)
+        self._sig = self._signature()
 
     @torch.no_grad()
-    def step(self, closure=None, grad_scale: float = 1.0, max_norm: float = 0.0, update_scaler: bool = True):
-        loss = closure() if closure is not None else None
-        dev = self.param_groups[0]["params"][0].device
-        if self._tables is None:
+    def step(self, closure=None, grad_scale: Optional[float] = 1.0, max_norm: float = 0.0,
+             update_scaler: bool = True):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        dev = None
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is not None:
+                    dev = p.device
+                    break
+            if dev is not None:
+                break
+        if dev is None:
+            return loss
+        self._ensure_device_state(dev)
+        if self._tables is None or self._signature() != self._sig:
             self._build(dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
         L = sp.lib()
         gptr = []
         for tab in self._tables:
-            gs = []
-            for p in tab["params"]:
-                if p.grad is None:
-                    p.grad = torch.zeros_like(p)
-                gs.append(p.grad)
-            g = torch.tensor([t.data_ptr() for t in gs], dtype=torch.int64, device=dev)
+            g = torch.tensor([p.grad.data_ptr() for p in tab["params"]], dtype=torch.int64, device=dev)
             gptr.append(g)
             sp._check(L.sdp_grad_sumsq(g.data_ptr(), tab["sizes"].data_ptr(), tab["blocks"].data_ptr(),
                                        tab["nblocks"], self.state_buf.data_ptr(), stream), "grad_sumsq")
-        inv = 1.0 / float(grad_scale)
+        dscale = self.scaler.data_ptr() if grad_scale is None else None
+        inv = 1.0 if grad_scale is None else 1.0 / float(grad_scale)
         for tab, g, group in zip(self._tables, gptr, self.param_groups):
-            b1, b2 = group["betas"]
-            step = None
-            for p in tab["params"]:
-                self.state[p]["step"] += 1
-                step = self.state[p]["step"]
-            if step is None:
+            if not tab["params"]:
                 continue
-            sp._check(L.sdp_adamw(tab["pp"].data_ptr(), g.data_ptr(), tab["m1"].data_ptr(), tab["m2"].data_ptr(),
-                                  tab["sizes"].data_ptr(), tab["blocks"].data_ptr(), tab["nblocks"],
-                                  self.state_buf.data_ptr(), float(group["lr"]), float(b1), float(b2),
-                                  float(group["eps"]), float(group["weight_decay"]), int(step), inv,
-                                  float(max_norm), stream), "adamw")
-        if update_scaler:
-            sp._check(L.sdp_scaler_update(self.state_buf.data_ptr(), self.scaler.data_ptr(), 2.0, 0.5,
-                                          self.growth_interval, stream), "scaler_update")
+            b1, b2 = group["betas"]
+            sp._check(L.sdp_adamw_dev(tab["pp"].data_ptr(), g.data_ptr(), tab["m1"].data_ptr(),
+                                      tab["m2"].data_ptr(), tab["sizes"].data_ptr(), tab["blocks"].data_ptr(),
+                                      tab["nblocks"], self.state_buf.data_ptr(), float(group["lr"]), float(b1),
+                                      float(b2), float(group["eps"]), float(group["weight_decay"]),
+                                      tab["steps"].data_ptr(), dscale, inv, float(max_norm), stream), "adamw")
+        # step counts advance only if the step was taken; scale update; state reset
+        sp._check(L.sdp_adamw_finish(self.state_buf.data_ptr(), self.scaler.data_ptr() if update_scaler else None,
+                                     2.0, 0.5, self.growth_interval, self._steps.data_ptr(), self._steps.numel(),
+                                     stream), "adamw_finish")
         return loss

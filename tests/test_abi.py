@@ -15,7 +15,7 @@ HEADER = os.path.join(REPO, "include", "sdpnet_hip.h")
 
 def header_symbols():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(sdp_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^(?:int64_t|int|const char\*)\s+(sdp_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_header_symbol():

@@ -155,6 +155,113 @@ def test_adamw_kernel_matches_torch_adamw_with_scaler_and_clip():
     assert float(opt_o.scaler[0]) == 65536.0 * 0.5
 
 
+def _torch_adamw_reference(shapes, lr=3e-3, wd=0.05, init_scale=1024.0, growth_interval=2):
+    ps = [torch.randn(*sh, device=DEV) for sh in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    opt = torch.optim.AdamW(ref, lr=lr, weight_decay=wd)
+    scaler = torch.amp.GradScaler("cuda", init_scale=init_scale, growth_interval=growth_interval)
+    scaler.scale(torch.ones((), device=DEV))  # lazy-initialises the scale on the device
+    return ps, ref, opt, scaler
+
+
+@pytest.mark.gpu
+def test_adamw_gradscaler_semantics_match_torch_step_for_step():
+    """GradScaler + AdamW with an inf step in the middle (training_tools.py:91-99): the skipped step
+    leaves params, moments and step counts alone, the scale backs off, the following finite steps
+    use the right bias corrections, and the scale grows after `growth_interval` clean steps.
+    Ours runs on the device scale (loss scaled by opt.scaler[0], grad_scale=None: no host sync)."""
+    import sdpnet_train
+    torch.manual_seed(5)
+    shapes = [(300, 70), (5000,), (3, 4, 5), (1,)]
+    ps, ref, opt_r, scaler = _torch_adamw_reference(shapes)
+    ours = [p.clone().requires_grad_(True) for p in ps]
+    opt_o = sdpnet_train.AdamW(ours, lr=3e-3, weight_decay=0.05, init_scale=1024.0, growth_interval=2)
+    for it in range(6):
+        gs = [torch.randn(*sh, device=DEV) * (8.0 if it == 3 else 0.1) for sh in shapes]
+        if it in (1, 4):
+            gs[1][17] = float("inf") if it == 1 else float("nan")
+        s_ref = scaler.get_scale()
+        for r, g in zip(ref, gs):
+            r.grad = g * s_ref
+        scaler.unscale_(opt_r)
+        torch.nn.utils.clip_grad_norm_(ref, 5.0)
+        scaler.step(opt_r)
+        scaler.update()
+        for o, g in zip(ours, gs):
+            o.grad = opt_o.scale(g)  # grads of opt.scale(loss).backward()
+        opt_o.step(grad_scale=None, max_norm=5.0)
+        torch.cuda.synchronize()
+        assert float(opt_o.scaler[0]) == scaler.get_scale(), it
+        for r, o in zip(ref, ours):
+            assert torch.allclose(r, o, atol=2e-6, rtol=1e-5), (it, (r - o).abs().max().item())
+            sr, so = opt_r.state.get(r, {}), opt_o.state[o]
+            if sr:
+                assert float(sr["step"]) == float(so["step"]), it
+                assert torch.allclose(sr["exp_avg"], so["exp_avg"], atol=1e-7, rtol=1e-5)
+                assert torch.allclose(sr["exp_avg_sq"], so["exp_avg_sq"], atol=1e-9, rtol=1e-5)
+    assert float(opt_o.state[ours[0]]["step"]) == 4.0  # 6 calls, 2 skipped
+
+
+@pytest.mark.gpu
+def test_adamw_skips_params_without_grad_and_resets_state_without_scaler_update():
+    import sdpnet_train
+    torch.manual_seed(6)
+    shapes = [(64, 8), (33,), (7,)]
+    ps, ref, opt_r, _ = _torch_adamw_reference(shapes)
+    ours = [p.clone().requires_grad_(True) for p in ps]
+    opt_o = sdpnet_train.AdamW(ours, lr=3e-3, weight_decay=0.05)
+    for it in range(3):
+        gs = [torch.randn(*sh, device=DEV) for sh in shapes]
+        for r, o, g, i in zip(ref, ours, gs, range(3)):
+            r.grad = None if i == 1 else g.clone()
+            o.grad = None if i == 1 else g.clone()
+        if it == 0:  # an inf with update_scaler=False: skipped, and the flag must not stick
+            ours[0].grad[0, 0] = float("inf")
+            before = [o.detach().clone() for o in ours]
+            opt_o.step(grad_scale=1.0, update_scaler=False)
+            torch.cuda.synchronize()
+            assert all(torch.equal(b, o) for b, o in zip(before, ours))
+            continue
+        opt_r.step()
+        opt_o.step(grad_scale=1.0, update_scaler=False)
+        torch.cuda.synchronize()
+        for r, o in zip(ref, ours):
+            assert torch.allclose(r, o, atol=2e-6, rtol=1e-5), (it, (r - o).abs().max().item())
+    assert torch.equal(ours[1], ps[1]) and not opt_o.state.get(ours[1])
+
+
+@pytest.mark.gpu
+def test_adamw_state_dict_reload_from_cpu_then_step():
+    """Resume as training_tools.py:198 does: optimizer.load_state_dict of a CPU copy between
+    steps must rebuild the device work lists (no stale pointers) and continue like torch."""
+    import copy
+    import sdpnet_train
+    torch.manual_seed(7)
+    shapes = [(100, 30), (9,)]
+    ps, ref, opt_r, _ = _torch_adamw_reference(shapes)
+    ours = [p.clone().requires_grad_(True) for p in ps]
+    opt_o = sdpnet_train.AdamW(ours, lr=3e-3, weight_decay=0.05)
+    for it in range(4):
+        gs = [torch.randn(*sh, device=DEV) for sh in shapes]
+        for r, o, g in zip(ref, ours, gs):
+            r.grad = g.clone()
+            o.grad = g.clone()
+        opt_r.step()
+        opt_o.step(grad_scale=1.0)
+        if it == 1:
+            sd = copy.deepcopy(opt_o.state_dict())
+            for st in sd["state"].values():
+                for k in list(st):
+                    st[k] = st[k].detach().cpu().clone()
+            opt_o.load_state_dict(sd)
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        torch.cuda.synchronize()
+        for r, o in zip(ref, ours):
+            assert torch.allclose(r, o, atol=2e-6, rtol=1e-5), (it, (r - o).abs().max().item())
+    assert float(opt_o.state[ours[0]]["step"]) == 4.0
+
+
 @pytest.mark.gpu
 def test_dropout_and_drop_path_are_active_in_train_mode():
     """Canonical-style dropouts (0.2) and drop path: train-mode logits differ between two
