@@ -112,7 +112,17 @@ def cpu_baseline(model_cpu_sd, cfg, seconds=12.0, name="SdP-Net-M"):
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
+    import glob
+    ratio = None  # oracle speed / the reference's own CPU forward, measured in the build container
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_cpu_ratio.json")), reverse=True):
+        try:
+            ratio = json.load(open(f))
+            ratio["source"] = os.path.relpath(f, REPO)
+            break
+        except (OSError, ValueError):
+            continue
     return {"value": round(n / dt, 3), "unit": "images/sec", "cores": threads, "kind": "port",
+            "port_vs_reference": ratio,
             "sample": f"{name} fp32 eval forward, {n} images in batches of {bs}, {dt:.1f} s, "
                       f"oracle/sdpnet_oracle.py (reference math, stock torch CPU ops)"}
 

@@ -107,7 +107,8 @@ int sdp_gemm_set_exact_gelu(int on);
  *   sdp_gemm_set_workspace(stream, ws, bytes)  register ZERO-FILLED device memory (256-B
  *       aligned) for GEMMs launched on `stream` (ws = NULL unregisters).  The library keeps
  *       it zero between launches; streams without one use the data-parallel schedule.
- *   sdp_gemm_set_schedule(mode)  1 = stream-K where it applies (default), 0 = never.
+ *   sdp_gemm_set_schedule(mode)  1 = stream-K where it applies, 0 = never (default: on the
+ *       model shapes it measured slower than the data-parallel grid).
  *   sdp_gemm_sk_applies(M, N, K) 1 if such a launch takes stream-K (given a workspace).
  *   sdp_gemm_sk_status(stream, &n) synchronous: bounded-wait give-ups recorded on the
  *       stream's workspace (0 unless a split tile's producer never published).
@@ -401,6 +402,12 @@ int sdp_adamw_dev(float* const* params, float* const* grads, float* const* exp_a
                   float inv_scale, float max_norm, void* stream);
 int sdp_adamw_finish(float* state, float* scale_tracker, float growth, float backoff, int interval, float* steps,
                      int nsteps, void* stream);
+/* Bit-reproducible gradient norm: sdp_grad_sumsq_parts writes block b's sum of squares to
+ * partials[b] (and flags non-finite values in state[1]); sdp_sum_partials adds partials[0..n)
+ * in a fixed order into state[0].  Same result as sdp_grad_sumsq without float atomics. */
+int sdp_grad_sumsq_parts(float* const* grads, const int64_t* sizes, const void* blocks, int nblocks,
+                         float* partials, float* state, void* stream);
+int sdp_sum_partials(const float* partials, int n, float* state, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1626,6 +1626,68 @@ __global__ __launch_bounds__(256) void sumsq_k(float* const* __restrict__ grads,
 // bias corrections of this step use steps[t] + 1, computed in double (torch AdamW computes
 // 1 - beta ** step on the host in double).  dscale (optional): the device GradScaler scale;
 // the grads are unscaled by 1 / dscale[0] instead of inv_scale.
+// Deterministic form of sumsq_k: block b writes its sum of squares to partials[b] (the
+// non-finite flag is an integer max, order-free), sum_partials_k adds them in a fixed order,
+// so the clip coefficient -- and every parameter after the step -- is bit-reproducible.
+__global__ __launch_bounds__(256) void sumsq_parts_k(float* const* __restrict__ grads,
+                                                     const int64_t* __restrict__ sizes,
+                                                     const MTBlock* __restrict__ blocks, float* __restrict__ partials,
+                                                     float* __restrict__ state) {
+  const MTBlock bl = blocks[blockIdx.x];
+  const float* g = grads[bl.tensor];
+  const int64_t n = sizes[bl.tensor];
+  float s = 0.f;
+  int bad = 0;
+  for (int64_t i = bl.start + threadIdx.x; i < min(n, bl.start + 4096); i += 256) {
+    const float v = g[i];
+    s = fmaf(v, v, s);
+    bad |= !isfinite(v);
+  }
+  __shared__ float red[4];
+  __shared__ int rb[4];
+  s = wave_sum(s);
+  const int wb = __ballot(bad) != 0ull ? 1 : 0;
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = s;
+    rb[threadIdx.x >> 6] = wb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (rb[0] | rb[1] | rb[2] | rb[3]) atomicMax((int*)(state + 1), 1);
+  }
+}
+
+__global__ __launch_bounds__(1024) void sum_partials_k(const float* __restrict__ partials, int n,
+                                                       float* __restrict__ state) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 1024) s += partials[i];  // fixed stride order
+  __shared__ float red[16];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += red[w];
+    state[0] += t;
+  }
+}
+
+extern "C" int sdp_grad_sumsq_parts(float* const* grads, const int64_t* sizes, const void* blocks, int nblocks,
+                                    float* partials, float* state, void* stream) {
+  if (!grads || !sizes || !blocks || !partials || !state || nblocks < 0) return (int)hipErrorInvalidValue;
+  if (nblocks == 0) return 0;
+  hipLaunchKernelGGL(sumsq_parts_k, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, grads, sizes,
+                     (const MTBlock*)blocks, partials, state);
+  return SDP_CHECK_LAUNCH();
+}
+
+extern "C" int sdp_sum_partials(const float* partials, int n, float* state, void* stream) {
+  if (!partials || !state || n < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sum_partials_k, dim3(1), dim3(1024), 0, (hipStream_t)stream, partials, n, state);
+  return SDP_CHECK_LAUNCH();
+}
+
 __global__ __launch_bounds__(256) void adamw_k(float* const* __restrict__ params, float* const* __restrict__ grads,
                                                float* const* __restrict__ m1, float* const* __restrict__ m2,
                                                const int64_t* __restrict__ sizes, const MTBlock* __restrict__ blocks,

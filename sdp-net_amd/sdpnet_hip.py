@@ -99,6 +99,8 @@ _SIGS = {
     "sdp_adamw_dev": ([_vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _f32, _f32,
                        _vp], _i32),
     "sdp_adamw_finish": ([_vp, _vp, _f32, _f32, _i32, _vp, _i32, _vp], _i32),
+    "sdp_grad_sumsq_parts": ([_vp, _vp, _vp, _i32, _vp, _vp, _vp], _i32),
+    "sdp_sum_partials": ([_vp, _i32, _vp, _vp], _i32),
 }
 
 _lib = None

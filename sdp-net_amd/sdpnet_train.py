@@ -752,6 +752,8 @@ class AdamW(torch.optim.Optimizer):
             self._tables.append(dict(params=ps, blocks=btab, nblocks=len(blocks), sizes=sizes, pp=ptrs(ps),
                                      m1=ptrs([self.state[p]["exp_avg"] for p in ps]),
                                      m2=ptrs([self.state[p]["exp_avg_sq"] for p in ps]), steps=steps))
+        nb = sum(t["nblocks"] for t in self._tables)
+        self._partials = torch.zeros(max(1, nb), dtype=torch.float32, device=dev)
         self._ensure_device_state(dev)
         self._sig = self._signature()
 
@@ -778,11 +780,16 @@ class AdamW(torch.optim.Optimizer):
         stream = torch.cuda.current_stream(dev).cuda_stream
         L = sp.lib()
         gptr = []
-        for tab in self._tables:
+        off = 0
+        for tab in self._tables:  # per-block sums of squares, then one fixed-order sum (bit-reproducible)
             g = torch.tensor([p.grad.data_ptr() for p in tab["params"]], dtype=torch.int64, device=dev)
             gptr.append(g)
-            sp._check(L.sdp_grad_sumsq(g.data_ptr(), tab["sizes"].data_ptr(), tab["blocks"].data_ptr(),
-                                       tab["nblocks"], self.state_buf.data_ptr(), stream), "grad_sumsq")
+            sp._check(L.sdp_grad_sumsq_parts(g.data_ptr(), tab["sizes"].data_ptr(), tab["blocks"].data_ptr(),
+                                             tab["nblocks"], self._partials.data_ptr() + 4 * off,
+                                             self.state_buf.data_ptr(), stream), "grad_sumsq")
+            off += tab["nblocks"]
+        sp._check(L.sdp_sum_partials(self._partials.data_ptr(), off, self.state_buf.data_ptr(), stream),
+                  "sum_partials")
         dscale = self.scaler.data_ptr() if grad_scale is None else None
         inv = 1.0 if grad_scale is None else 1.0 / float(grad_scale)
         for tab, g, group in zip(self._tables, gptr, self.param_groups):

@@ -321,6 +321,95 @@ def test_full_size_row_counts_against_oracle():
     assert worst[0] <= 1e-4, worst
 
 
+XL_TRAIN_CFG = dict(embedding_dim=768, num_blocks=2, n_head=8, conv_kernel_size=7, patch_size=14,
+                    max_image_size=[16, 16], max_num_registers=5, head_output_from_register=True, conv_first=True,
+                    normalize_qv=True, ffn_dropout=0.0, attn_dropout=0.0, stochastic_depth_p=[0.0, 0.0],
+                    output_classes=1000, activation="gelu")
+
+
+@pytest.mark.gpu
+def test_xl_architecture_training_step_against_oracle():
+    """BASELINE.json configs[4]'s architecture (training_tools.py:77-103): SdP-Net-XL's block
+    dimensions -- d 768, 8 heads of 96, patch 14, 256 patches + 4 registers = 260 tokens -- with
+    2 blocks to keep the CPU side cheap, batch 2.  fp32: every HIP gradient within 1e-4 (relative)
+    of autograd through the oracle (pinned by the train fixtures); the fused AdamW step equals
+    torch.optim.AdamW + clip_grad_norm_ on the same gradients.  bf16 (autocast): each gradient's
+    error within 2x the oracle's own CPU-autocast error + 6e-2 (the fixture rule)."""
+    import model as ours
+    import sdpnet_train
+    cfg = XL_TRAIN_CFG
+    torch.manual_seed(0)
+    m = ours.MainModel.from_dict(**cfg)
+    sd = synth.synth_state_dict(m, 21)
+    m.load_state_dict(sd)
+    x = synth.synth_images(9, 2, 224)
+    y = torch.tensor([3, 917])
+    osd = {k: v.clone().requires_grad_(v.is_floating_point()) for k, v in sd.items()}
+    F.cross_entropy(orc.forward.__wrapped__(x, osd, cfg), y, label_smoothing=0.1).backward()
+    ref = {k: osd[k].grad.numpy() for k, _ in m.named_parameters()}
+    asd = {k: v.clone().requires_grad_(v.is_floating_point()) for k, v in sd.items()}
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        lac = F.cross_entropy(orc.forward.__wrapped__(x, asd, cfg), y, label_smoothing=0.1)
+    lac.backward()
+    fl = 1e-3 * max(float(np.abs(g).max()) for g in ref.values())
+    m = m.to(DEV).train()
+    for bf16 in (False, True):
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+            loss = sdpnet_train.cross_entropy(m(x.to(DEV)), y.to(DEV), 0.1)
+        loss.backward()
+        worst = []
+        for k, p in m.named_parameters():
+            r = _rel(p.grad.cpu().numpy(), ref[k], fl)
+            rac = _rel(asd[k].grad.float().numpy(), ref[k], fl)
+            tol = (2 * rac + 6e-2) if bf16 else 1e-4
+            worst.append((r / tol, r, rac, k))
+        worst.sort(reverse=True)
+        print(f"XL-dim training bf16={bf16}: worst", [(k, f"{r:.2e}", f"{rac:.2e}") for _, r, rac, k in worst[:3]])
+        assert worst[0][0] <= 1.0, worst[:3]
+    # fused AdamW (+ clip) vs torch.optim.AdamW on the same (bf16-path) gradients
+    params = [p for p in m.parameters()]
+    ref_p = [p.detach().clone().requires_grad_(True) for p in params]
+    for rp, p in zip(ref_p, params):
+        rp.grad = p.grad.detach().clone()
+    torch.nn.utils.clip_grad_norm_(ref_p, 5.0)
+    torch.optim.AdamW(ref_p, lr=0.0015, weight_decay=0.05).step()
+    sdpnet_train.AdamW(params, lr=0.0015, weight_decay=0.05).step(grad_scale=1.0, max_norm=5.0)
+    torch.cuda.synchronize()
+    err = max(float((rp - p).abs().max()) for rp, p in zip(ref_p, params))
+    assert err <= 1e-5, err
+
+
+@pytest.mark.gpu
+def test_xl_full_size_training_step_is_deterministic():
+    """The benchmarked XL training step at its full per-GPU batch (120 images, configs[4]):
+    two runs from the same seeds give bit-identical parameters after one fused step (dropout
+    masks from the counter hash, split-K reductions and the gradient norm in a fixed order),
+    and every gradient is finite."""
+    import model as ours
+    import sdpnet_train
+    cfg = dict(XL_TRAIN_CFG, num_blocks=17, ffn_dropout=0.2, attn_dropout=0.2)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(120, 3, 224, 224, generator=g).to(DEV)
+    y = torch.randint(0, 1000, (120,), generator=g).to(DEV)
+    outs = []
+    for _ in range(2):
+        torch.manual_seed(231424314)
+        m = ours.MainModel.from_dict(**cfg).to(DEV).train()
+        opt = sdpnet_train.AdamW(m.parameters(), lr=0.0015, weight_decay=0.05)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = sdpnet_train.cross_entropy(m(x), y, 0.1)
+        opt.scale(loss).backward()
+        assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+        opt.step(grad_scale=None, max_norm=5.0)
+        torch.cuda.synchronize()
+        assert float(opt._steps[0]) == 1.0  # the step was taken (no inf / nan)
+        outs.append(torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu())
+        del m, opt
+        torch.cuda.empty_cache()
+    assert torch.equal(outs[0], outs[1])
+
+
 class _OracleModule(torch.nn.Module):
     """The oracle forward (reference math, stock torch CPU ops) as a module whose parameters
     DDP can hook (CPU gloo test of the data-parallel gradient average)."""
