@@ -154,6 +154,15 @@ class MainModel(SdPModel):
         if self.training:
             # training_tools.py:77-103: the train-mode forward with dropout / drop path, whose
             # backward runs on the HIP kernels too (sdpnet_train.py)
+            if torch.compiler.is_compiling():
+                # torch.compile of a training model (cifar100_test.py:93, training_tools.py:39):
+                # one opaque op pair (sdpnet_ops.train_forward / train_backward)
+                if return_raw_outputs:
+                    raise NotImplementedError("sdpnet training path returns logits only")
+                code = sdpnet_ops.DTYPE_CODES[compute_dtype(x, self)]
+                params = [p for p in self.parameters()]
+                logits, _ = torch.ops.sdpnet.train_forward(x, params, self._sdp_handle, num_registers, code)
+                return logits
             import sdpnet_train
             return sdpnet_train.train_forward(self, x, num_registers, return_raw_outputs)
         if torch.compiler.is_compiling():

@@ -26,6 +26,7 @@ import torch
 from torch import Tensor
 
 from sdpnet_engine import num_reg_rows
+from typing import List
 
 _MODELS: "dict[int, weakref.ref]" = {}
 _NEXT = itertools.count(1)
@@ -87,3 +88,72 @@ def _main_forward_raw_fake(x, handle, num_registers, dtype_code):
     dt = _DTYPES[dtype_code]
     return (x.new_empty((B, ncls), dtype=dt), x.new_empty((B, C, Hp, Wp), dtype=dt),
             x.new_empty((B, R, C), dtype=dt))
+
+
+# ---------------------------------------------------------------------------
+# Training mode under torch.compile (cifar100_test.py:93 fullgraph=True, dynamic=True;
+# training_tools.py:38-39): the whole train-mode forward is ONE opaque op whose autograd
+# formula is a second opaque op, so Dynamo traces model(x) -> loss.backward() with 0 graph
+# breaks and AOTAutograd never looks inside.
+#
+#   sdpnet::train_forward(x, params, handle, num_registers, dtype_code) -> (logits, key)
+#   sdpnet::train_backward(grad_logits, key, params, handle) -> grads (one per param)
+#
+# The forward runs sdpnet_train.tape_forward (the eager path's own sub-layer Functions,
+# called directly) and parks the tape in _TAPES under ``key``, a 1-element tensor that is
+# also a saved tensor of the autograd node: backward finds the tape by key.data_ptr() (no
+# host sync) and frees it; a tape whose key dies without a backward is dropped with it.
+# ---------------------------------------------------------------------------
+_TAPES: "dict[int, list]" = {}
+
+
+def _drop_tape(k: int):
+    _TAPES.pop(k, None)
+
+
+@torch.library.custom_op("sdpnet::train_forward", mutates_args=(), device_types="cuda")
+def train_forward(x: Tensor, params: List[Tensor], handle: int, num_registers: int,
+                  dtype_code: int) -> Tuple[Tensor, Tensor]:
+    import sdpnet_train
+    model = lookup(handle)
+    logits, tape = sdpnet_train.tape_forward(model, x, num_registers, _DTYPES[dtype_code])
+    key = torch.empty(1, dtype=torch.int64, device=x.device)
+    _TAPES[key.data_ptr()] = tape
+    weakref.finalize(key, _drop_tape, key.data_ptr())
+    return logits, key
+
+
+@train_forward.register_fake
+def _train_forward_fake(x, params, handle, num_registers, dtype_code):
+    B, C, Hp, Wp, ncls, R = _shapes(lookup(handle), x, num_registers)
+    return x.new_empty((B, ncls), dtype=_DTYPES[dtype_code]), x.new_empty((1,), dtype=torch.int64)
+
+
+@torch.library.custom_op("sdpnet::train_backward", mutates_args=(), device_types="cuda")
+def train_backward(grad_logits: Tensor, key: Tensor, params: List[Tensor], handle: int) -> List[Tensor]:
+    import sdpnet_train
+    tape = _TAPES.pop(key.data_ptr(), None)
+    if tape is None:
+        raise RuntimeError("sdpnet: no saved training forward for this backward (backward run twice?)")
+    return sdpnet_train.tape_backward(tape, grad_logits.contiguous(), params)
+
+
+@train_backward.register_fake
+def _train_backward_fake(grad_logits, key, params, handle):
+    return [torch.empty_like(p) for p in params]
+
+
+def _train_setup_context(ctx, inputs, output):
+    x, params, handle, num_registers, dtype_code = inputs
+    ctx.save_for_backward(output[1], *params)
+    ctx.handle = handle
+    ctx.nparams = len(params)
+
+
+def _train_backward_formula(ctx, grad_logits, grad_key):
+    key, *params = ctx.saved_tensors
+    grads = torch.ops.sdpnet.train_backward(grad_logits, key, params, ctx.handle)
+    return None, list(grads), None, None, None
+
+
+train_forward.register_autograd(_train_backward_formula, setup_context=_train_setup_context)

@@ -619,6 +619,88 @@ def train_forward(model, x: torch.Tensor, num_registers: int = 3, return_raw_out
 
 
 # ---------------------------------------------------------------------------
+# The same training forward / backward as an explicit tape (torch.compile path)
+# ---------------------------------------------------------------------------
+class _Ctx:
+    """Stand-in for an autograd ctx: the Functions above keep their state in plain attributes."""
+
+
+def tape_forward(model, x: torch.Tensor, num_registers: int, dt):
+    """train_forward with every sub-layer Function's forward called directly and its ctx
+    kept on a tape (no autograd graph), for the opaque torch.compile custom op
+    (sdpnet_ops.train_forward).  Same kernels, same order, same RNG draws as train_forward,
+    so a compiled step is bit-identical to an eager one."""
+    B, _, Hi, Wi = x.shape
+    p = model.conv_init.patch_size
+    Hp, Wp = Hi // p, Wi // p
+    emb = model.embedding_layer
+    conv_emb = not hasattr(emb, "horizontal_embedding_layer")
+    if conv_emb:
+        R = num_reg_rows(emb.register.shape[0], num_registers)
+        eh = ew = None
+    else:
+        R = num_reg_rows(emb.max_num_registers, num_registers)
+        eh, ew = emb.horizontal_embedding_layer.weight, emb.vertical_embedding_layer.weight
+        if Hp > eh.shape[0] or Wp > ew.shape[0]:
+            raise RuntimeError(f"image grid {Hp}x{Wp} exceeds max_image_size {[ew.shape[0], eh.shape[0]]}")
+    N = R + Hp * Wp
+    C = model.conv_init.conv.out_channels
+    rng = _RNG()
+    tape = []
+
+    def run(fn, lead, params, *args):
+        ctx = _Ctx()
+        out = fn.forward(ctx, *args, *params)
+        tape.append((fn, ctx, lead, params))
+        return out
+
+    xin = x if x.dtype == dt else as_dtype(x, dt)
+    with torch.no_grad():
+        tok = run(_EmbedFn, 4, [model.conv_init.conv.weight, eh, ew, emb.register_embedding_layer.weight],
+                  xin, (B, R, Hp, Wp, num_registers), model, dt)
+
+        def enc(t, e):
+            return run(_EncoderFn, 5, _enc_params(e), t, (B, N), e, dt, rng)
+
+        def mixers(t, blk):
+            for mx in blk.conv_blocks:
+                t = run(_MixerFn, 4, _mixer_params(mx), t, (B, R, Hp, Wp), mx, dt)
+            return t
+
+        for blk in model.blocks:
+            if blk.conv_first:
+                tok = enc(mixers(tok, blk), blk.t_block)
+            else:
+                tok = mixers(enc(tok, blk.t_block), blk)
+        tok = enc(tok, model.final_block.t_block)
+        head = model.output_head
+        logits = run(_HeadFn, 5, _head_params(head), tok, (B, R, Hp * Wp, N, C), head, dt, rng)
+    return logits, tape
+
+
+def tape_backward(tape, dlogits: torch.Tensor, params: List[torch.Tensor]) -> List[torch.Tensor]:
+    """Replay the tape backwards; returns one fp32 gradient per entry of ``params`` (zeros for
+    a parameter the forward did not use)."""
+    grads = {}
+    g = dlogits
+    with torch.no_grad():
+        for fn, ctx, lead, ps in reversed(tape):
+            outs = fn.backward(ctx, g)
+            g = outs[0]
+            for prm, gp in zip(ps, outs[lead:]):
+                if prm is not None and gp is not None:
+                    grads[id(prm)] = gp if id(prm) not in grads else grads[id(prm)] + gp
+    tape.clear()
+    out = []
+    for q in params:
+        t = grads[id(q)].reshape(q.shape).to(q.dtype) if id(q) in grads else torch.zeros_like(q)
+        if t._base is not None:  # e.g. the q/k/v slices of one fused dW: the op's outputs may not alias
+            t = t.clone()
+        out.append(t)
+    return out
+
+
+# ---------------------------------------------------------------------------
 # Loss and optimizer
 # ---------------------------------------------------------------------------
 class _CEFn(torch.autograd.Function):

@@ -121,3 +121,53 @@ def test_compiled_equals_eager_on_gpu():
     y_raw = cm(x.bfloat16(), return_raw_outputs=True)
     for a, b in zip(y_raw, ref_raw):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+# --------------------------------------------------------------- training mode under compile
+def test_train_mode_fullgraph_single_op_pair():
+    """model.train() under torch.compile (cifar100_test.py:93 fullgraph=True, training_tools.py:39
+    dynamic=True): the forward is one sdpnet::train_forward op taking the parameters, so
+    Dynamo sees no graph break; its autograd formula is the sdpnet::train_backward op."""
+    m = _model(ffn_dropout=0.2, attn_dropout=0.2).train()
+    with FakeTensorMode(allow_non_fake_inputs=True):
+        x = torch.empty(2, 3, 224, 224, device="cuda")
+        gm = _export(m, x)
+    nodes = _sdp_nodes(gm)
+    assert len(nodes) == 2 or len(nodes) == 1  # the op (+ its getitem when exported)
+    assert any("train_forward" in str(n.target) for n in nodes)
+    assert "train_backward" in str(torch.ops.sdpnet.train_backward)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bf16", [False, True])
+def test_compiled_train_step_equals_eager_on_gpu(bf16):
+    """A compiled training step (fullgraph=True, dynamic=True; loss outside the model as in
+    cifar100_test.py:136-140) gives the eager step's loss and every gradient bit for bit,
+    dropout and drop path active (same seeds -> same masks)."""
+    import torch.nn.functional as F
+    torch.manual_seed(0)
+    m = _model(ffn_dropout=0.2, attn_dropout=0.2, stochastic_depth_p=[0.1, 0.2]).to("cuda").train()
+    x = torch.randn(4, 3, 224, 224, device="cuda")
+    y = torch.randint(0, 10, (4,), device="cuda")
+
+    def step(mod):
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(7)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+            out = mod(x)
+        loss = F.cross_entropy(out.float(), y, label_smoothing=0.1)
+        loss.backward()
+        return loss.detach(), {k: (p.grad.clone() if p.grad is not None else torch.zeros_like(p))
+                               for k, p in m.named_parameters()}
+
+    l_eager, g_eager = step(m)
+    torch._dynamo.reset()
+    cm = torch.compile(m, fullgraph=True, dynamic=True)
+    l_c, g_c = step(cm)
+    l_c2, g_c2 = step(cm)  # a second compiled step reuses the graph and the tape registry
+    assert torch.equal(l_eager, l_c) and torch.equal(l_c, l_c2)
+    for k in g_eager:
+        assert torch.equal(g_eager[k], g_c[k]), k
+        assert torch.equal(g_c[k], g_c2[k]), k
+    import sdpnet_ops
+    assert not sdpnet_ops._TAPES  # every tape was consumed by its backward
