@@ -440,8 +440,7 @@ class _EmbedFn(torch.autograd.Function):
         p = pat.patch_size
         P, N = Hp * Wp, R + Hp * Wp
         dev = x.device
-        if act_code(emb.activation) != 0:
-            raise NotImplementedError("sdpnet training path: embedding_activation must be 'none'")
+        act = act_code(emb.activation)  # layers.py:168 / :209: activation(x + pos) on the image rows
         kp = pat._kpad()
         patches = _empty((B * P, kp), dt, dev)
         sp.patchify(x.contiguous(), patches, p, kp)
@@ -458,12 +457,18 @@ class _EmbedFn(torch.autograd.Function):
             sp.pos_table(f32(eh), f32(ew), pos, Hp, Wp, C)
         posd = pos if dt == torch.float32 else as_dtype(pos, dt)
         tok = _empty((B * N, C), dt, dev)
-        sp.gemm(_dense(patches), w, Rows(tok, C, P, N, R), B * P, C, kp, resid=Rows(posd, C, P, 0, 0),
-                resid_pre=True)
+        z = None
+        if act == 0:
+            sp.gemm(_dense(patches), w, Rows(tok, C, P, N, R), B * P, C, kp, resid=Rows(posd, C, P, 0, 0),
+                    resid_pre=True)
+        else:  # keep the pre-activation for the backward
+            z = _empty((B * P, C), dt, dev)
+            sp.gemm(_dense(patches), w, _dense(z), B * P, C, kp, resid=Rows(posd, C, P, 0, 0), resid_pre=True)
+            sp.rowscale_add(_dense(z), Rows(tok, C, P, N, R), B * P, C, act=act)
         table, R2 = emb._register_rows(nreg_arg)
         if R:
             sp.copy_rows(table.contiguous(), C, 0, tok, C, N * C, B, R, C)
-        ctx.st = dict(patches=patches, geo=(B, R, Hp, Wp, C, P, N, p, kp), dt=dt, conv_emb=conv_emb,
+        ctx.st = dict(patches=patches, geo=(B, R, Hp, Wp, C, P, N, p, kp), dt=dt, conv_emb=conv_emb, act=act, z=z,
                       nrow_eh=None if conv_emb else eh.shape[0], nrow_ew=None if conv_emb else ew.shape[0],
                       nreg=ereg.shape[0], wshape=wp.shape)
         return tok
@@ -476,11 +481,13 @@ class _EmbedFn(torch.autograd.Function):
         dtok = dtok.contiguous().to(dt)
         dev = dtok.device
         dimg = _dense_copy(Rows(dtok, C, P, N, R), B * P, C, dt)
+        if S["act"]:  # through the embedding activation: dz = act'(z) * d
+            sp.act_bwd(S["z"], dimg, dimg, B * P, C, S["act"])
         gw = _wgrad(dimg, S["patches"])[:, : 3 * p * p].contiguous().view(S["wshape"])
         geh = gew = None
         if not S["conv_emb"]:
             dpos = _empty((P, C), torch.float32, dev)
-            sp.seg_colsum(dtok, dpos, P, B, 1, N, C, x_off=R * C)         # sum over the batch
+            sp.seg_colsum(dimg, dpos, P, B, 1, P, C)                       # sum over the batch
             geh = torch.zeros(S["nrow_eh"], C, dtype=torch.float32, device=dev)
             gew = torch.zeros(S["nrow_ew"], C, dtype=torch.float32, device=dev)
             sp.seg_colsum(dpos, geh, Hp, Wp, Wp, 1, C)                      # Eh indexed by h (rows)
@@ -575,10 +582,37 @@ def _head_params(head) -> List[Optional[nn.Parameter]]:
 
 
 # ---------------------------------------------------------------------------
+class _RawOutFn(torch.autograd.Function):
+    """(x_raw_output [B, C, H, W], registers [B, R, C]) views of the final token buffer
+    (model.py:147-148: return_raw_outputs); their gradients flow back into the token rows."""
+
+    @staticmethod
+    def forward(ctx, tok, geo):
+        B, R, Hp, Wp, C = geo
+        N = R + Hp * Wp
+        xo = _empty((B, C, Hp, Wp), tok.dtype, tok.device)
+        sp.rows_to_nchw(Rows(tok, C, Hp * Wp, N, R), xo)
+        regs = _empty((B, R, C), tok.dtype, tok.device)
+        if R:
+            sp.copy_rows(tok, C, N * C, regs, C, R * C, B, R, C)
+        ctx.geo = geo
+        return xo, regs
+
+    @staticmethod
+    def backward(ctx, dxo, dregs):
+        B, R, Hp, Wp, C = ctx.geo
+        N = R + Hp * Wp
+        dt = dxo.dtype if dxo is not None else dregs.dtype
+        dtok = torch.zeros(B * N, C, dtype=dt, device=(dxo if dxo is not None else dregs).device)
+        if dxo is not None:
+            sp.nchw_to_rows(dxo.contiguous(), Rows(dtok, C, Hp * Wp, N, R))
+        if dregs is not None and R:
+            sp.copy_rows(dregs.contiguous().to(dt), C, R * C, dtok, C, N * C, B, R, C)
+        return dtok, None
+
+
 def train_forward(model, x: torch.Tensor, num_registers: int = 3, return_raw_outputs: bool = False):
     """MainModel.forward in training mode (model.py:129-149 with dropout / drop path active)."""
-    if return_raw_outputs:
-        raise NotImplementedError("sdpnet training path returns logits only (return_raw_outputs is eval-only)")
     dt = compute_dtype(x, model)
     B, _, Hi, Wi = x.shape
     p = model.conv_init.patch_size
@@ -615,7 +649,11 @@ def train_forward(model, x: torch.Tensor, num_registers: int = 3, return_raw_out
             tok = mixers(enc(tok, blk.t_block), blk)
     tok = enc(tok, model.final_block.t_block)                          # model.py:143
     head = model.output_head
-    return _HeadFn.apply(tok, (B, R, Hp * Wp, N, C), head, dt, rng, *_head_params(head))
+    logits = _HeadFn.apply(tok, (B, R, Hp * Wp, N, C), head, dt, rng, *_head_params(head))
+    if not return_raw_outputs:
+        return logits
+    xo, regs = _RawOutFn.apply(tok, (B, R, Hp, Wp, C))
+    return logits, xo, regs
 
 
 # ---------------------------------------------------------------------------

@@ -321,6 +321,41 @@ def test_full_size_row_counts_against_oracle():
     assert worst[0] <= 1e-4, worst
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("conv_emb", [False, True])
+def test_train_mode_embedding_activation_and_raw_outputs(conv_emb):
+    """Train-mode surface the reference computes (layers.py:157-168 / :205, model.py:147-148):
+    an embedding activation (GELU on x + pos) and return_raw_outputs=True, whose outputs carry
+    gradients back into the model.  fp32 gradients vs autograd through the oracle."""
+    import model as ours
+    import sdpnet_train
+    cfg = dict(embedding_dim=64, num_blocks=1, n_head=4, conv_kernel_size=7, patch_size=16, max_image_size=[16, 16],
+               head_output_from_register=True, ffn_dropout=0.0, attn_dropout=0.0, output_classes=10,
+               embedding_activation="gelu", conv_embedding=conv_emb, conv_embedding_kernel_size=5)
+    torch.manual_seed(0)
+    m = ours.MainModel.from_dict(**cfg)
+    sd = synth.synth_state_dict(m, 31)
+    m.load_state_dict(sd)
+    x = synth.synth_images(6, 3, 224)
+    y = torch.tensor([1, 7, 3])
+
+    def objective(logits, xo, regs):  # a loss that reaches all three outputs
+        return F.cross_entropy(logits, y.to(logits.device), label_smoothing=0.1) + (xo.float() ** 2).mean() \
+            + 0.5 * regs.float().abs().mean()
+
+    osd = {k: v.clone().requires_grad_(v.is_floating_point()) for k, v in sd.items()}
+    lo, xo, ro = orc.forward.__wrapped__(x, osd, cfg, return_raw_outputs=True)
+    objective(lo, xo, ro).backward()
+    m = m.to(DEV).train()
+    lg, xg, rg = m(x.to(DEV), return_raw_outputs=True)
+    assert xg.shape == xo.shape and rg.shape == ro.shape
+    assert float((xg.cpu() - xo.detach()).abs().max()) <= 1e-4
+    objective(lg, xg, rg).backward()
+    fl = 1e-3 * max(float(osd[k].grad.abs().max()) for k, _ in m.named_parameters())
+    worst = max((_rel(p.grad.cpu().numpy(), osd[k].grad.numpy(), fl), k) for k, p in m.named_parameters())
+    assert worst[0] <= 1e-4, worst
+
+
 XL_TRAIN_CFG = dict(embedding_dim=768, num_blocks=2, n_head=8, conv_kernel_size=7, patch_size=14,
                     max_image_size=[16, 16], max_num_registers=5, head_output_from_register=True, conv_first=True,
                     normalize_qv=True, ffn_dropout=0.0, attn_dropout=0.0, stochastic_depth_p=[0.0, 0.0],
