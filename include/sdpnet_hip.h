@@ -405,6 +405,26 @@ int sdp_adamw_finish(float* state, float* scale_tracker, float growth, float bac
 /* Bit-reproducible gradient norm: sdp_grad_sumsq_parts writes block b's sum of squares to
  * partials[b] (and flags non-finite values in state[1]); sdp_sum_partials adds partials[0..n)
  * in a fixed order into state[0].  Same result as sdp_grad_sumsq without float atomics. */
+/*
+ * Flash-style training attention (layers.py:289-291, F.scaled_dot_product_attention with
+ * dropout_p; bf16 only, hd % 16 == 0, hd <= 128, K + V of one head <= 160 KiB of LDS).
+ * q, k, v of head h are columns h*hd, C + h*hd, 2C + h*hd of the [B*N, ldq] rows (C = H*hd).
+ *   sdp_attn_train_fwd: O = dropout(softmax(scale Q K^T)) V into [B*N, ldo] rows; lse[(b*H+h)*N+q]
+ *     = log2 sum_k exp2(scale log2(e) q.k) (fp32).  S and P are never stored.
+ *   sdp_attn_train_bwd: dQ, dK, dV (bf16 rows, head h at column h*hd of each) from dO, O, lse;
+ *     P recomputed; `delta` is caller scratch of B*H*N floats.  The dropout mask is a counter hash
+ *     of (seed, b*H + h, q, k) -- the same in both directions; sdp_attn_dropout_mask writes it as
+ *     bytes [B*H][N][N] (keep = 1) for tests.
+ *   sdp_attn_train_applies(dtype, N, hd): 1 if the shape takes these kernels.
+ */
+int sdp_attn_train_applies(int dtype, int N, int hd);
+int sdp_attn_train_fwd(int dtype, const void* qkv, int64_t ldq, void* o, int64_t ldo, float* lse, int B, int N, int H,
+                       int hd, float scale, float p, uint64_t seed, void* stream);
+int sdp_attn_train_bwd(int dtype, const void* qkv, int64_t ldq, const void* o, int64_t ldo, const void* dO,
+                       int64_t lddo, const float* lse, float* delta, void* dq, int64_t lddq, void* dk, int64_t lddk,
+                       void* dv, int64_t lddv, int B, int N, int H, int hd, float scale, float p, uint64_t seed,
+                       void* stream);
+int sdp_attn_dropout_mask(uint8_t* out, int Z, int N, float p, uint64_t seed, void* stream);
 int sdp_grad_sumsq_parts(float* const* grads, const int64_t* sizes, const void* blocks, int nblocks,
                          float* partials, float* state, void* stream);
 int sdp_sum_partials(const float* partials, int n, float* state, void* stream);

@@ -101,6 +101,11 @@ _SIGS = {
     "sdp_adamw_finish": ([_vp, _vp, _f32, _f32, _i32, _vp, _i32, _vp], _i32),
     "sdp_grad_sumsq_parts": ([_vp, _vp, _vp, _i32, _vp, _vp, _vp], _i32),
     "sdp_sum_partials": ([_vp, _i32, _vp, _vp], _i32),
+    "sdp_attn_train_applies": ([_i32, _i32, _i32], _i32),
+    "sdp_attn_train_fwd": ([_i32, _vp, _i64, _vp, _i64, _vp, _i32, _i32, _i32, _i32, _f32, _f32, _u64, _vp], _i32),
+    "sdp_attn_train_bwd": ([_i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32,
+                            _i32, _i32, _i32, _f32, _f32, _u64, _vp], _i32),
+    "sdp_attn_dropout_mask": ([_vp, _i32, _i32, _f32, _u64, _vp], _i32),
 }
 
 _lib = None
@@ -666,3 +671,45 @@ def ln_fwd(x: Rows, eps: float, gamma: torch.Tensor, beta: torch.Tensor, stats: 
     rc = lib().sdp_ln_fwd(dcode(x.t.dtype), *x.args(), float(eps), gamma.data_ptr(), beta.data_ptr(),
                           stats.data_ptr(), *y.args(), M, C, _stream(y.t))
     _check(rc, "ln_fwd")
+
+
+# ------------------------------------------------------------------ flash training attention
+def attn_train_applies(dtype: torch.dtype, N: int, hd: int) -> bool:
+    return dtype == torch.bfloat16 and bool(lib().sdp_attn_train_applies(BF16, N, hd))
+
+
+def attn_train_fwd(qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, B: int, N: int, H: int, hd: int,
+                   scale: float, p: float, seed: int):
+    """O = dropout(softmax(scale Q K^T)) V (rows of o), lse (fp32, B*H*N) = base-2 log-sum-exp."""
+    _need_cuda(qkv, o, lse)
+    _req(qkv.dtype == o.dtype == torch.bfloat16 and lse.dtype == torch.float32 and lse.numel() >= B * H * N)
+    _req(qkv.shape[0] >= B * N and o.shape[0] >= B * N and qkv.stride(1) == 1 and o.stride(1) == 1)
+    rc = lib().sdp_attn_train_fwd(BF16, qkv.data_ptr(), qkv.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(),
+                                  B, N, H, hd, float(scale), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(o))
+    _check(rc, "attn_train_fwd")
+
+
+def attn_train_bwd(qkv: torch.Tensor, o: torch.Tensor, do: torch.Tensor, lse: torch.Tensor, delta: torch.Tensor,
+                   dq: Tuple[torch.Tensor, int], dk: Tuple[torch.Tensor, int], dv: Tuple[torch.Tensor, int],
+                   B: int, N: int, H: int, hd: int, scale: float, p: float, seed: int):
+    """dQ, dK, dV into (tensor, first column) row blocks; delta: fp32 scratch of B*H*N."""
+    _need_cuda(qkv, o, do, lse, delta, dq[0], dk[0], dv[0])
+    _req(qkv.dtype == o.dtype == do.dtype == torch.bfloat16 and delta.numel() >= B * H * N)
+    for t, c in (dq, dk, dv):
+        _req(t.dtype == torch.bfloat16 and t.stride(1) == 1 and t.shape[0] >= B * N and t.shape[1] >= c + H * hd)
+    es = 2
+    rc = lib().sdp_attn_train_bwd(BF16, qkv.data_ptr(), qkv.stride(0), o.data_ptr(), o.stride(0), do.data_ptr(),
+                                  do.stride(0), lse.data_ptr(), delta.data_ptr(),
+                                  dq[0].data_ptr() + es * dq[1], dq[0].stride(0),
+                                  dk[0].data_ptr() + es * dk[1], dk[0].stride(0),
+                                  dv[0].data_ptr() + es * dv[1], dv[0].stride(0),
+                                  B, N, H, hd, float(scale), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(o))
+    _check(rc, "attn_train_bwd")
+
+
+def attn_dropout_mask(Z: int, N: int, p: float, seed: int, device) -> torch.Tensor:
+    """The training attention's dropout keep mask [Z, N, N] (uint8, 1 = kept), for tests."""
+    out = torch.empty(Z, N, N, dtype=torch.uint8, device=device)
+    _check(lib().sdp_attn_dropout_mask(out.data_ptr(), Z, N, float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(out)),
+           "attn_dropout_mask")
+    return out

@@ -291,6 +291,40 @@ def _enc_params(e) -> List[Optional[nn.Parameter]]:
             e.ff_linear2.weight, e.ff_linear2.bias]
 
 
+def _attn_materialized(qkvn, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seed):
+    """Attention with S / P materialised per (b, h) (fp32 path, and shapes the flash kernels
+    do not take): S = QK^T (fp32) -> softmax (+ dropout) -> O = Pd V."""
+    T = B * N
+    Sm = _empty((B, Hn, N, Np), torch.float32, dev)
+    sp.gemm_flex(qkvn, qkvn, Sm, N, N, hd, ta=False, tb=True, lda=3 * C, ldb=3 * C, ldc=Np, Z=Z, zdiv=Hn,
+                 sa=(N * 3 * C, hd), sb=(N * 3 * C, hd), sc=(Hn * N * Np, N * Np), b_off=C)
+    Pm = _empty((B, Hn, N, Np), dt, dev)
+    Pd = _empty((B, Hn, N, Np), dt, dev) if p_att > 0 else Pm
+    sp.softmax_fwd(Sm.view(-1, Np), Pm.view(-1, Np), Pd.view(-1, Np) if p_att > 0 else None, Z * N, N, Np,
+                   1.0 / math.sqrt(hd), p_att, seed)
+    del Sm
+    o = _empty((T, C), dt, dev)
+    sp.gemm_flex(Pd, qkvn, o, N, hd, N, ta=False, tb=False, lda=Np, ldb=3 * C, ldc=C, Z=Z, zdiv=Hn,
+                 sa=(Hn * N * Np, N * Np), sb=(N * 3 * C, hd), sc=(N * C, hd), b_off=2 * C)
+    return o, None, Pm, Pd
+
+
+def _attn_materialized_bwd(qkvn, Pm, Pd, do, dqkv, dqk, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seed):
+    dPd = _empty((B, Hn, N, Np), dt, dev)
+    sp.gemm_flex(do, qkvn, dPd, N, N, hd, ta=False, tb=True, lda=C, ldb=3 * C, ldc=Np, Z=Z, zdiv=Hn,
+                 sa=(N * C, hd), sb=(N * 3 * C, hd), sc=(Hn * N * Np, N * Np), b_off=2 * C)
+    sp.gemm_flex(Pd, do, dqkv, N, hd, N, ta=True, tb=False, lda=Np, ldb=C, ldc=3 * C, Z=Z, zdiv=Hn,
+                 sa=(Hn * N * Np, N * Np), sb=(N * C, hd), sc=(N * 3 * C, hd), c_off=2 * C)      # dV
+    dS = _empty((B, Hn, N, Np), dt, dev)
+    sp.softmax_bwd(Pm.view(-1, Np), dPd.view(-1, Np), dS.view(-1, Np), Z * N, N, Np, p_att, seed)
+    del dPd
+    scale = 1.0 / math.sqrt(hd)
+    sp.gemm_flex(dS, qkvn, dqk, N, hd, N, ta=False, tb=False, lda=Np, ldb=3 * C, ldc=3 * C, Z=Z, zdiv=Hn,
+                 sa=(Hn * N * Np, N * Np), sb=(N * 3 * C, hd), sc=(N * 3 * C, hd), b_off=C, alpha=scale)   # dQ
+    sp.gemm_flex(dS, qkvn, dqk, N, hd, N, ta=True, tb=False, lda=Np, ldb=3 * C, ldc=3 * C, Z=Z, zdiv=Hn,
+                 sa=(Hn * N * Np, N * Np), sb=(N * 3 * C, hd), sc=(N * 3 * C, hd), c_off=C, alpha=scale)   # dK
+
+
 class _EncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, tok, geo, e, dt, rng, *params):
@@ -332,17 +366,14 @@ class _EncoderFn(torch.autograd.Function):
         # attention (:289-298): S = QK^T, P = softmax(S / sqrt(hd)), Pd = dropout(P), O = Pd V
         Np = (N + 7) // 8 * 8
         Z = B * Hn
-        Sm = _empty((B, Hn, N, Np), torch.float32, dev)
-        sp.gemm_flex(qkvn, qkvn, Sm, N, N, hd, ta=False, tb=True, lda=3 * C, ldb=3 * C, ldc=Np, Z=Z, zdiv=Hn,
-                     sa=(N * 3 * C, hd), sb=(N * 3 * C, hd), sc=(Hn * N * Np, N * Np), b_off=C)
-        Pm = _empty((B, Hn, N, Np), dt, dev)
-        Pd = _empty((B, Hn, N, Np), dt, dev) if p_att > 0 else Pm
-        sp.softmax_fwd(Sm.view(-1, Np), Pm.view(-1, Np), Pd.view(-1, Np) if p_att > 0 else None, Z * N, N, Np,
-                       1.0 / math.sqrt(hd), p_att, seeds[0])
-        del Sm
-        o = _empty((T, C), dt, dev)
-        sp.gemm_flex(Pd, qkvn, o, N, hd, N, ta=False, tb=False, lda=Np, ldb=3 * C, ldc=C, Z=Z, zdiv=Hn,
-                     sa=(Hn * N * Np, N * Np), sb=(N * 3 * C, hd), sc=(N * C, hd), b_off=2 * C)
+        if sp.attn_train_applies(dt, N, hd):  # flash form: saves O and the row LSE only
+            o = _empty((T, C), dt, dev)
+            lse = _empty((Z * N,), torch.float32, dev)
+            sp.attn_train_fwd(qkvn, o, lse, B, N, Hn, hd, 1.0 / math.sqrt(hd), p_att, seeds[0])
+            Pm = Pd = None
+        else:
+            o, lse, Pm, Pd = _attn_materialized(qkvn, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seeds[0])
+
         # x = x + drop_path1(dropout(o_proj(o)))                       (:300-303)
         zo = _linear(o, W_["wo"], None, dt)
         if p_ff > 0:
@@ -361,7 +392,7 @@ class _EncoderFn(torch.autograd.Function):
             sp.act_fwd(z2, z2, T, C, 0, p_ff, seeds[3])
         out = _empty((T, C), dt, dev)
         sp.rowscale_add(_dense(z2), _dense(out), T, C, scale=dp2, sgrp=N, resid=_dense(t2))
-        ctx.st = dict(tok=tok, a1=a1, s1=s1, qkv=qkv, qkvn=qkvn, sq=sq, sk=sk, P=Pm, Pd=Pd, o=o, t2=t2, a2=a2, s2=s2,
+        ctx.st = dict(tok=tok, a1=a1, s1=s1, qkv=qkv, qkvn=qkvn, sq=sq, sk=sk, P=Pm, Pd=Pd, lse=lse, o=o, t2=t2, a2=a2, s2=s2,
                       z1=z1, h=h, W=W_, seeds=seeds, dp1=dp1, dp2=dp2, geo=(B, N, C, Hn, hd, Np), act=act, dt=dt,
                       p_ff=p_ff, p_att=p_att, qn=qn)
         ctx.has = [p is not None for p in params]
@@ -394,21 +425,14 @@ class _EncoderFn(torch.autograd.Function):
         gwo = _wgrad(dzo, S["o"])
         qkvn, Pm, Pd = S["qkvn"], S["P"], S["Pd"]
         dqkv = _empty((T, 3 * C), dt, dev)
-        dPd = _empty((B, Hn, N, Np), dt, dev)
-        sp.gemm_flex(do, qkvn, dPd, N, N, hd, ta=False, tb=True, lda=C, ldb=3 * C, ldc=Np, Z=Z, zdiv=Hn,
-                     sa=(N * C, hd), sb=(N * 3 * C, hd), sc=(Hn * N * Np, N * Np), b_off=2 * C)
-        sp.gemm_flex(Pd, do, dqkv, N, hd, N, ta=True, tb=False, lda=Np, ldb=C, ldc=3 * C, Z=Z, zdiv=Hn,
-                     sa=(Hn * N * Np, N * Np), sb=(N * C, hd), sc=(N * 3 * C, hd), c_off=2 * C)      # dV
-        dS = _empty((B, Hn, N, Np), dt, dev)
-        sp.softmax_bwd(Pm.view(-1, Np), dPd.view(-1, Np), dS.view(-1, Np), Z * N, N, Np, p_att, seeds[0])
-        del dPd
         scale = 1.0 / math.sqrt(hd)
         dqk = dqkv if not S["qn"] else _empty((T, 3 * C), dt, dev)
-        sp.gemm_flex(dS, qkvn, dqk, N, hd, N, ta=False, tb=False, lda=Np, ldb=3 * C, ldc=3 * C, Z=Z, zdiv=Hn,
-                     sa=(Hn * N * Np, N * Np), sb=(N * 3 * C, hd), sc=(N * 3 * C, hd), b_off=C, alpha=scale)   # dQ
-        sp.gemm_flex(dS, qkvn, dqk, N, hd, N, ta=True, tb=False, lda=Np, ldb=3 * C, ldc=3 * C, Z=Z, zdiv=Hn,
-                     sa=(Hn * N * Np, N * Np), sb=(N * 3 * C, hd), sc=(N * 3 * C, hd), c_off=C, alpha=scale)   # dK
-        del dS
+        if Pm is None:  # flash backward: P recomputed from Q, K and the saved LSE
+            delta = _empty((Z * N,), torch.float32, dev)
+            sp.attn_train_bwd(qkvn, S["o"], do, S["lse"], delta, (dqk, 0), (dqk, C), (dqkv, 2 * C), B, N, Hn, hd,
+                              scale, p_att, seeds[0])
+        else:
+            _attn_materialized_bwd(qkvn, Pm, Pd, do, dqkv, dqk, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seeds[0])
         gqg = gqb = gkg = gkb = None
         if S["qn"]:
             qkv = S["qkv"]

@@ -299,3 +299,49 @@ def test_act_rowscale_add_matches_two_passes(dtype, act, C):
     sp.rowscale_add(sp.dense(z), sp.Rows(got, C, P, N, R), B * P, C, scale=scale, sgrp=P,
                     resid=sp.Rows(tok, C, P, N, R), act=act)
     assert torch.equal(got, ref)
+
+
+# ------------------------------------------------- flash training attention (attn_train.hip)
+@pytest.mark.parametrize("B,N,H,hd", [(2, 260, 8, 96), (3, 200, 8, 96), (2, 53, 4, 16), (1, 77, 2, 64),
+                                      (1, 33, 2, 128), (2, 100, 4, 48), (1, 1, 2, 32), (2, 300, 2, 80)])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_flash_train_attention_vs_torch(B, N, H, hd, p):
+    """O, the row LSE and dQ / dK / dV of the flash training kernels against torch fp32 autograd of
+    dropout(softmax(QK^T / sqrt(hd))) V on the same bf16 inputs, with the kernels' own dropout mask
+    (sdp_attn_dropout_mask) -- layers.py:289-291.  Tolerance: bf16 operand / P rounding, 2e-2 of the
+    tensor's max |.| (O 1e-2); LSE 1e-4 relative."""
+    assert sp.attn_train_applies(BF, N, hd)
+    C = H * hd
+    T = B * N
+    qkv = rnd(T, 3 * C, seed=1, scale=1.5).to(BF)
+    do = rnd(T, C, seed=2).to(BF)
+    seed = 1234567 + N
+    o = torch.empty(T, C, dtype=BF, device=DEV)
+    lse = torch.empty(B * H * N, dtype=torch.float32, device=DEV)
+    scale = 1.0 / math.sqrt(hd)
+    sp.attn_train_fwd(qkv, o, lse, B, N, H, hd, scale, p, seed)
+    dqkv = torch.full((T, 3 * C), float("nan"), dtype=BF, device=DEV)
+    delta = torch.empty(B * H * N, dtype=torch.float32, device=DEV)
+    sp.attn_train_bwd(qkv, o, do, lse, delta, (dqkv, 0), (dqkv, C), (dqkv, 2 * C), B, N, H, hd, scale, p, seed)
+    # reference
+    x = qkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)  # [3, B, H, N, hd]
+    q, k, v = (t.clone().requires_grad_(True) for t in x)
+    s = q @ k.transpose(-1, -2) * scale
+    P = torch.softmax(s, -1)
+    mask = sp.attn_dropout_mask(B * H, N, p, seed, DEV).view(B, H, N, N).float()
+    if p > 0:
+        assert abs(float(mask.mean()) - (1 - p)) < 0.05 + 3.0 / math.sqrt(mask.numel())
+    Pd = P * mask / (1 - p)
+    ref_o = Pd @ v
+    ref_o.backward(do.float().view(B, N, H, hd).permute(0, 2, 1, 3))
+    close(o.float().view(B, N, H, hd).permute(0, 2, 1, 3), ref_o.detach(), 1e-2, "O")
+    ref_lse2 = torch.logsumexp(s.detach(), -1) / math.log(2.0)
+    close(lse.view(B, H, N), ref_lse2, 1e-4, "lse")
+    g = dqkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    close(g[2], v.grad, 2e-2, "dV")
+    # dQ / dK are judged on the gradient scale of the layer (dV's): D = rowsum(dO o O) uses the
+    # bf16-rounded O, so where the exact dS is 0 (N = 1: softmax of one key) ours is rounding noise
+    gs = max(1.0, float(v.grad.abs().max()))
+    for got, ref, what in ((g[0], q.grad, "dQ"), (g[1], k.grad, "dK")):
+        err = float((got - ref).abs().max())
+        assert err <= 2e-2 * max(gs, float(ref.abs().max())), f"{what}: {err:.3e} (scale {gs:.3e})"
