@@ -4,9 +4,8 @@
 //
 //   forward   O = dropout(P) V,  P = softmax(S),  S = Q K^T / sqrt(hd)       (per batch, head)
 //             saves O and the row log-sum-exp (base 2) -- never S or P
-//   backward  D = rowsum(dO o O)                                   (attn_delta_k)
+//   backward  dQ = scale * dS K, D = rowsum(dO o O)                (attn_bwd_q_k,  wave = query tile)
 //             dV = Pd^T dO,  dK = scale * dS^T Q                   (attn_bwd_kv_k, wave = key tile)
-//             dQ = scale * dS K                                    (attn_bwd_q_k,  wave = query tile)
 //             with P recomputed from Q, K and the saved LSE, Pd = P o M / (1 - p),
 //             dP = (dO V^T) o M / (1 - p),  dS = P o (dP - D)
 //
@@ -180,27 +179,6 @@ __global__ __launch_bounds__(640) void attn_fwd_k(const bf16_t* __restrict__ QKV
 }
 
 // ---------------------------------------------------------------------------
-// D[bh][q] = sum_d dO[q][d] O[q][d]   (one thread per (row, head))
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void attn_delta_k(const bf16_t* __restrict__ O, int64_t ldo,
-                                                    const bf16_t* __restrict__ dO, int64_t lddo,
-                                                    float* __restrict__ D, int T, int N, int H, int hd) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (int64_t)T * H) return;
-  const int row = (int)(idx / H), hh = (int)(idx - (int64_t)row * H);
-  const bf16_t* o = O + (int64_t)row * ldo + hh * hd;
-  const bf16_t* g = dO + (int64_t)row * lddo + hh * hd;
-  float s = 0.f;
-  for (int c = 0; c < hd; c += 8) {
-    const bf16x8 a = *(const bf16x8*)(o + c), d = *(const bf16x8*)(g + c);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s = fmaf(bf2f((bf16_t)a[e]), bf2f((bf16_t)d[e]), s);
-  }
-  const int b = row / N, q = row - b * N;
-  D[((int64_t)b * H + hh) * N + q] = s;
-}
-
-// ---------------------------------------------------------------------------
 // dK, dV: workgroup = (b, h, group of KTW key tiles), wave = one 32-key tile (K, V fragments of
 // its keys in registers, dK^T / dV^T accumulators); the query tiles stream through LDS.
 // ---------------------------------------------------------------------------
@@ -319,8 +297,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_k(const bf16_t* __restrict
 // ---------------------------------------------------------------------------
 template <int HDT>
 __global__ __launch_bounds__(640) void attn_bwd_q_k(const bf16_t* __restrict__ QKV, int64_t ldq,
+                                                    const bf16_t* __restrict__ O, int64_t ldo,
                                                     const bf16_t* __restrict__ dO, int64_t lddo,
-                                                    const float* __restrict__ lse, const float* __restrict__ D,
+                                                    const float* __restrict__ lse, float* __restrict__ D,
                                                     bf16_t* __restrict__ dQ, int64_t lddq, int N, int H, int hd,
                                                     float scale_log2, float scale, uint32_t thresh, float inv_keep,
                                                     uint64_t seed) {
@@ -352,7 +331,22 @@ __global__ __launch_bounds__(640) void attn_bwd_q_k(const bf16_t* __restrict__ Q
       }
     }
     const float lq = qok ? lse[(int64_t)bh * N + q] : INFINITY;
-    const float dq_ = qok ? D[(int64_t)bh * N + q] : 0.f;
+    // D = rowsum(dO o O) for this query (its two lane halves hold the two halves of every
+    // 16-wide d step); written for attn_bwd_kv_k, which runs next
+    float dq_ = 0.f;
+    if (qok) {
+      const bf16_t* orow = O + ((int64_t)b * N + q) * ldo + hh * hd;
+#pragma unroll
+      for (int s = 0; s < 2 * HDT; ++s) {
+        if (s < nds) {
+          const bf16x8 ov = *(const bf16x8*)(orow + 16 * s + 8 * hf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dq_ = fmaf(bf2f((bf16_t)ov[e]), bf2f((bf16_t)gf[s][e]), dq_);
+        }
+      }
+    }
+    dq_ += __shfl_xor(dq_, 32, 64);
+    if (qok && hf == 0) D[(int64_t)bh * N + q] = dq_;
     f32x16 acc[HDT];
 #pragma unroll
     for (int dt = 0; dt < HDT; ++dt)
@@ -459,24 +453,26 @@ static int launch_fwd(const void* qkv, int64_t ldq, void* o, int64_t ldo, float*
 }
 
 template <int HDT>
-static int launch_bwd(const void* qkv, int64_t ldq, const void* dO, int64_t lddo, const float* lse, const float* D,
-                      void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv, int B, int N, int H,
-                      int hd, float scale, uint32_t thresh, float inv_keep, uint64_t seed, hipStream_t s) {
+static int launch_bwd(const void* qkv, int64_t ldq, const void* o, int64_t ldo, const void* dO, int64_t lddo,
+                      const float* lse, float* D, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv,
+                      int64_t lddv, int B, int N, int H, int hd, float scale, uint32_t thresh, float inv_keep,
+                      uint64_t seed, hipStream_t s) {
   const int nkt = (N + 31) / 32;
-  const int groups = (nkt + 3) / 4, ktw = (nkt + groups - 1) / groups;
-  hipLaunchKernelGGL(attn_bwd_kv_k<HDT>, dim3(B * H * groups), dim3(64 * ktw), 0, s, (const bf16_t*)qkv, ldq,
-                     (const bf16_t*)dO, lddo, lse, D, (bf16_t*)dk, lddk, (bf16_t*)dv, lddv, N, H, hd, ktw, groups,
-                     scale * 1.4426950408889634f, scale, thresh, inv_keep, seed);
-  int rc = SDP_CHECK_LAUNCH();
-  if (rc) return rc;
+  // dQ (and D = rowsum(dO o O)) first: the dK / dV kernel reads D
   const size_t bytes = kv_lds_bytes(N, HDT);
   hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_q_k<HDT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)bytes);
   if (e != hipSuccess) return (int)e;
   const int waves = std::min(10, nkt);
   hipLaunchKernelGGL(attn_bwd_q_k<HDT>, dim3(B * H), dim3(64 * waves), bytes, s, (const bf16_t*)qkv, ldq,
-                     (const bf16_t*)dO, lddo, lse, D, (bf16_t*)dq, lddq, N, H, hd, scale * 1.4426950408889634f,
-                     scale, thresh, inv_keep, seed);
+                     (const bf16_t*)o, ldo, (const bf16_t*)dO, lddo, lse, D, (bf16_t*)dq, lddq, N, H, hd,
+                     scale * 1.4426950408889634f, scale, thresh, inv_keep, seed);
+  int rc = SDP_CHECK_LAUNCH();
+  if (rc) return rc;
+  const int groups = (nkt + 3) / 4, ktw = (nkt + groups - 1) / groups;
+  hipLaunchKernelGGL(attn_bwd_kv_k<HDT>, dim3(B * H * groups), dim3(64 * ktw), 0, s, (const bf16_t*)qkv, ldq,
+                     (const bf16_t*)dO, lddo, lse, (const float*)D, (bf16_t*)dk, lddk, (bf16_t*)dv, lddv, N, H, hd,
+                     ktw, groups, scale * 1.4426950408889634f, scale, thresh, inv_keep, seed);
   return SDP_CHECK_LAUNCH();
 }
 
@@ -507,13 +503,9 @@ extern "C" int sdp_attn_train_bwd(int dtype, const void* qkv, int64_t ldq, const
   float inv_keep;
   drop_params(p, &thresh, &inv_keep);
   hipStream_t s = (hipStream_t)stream;
-  const int64_t items = (int64_t)B * N * H;
-  hipLaunchKernelGGL(attn_delta_k, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, (const bf16_t*)o, ldo,
-                     (const bf16_t*)dO, lddo, delta, B * N, N, H, hd);
-  int rc = SDP_CHECK_LAUNCH();
-  if (rc) return rc;
-  SDP_HDT_DISPATCH(hd, rc = launch_bwd, qkv, ldq, dO, lddo, lse, delta, dq, lddq, dk, lddk, dv, lddv, B, N, H, hd,
-                   scale, thresh, inv_keep, seed, s);
+  int rc = 0;
+  SDP_HDT_DISPATCH(hd, rc = launch_bwd, qkv, ldq, o, ldo, dO, lddo, lse, delta, dq, lddq, dk, lddk, dv, lddv, B, N,
+                   H, hd, scale, thresh, inv_keep, seed, s);
   return rc;
 }
 
