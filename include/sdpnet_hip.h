@@ -212,6 +212,10 @@ int sdp_pos_table(const float* eh, const float* ew, float* out, int H, int W, in
 /* T[h*W + w][c] = mean_{k x k} bone[c][h+i][w+j]  (ConvEmbedding, layers.py:205). */
 int sdp_avgpool_table(const float* bone, int BH, int BW, float* out, int H, int W, int C, int k,
                       void* stream);
+/* Its adjoint (trainable bone in train mode, layers.py:189-190): dbone [C, BH, BW] fp32 from
+ * dtable [H*W, C] fp32. */
+int sdp_avgpool_table_bwd(const float* dtable, int H, int W, int C, int k, float* dbone, int BH, int BW,
+                          void* stream);
 
 /* dst[b*gstride + r*ldd + c] = src[b*sgstride + r*lds + c]; sgstride = 0 expands
  * the register table over the batch (layers.py:166, :208), otherwise it copies
@@ -329,6 +333,14 @@ int sdp_act_rowscale_add(int dtype, int act, const void* X, int64_t ldx, int x_g
                          const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp, int64_t r_gstride,
                          int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int M, int N,
                          void* stream);
+/* Mixed-dtype form of the two above (act 0 = none): X in x_dtype, R and Y in y_dtype, 16-B
+ * aligned rows and N % 8 == 0 when the dtypes differ.  The fp32 residual stream of bf16 training
+ * (training_tools.py:85 autocast keeps x + branch in fp32): y32 = act(x16) * s + r32, and the
+ * stream gradient cast into a bf16 branch, y16 = x32 * s. */
+int sdp_rowscale_add_mixed(int x_dtype, int y_dtype, int act, const void* X, int64_t ldx, int x_grp,
+                           int64_t x_gstride, int x_off, const float* scale, int sgrp, const void* R, int64_t ldr,
+                           int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
+                           int64_t y_gstride, int y_off, int M, int N, void* stream);
 
 /* LayerNorm from given statistics (stats[2m] = mean, stats[2m+1] = rstd, from sdp_rowstats):
  * Y = (X - mean) * rstd * gamma + beta; and its backward
@@ -348,6 +360,17 @@ int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstri
                const float* gamma, const void* DY, int64_t lddy, int dy_grp, int64_t dy_gstride, int dy_off,
                const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride, int a_off, void* DX, int64_t lddx,
                int dx_grp, int64_t dx_gstride, int dx_off, int M, int C, float* part, void* stream);
+/* Mixed-dtype LayerNorm (fp32 residual stream, bf16 GEMM operands; vector path only):
+ * sdp_ln_fwd_mixed reads X in x_dtype and writes Y in y_dtype; sdp_ln_bwd_mixed reads X, ADD
+ * and writes DX in x_dtype, DY in dy_dtype. */
+int sdp_ln_fwd_mixed(int x_dtype, int y_dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                     float eps, const float* gamma, const float* beta, float* stats, void* Y, int64_t ldy, int y_grp,
+                     int64_t y_gstride, int y_off, int M, int C, void* stream);
+int sdp_ln_bwd_mixed(int x_dtype, int dy_dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                     const float* stats, const float* gamma, const void* DY, int64_t lddy, int dy_grp,
+                     int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,
+                     int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride, int dx_off, int M, int C,
+                     float* part, void* stream);
 
 /* Attention rows (layers.py:289-298, SDPA dropout_p in training): P = softmax(scale * S[:, :N])
  * (S fp32), Pd = P with dropout p (may be NULL), columns [N, Npad) zeroed; backward

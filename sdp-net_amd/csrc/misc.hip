@@ -117,6 +117,33 @@ extern "C" int sdp_avgpool_table(const float* bone, int BH, int BW, float* out, 
   return SDP_CHECK_LAUNCH();
 }
 
+// Adjoint of sdp_avgpool_table (trainable bone, layers.py:189-190): dbone[c, i, j] =
+// 1/k^2 * sum of dtable[h * W + w, c] over the windows (h, w) covering (i, j); the whole
+// [C, BH, BW] gradient is written (zeros outside the used region).
+__global__ void avgpool_table_bwd_k(const float* __restrict__ dt, int H, int W, int C, int k, float* __restrict__ dbone,
+                                    int BH, int BW) {
+  const int64_t total = (int64_t)C * BH * BW;
+  const float inv = 1.0f / (float)(k * k);
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(idx % BW), i = (int)((idx / BW) % BH), c = (int)(idx / ((int64_t)BW * BH));
+    float s = 0.f;
+    for (int h = max(0, i - k + 1); h <= min(H - 1, i); ++h)
+      for (int w = max(0, j - k + 1); w <= min(W - 1, j); ++w) s += dt[((int64_t)h * W + w) * C + c];
+    dbone[idx] = s * inv;
+  }
+}
+
+extern "C" int sdp_avgpool_table_bwd(const float* dtable, int H, int W, int C, int k, float* dbone, int BH, int BW,
+                                     void* stream) {
+  if (!dtable || !dbone || H <= 0 || W <= 0 || C <= 0 || k <= 0 || H + k - 1 > BH || W + k - 1 > BW)
+    return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)C * BH * BW;
+  hipLaunchKernelGGL(avgpool_table_bwd_k, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, dtable, H, W, C, k, dbone, BH, BW);
+  return SDP_CHECK_LAUNCH();
+}
+
 template <typename TI, typename TO>
 __global__ void broadcast_rows_k(const TI* __restrict__ src, int64_t lds, int64_t sgstride, TO* __restrict__ dst,
                                  int64_t ldd, int64_t gstride, int B, int R, int C) {

@@ -519,34 +519,51 @@ __global__ __launch_bounds__(256) void act_bwd_v8(const T* __restrict__ Z, int64
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void rowscale_v8(const T* __restrict__ X, int64_t ldx, RowMap xm,
-                                                   const float* __restrict__ sc, int sgrp, const T* __restrict__ R,
-                                                   int64_t ldr, RowMap rm, T* __restrict__ Y, int64_t ldy, RowMap ym,
+// X in TX; the residual R and the output Y in TY (TX = bf16 branch, TY = fp32 residual stream
+// in the fp32-stream training mode; the reverse for a stream gradient cast into a branch).
+template <typename TX, typename TY>
+__global__ __launch_bounds__(256) void rowscale_v8(const TX* __restrict__ X, int64_t ldx, RowMap xm,
+                                                   const float* __restrict__ sc, int sgrp, const TY* __restrict__ R,
+                                                   int64_t ldr, RowMap rm, TY* __restrict__ Y, int64_t ldy, RowMap ym,
                                                    int M, int N, int act) {
   const int n8 = N >> 3;
   const int64_t total = (int64_t)M * n8;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     const int64_t m = e / n8;
     const int n = (int)(e - m * n8) * 8;
-    V8<T> x;
+    V8<TX> x;
     x.load(X + xm(m) * ldx + n);
-    if (act != ACT_NONE) {  // = sdp_act_fwd's stored output (rounded to T) without the round trip
+    if (act != ACT_NONE) {  // = sdp_act_fwd's stored output (rounded to TX) without the round trip
 #pragma unroll
-      for (int q = 0; q < 8; ++q) x.v[q] = to_f<T>(from_f<T>(apply_act(act, x.v[q])));
+      for (int q = 0; q < 8; ++q) x.v[q] = to_f<TX>(from_f<TX>(apply_act(act, x.v[q])));
     }
     const float s_ = sc ? sc[m / sgrp] : 1.0f;
+    V8<TY> y;
     if (R) {
-      V8<T> r;
-      r.load(R + rm(m) * ldr + n);
+      y.load(R + rm(m) * ldr + n);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) x.v[q] = fmaf(x.v[q], s_, r.v[q]);
+      for (int q = 0; q < 8; ++q) y.v[q] = fmaf(x.v[q], s_, y.v[q]);
     } else {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) x.v[q] *= s_;
+      for (int q = 0; q < 8; ++q) y.v[q] = x.v[q] * s_;
     }
-    x.store(Y + ym(m) * ldy + n);
+    y.store(Y + ym(m) * ldy + n);
   }
+}
+
+template <typename T>
+struct DTag {
+  using type = T;
+};
+
+// Calls f(DTag<A>{}, DTag<B>{}) for the (a, b) dtype codes (0 fp32, 1 bf16).
+template <typename F>
+static int by_dtypes(int a, int b, F&& f) {
+  if (a == 1 && b == 1) return f(DTag<bf16_t>{}, DTag<bf16_t>{});
+  if (a == 0 && b == 0) return f(DTag<float>{}, DTag<float>{});
+  if (a == 0 && b == 1) return f(DTag<float>{}, DTag<bf16_t>{});
+  if (a == 1 && b == 0) return f(DTag<bf16_t>{}, DTag<float>{});
+  return (int)hipErrorInvalidValue;
 }
 
 template <typename T>
@@ -657,10 +674,10 @@ __global__ __launch_bounds__(256) void rowscale_k(const T* __restrict__ X, int64
   }
 }
 
-static int rowscale_impl(int dtype, int act, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
-                         const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp, int64_t r_gstride,
-                         int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int M, int N,
-                         void* stream) {
+static int rowscale_impl(int xdt, int ydt, int act, const void* X, int64_t ldx, int x_grp, int64_t x_gstride,
+                         int x_off, const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp,
+                         int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off,
+                         int M, int N, void* stream) {
   if (!X || !Y || M < 0 || N < 0 || (scale && sgrp <= 0) || act < 0 || act > ACT_KELU) return (int)hipErrorInvalidValue;
   if ((int64_t)M * N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
@@ -669,21 +686,20 @@ static int rowscale_impl(int dtype, int act, const void* X, int64_t ldx, int x_g
   if (N % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && (!R || (ldr % 8 == 0 && (uintptr_t)R % 16 == 0)) &&
       (uintptr_t)X % 16 == 0 && (uintptr_t)Y % 16 == 0) {
     const int gv = ew_grid((int64_t)M * (N / 8));
-    if (dtype == 1)
-      hipLaunchKernelGGL(rowscale_v8<bf16_t>, dim3(gv), dim3(256), 0, s, (const bf16_t*)X, ldx, xm, scale, sgrp,
-                         (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, M, N, act);
-    else if (dtype == 0)
-      hipLaunchKernelGGL(rowscale_v8<float>, dim3(gv), dim3(256), 0, s, (const float*)X, ldx, xm, scale, sgrp,
-                         (const float*)R, ldr, rm, (float*)Y, ldy, ym, M, N, act);
-    else
-      return (int)hipErrorInvalidValue;
-    return SDP_CHECK_LAUNCH();
+    return by_dtypes(xdt, ydt, [&](auto tx, auto ty) {
+      using TX = typename decltype(tx)::type;
+      using TY = typename decltype(ty)::type;
+      hipLaunchKernelGGL((rowscale_v8<TX, TY>), dim3(gv), dim3(256), 0, s, (const TX*)X, ldx, xm, scale, sgrp,
+                         (const TY*)R, ldr, rm, (TY*)Y, ldy, ym, M, N, act);
+      return SDP_CHECK_LAUNCH();
+    });
   }
+  if (xdt != ydt) return (int)hipErrorInvalidValue;  // mixed dtypes: 16-B aligned rows, N % 8 == 0 only
   const int g = ew_grid((int64_t)M * N);
-  if (dtype == 1)
+  if (xdt == 1)
     hipLaunchKernelGGL(rowscale_k<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)X, ldx, xm, scale, sgrp,
                        (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, M, N, act);
-  else if (dtype == 0)
+  else if (xdt == 0)
     hipLaunchKernelGGL(rowscale_k<float>, dim3(g), dim3(256), 0, s, (const float*)X, ldx, xm, scale, sgrp,
                        (const float*)R, ldr, rm, (float*)Y, ldy, ym, M, N, act);
   else
@@ -695,8 +711,8 @@ extern "C" int sdp_rowscale_add(int dtype, const void* X, int64_t ldx, int x_grp
                                 const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp, int64_t r_gstride,
                                 int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int M, int N,
                                 void* stream) {
-  return rowscale_impl(dtype, ACT_NONE, X, ldx, x_grp, x_gstride, x_off, scale, sgrp, R, ldr, r_grp, r_gstride, r_off,
-                       Y, ldy, y_grp, y_gstride, y_off, M, N, stream);
+  return rowscale_impl(dtype, dtype, ACT_NONE, X, ldx, x_grp, x_gstride, x_off, scale, sgrp, R, ldr, r_grp, r_gstride,
+                       r_off, Y, ldy, y_grp, y_gstride, y_off, M, N, stream);
 }
 
 // Y = act(X) * scale + R: activation, drop path and residual add of a ConvMixer branch in one
@@ -705,8 +721,18 @@ extern "C" int sdp_act_rowscale_add(int dtype, int act, const void* X, int64_t l
                                     int x_off, const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp,
                                     int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride,
                                     int y_off, int M, int N, void* stream) {
-  return rowscale_impl(dtype, act, X, ldx, x_grp, x_gstride, x_off, scale, sgrp, R, ldr, r_grp, r_gstride, r_off, Y,
-                       ldy, y_grp, y_gstride, y_off, M, N, stream);
+  return rowscale_impl(dtype, dtype, act, X, ldx, x_grp, x_gstride, x_off, scale, sgrp, R, ldr, r_grp, r_gstride,
+                       r_off, Y, ldy, y_grp, y_gstride, y_off, M, N, stream);
+}
+
+// Mixed-dtype form: X in x_dtype, R and Y in y_dtype (fp32 residual stream of bf16 training:
+// y32 = act(x16) * scale + r32, or a stream gradient cast into a branch, y16 = x32 * scale).
+extern "C" int sdp_rowscale_add_mixed(int x_dtype, int y_dtype, int act, const void* X, int64_t ldx, int x_grp,
+                                      int64_t x_gstride, int x_off, const float* scale, int sgrp, const void* R,
+                                      int64_t ldr, int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy,
+                                      int y_grp, int64_t y_gstride, int y_off, int M, int N, void* stream) {
+  return rowscale_impl(x_dtype, y_dtype, act, X, ldx, x_grp, x_gstride, x_off, scale, sgrp, R, ldr, r_grp, r_gstride,
+                       r_off, Y, ldy, y_grp, y_gstride, y_off, M, N, stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -799,10 +825,10 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ X, int64_t
 
 // Same backward, 8 consecutive channels per lane (16-B accesses; C % 8 == 0, aligned rows):
 // lane covers channels 8 * lane + 512 * i, i < V.
-template <typename T, int V>
+template <typename T, typename TD, int V>
 __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_t ldx, RowMap xm,
                                                  const float* __restrict__ st, const float* __restrict__ g,
-                                                 const T* __restrict__ DY, int64_t lddy, RowMap dym,
+                                                 const TD* __restrict__ DY, int64_t lddy, RowMap dym,
                                                  const T* __restrict__ ADD, int64_t ldadd, RowMap am,
                                                  T* __restrict__ DX, int64_t lddx, RowMap dxm, int M, int C,
                                                  float* __restrict__ part) {
@@ -816,14 +842,14 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
   for (int64_t m = (int64_t)blockIdx.x * 4 + w; m < M; m += (int64_t)gridDim.x * 4) {
     const float mean = st[2 * m], rstd = st[2 * m + 1];
     const T* xp = X + xm(m) * ldx;
-    const T* dyp = DY + dym(m) * lddy;
+    const TD* dyp = DY + dym(m) * lddy;
     V8<T> xh[V], gd[V];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       const int c = 8 * lane + 512 * i;
       if (c < C) {
-        V8<T> dy;
+        V8<TD> dy;
         dy.load(dyp + c);
         xh[i].load(xp + c);
         const f32x4 g0 = *(const f32x4*)(g + c), g1 = *(const f32x4*)(g + c + 4);
@@ -880,10 +906,10 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
 
 // LayerNorm forward that also writes its statistics (training forward keeps them for the
 // backward): one wave per row, 8 consecutive channels per lane (C % 8 == 0, <= 2048).
-template <typename T, int V>
+template <typename T, typename TY, int V>
 __global__ __launch_bounds__(256) void ln_fwd_v8(const T* __restrict__ X, int64_t ldx, RowMap xm, float eps,
                                                  const float* __restrict__ g, const float* __restrict__ b,
-                                                 float* __restrict__ st, T* __restrict__ Y, int64_t ldy, RowMap ym,
+                                                 float* __restrict__ st, TY* __restrict__ Y, int64_t ldy, RowMap ym,
                                                  int M, int C) {
   const int lane = threadIdx.x & 63;
   const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -912,17 +938,18 @@ __global__ __launch_bounds__(256) void ln_fwd_v8(const T* __restrict__ X, int64_
   }
   const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)C + eps);
   if (lane == 0) *(float2*)(st + 2 * m) = float2{mean, rstd};
-  T* yp = Y + ym(m) * ldy;
+  TY* yp = Y + ym(m) * ldy;
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int c = 8 * lane + 512 * i;
     if (c < C) {
       const f32x4 g0 = *(const f32x4*)(g + c), g1 = *(const f32x4*)(g + c + 4);
       const f32x4 b0 = *(const f32x4*)(b + c), b1 = *(const f32x4*)(b + c + 4);
+      V8<TY> y;
 #pragma unroll
       for (int q = 0; q < 8; ++q)
-        x[i].v[q] = (x[i].v[q] - mean) * rstd * (q < 4 ? g0[q] : g1[q - 4]) + (q < 4 ? b0[q] : b1[q - 4]);
-      x[i].store(yp + c);
+        y.v[q] = (x[i].v[q] - mean) * rstd * (q < 4 ? g0[q] : g1[q - 4]) + (q < 4 ? b0[q] : b1[q - 4]);
+      y.store(yp + c);
     }
   }
 }
@@ -937,10 +964,10 @@ SDP_DEV float seg_sum(float v) {
   return v;
 }
 
-template <typename T, int L>
+template <typename T, typename TY, int L>
 __global__ __launch_bounds__(256) void ln_fwd_sm(const T* __restrict__ X, int64_t ldx, RowMap xm, float eps,
                                                  const float* __restrict__ g, const float* __restrict__ b,
-                                                 float* __restrict__ st, T* __restrict__ Y, int64_t ldy, RowMap ym,
+                                                 float* __restrict__ st, TY* __restrict__ Y, int64_t ldy, RowMap ym,
                                                  int M, int C) {
   constexpr int R = 64 / L;
   const int lane = threadIdx.x & 63, seg = lane / L, sl = lane % L;
@@ -965,17 +992,18 @@ __global__ __launch_bounds__(256) void ln_fwd_sm(const T* __restrict__ X, int64_
   if (act) {
     const f32x4 g0 = *(const f32x4*)(g + c), g1 = *(const f32x4*)(g + c + 4);
     const f32x4 b0 = *(const f32x4*)(b + c), b1 = *(const f32x4*)(b + c + 4);
+    V8<TY> y;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
-      x.v[q] = (x.v[q] - mean) * rstd * (q < 4 ? g0[q] : g1[q - 4]) + (q < 4 ? b0[q] : b1[q - 4]);
-    x.store(Y + ym(m) * ldy + c);
+      y.v[q] = (x.v[q] - mean) * rstd * (q < 4 ? g0[q] : g1[q - 4]) + (q < 4 ? b0[q] : b1[q - 4]);
+    y.store(Y + ym(m) * ldy + c);
   }
 }
 
-template <typename T, int L>
+template <typename T, typename TD, int L>
 __global__ __launch_bounds__(256) void ln_bwd_sm(const T* __restrict__ X, int64_t ldx, RowMap xm,
                                                  const float* __restrict__ st, const float* __restrict__ g,
-                                                 const T* __restrict__ DY, int64_t lddy, RowMap dym,
+                                                 const TD* __restrict__ DY, int64_t lddy, RowMap dym,
                                                  const T* __restrict__ ADD, int64_t ldadd, RowMap am,
                                                  T* __restrict__ DX, int64_t lddx, RowMap dxm, int M, int C,
                                                  float* __restrict__ part) {
@@ -1001,7 +1029,7 @@ __global__ __launch_bounds__(256) void ln_bwd_sm(const T* __restrict__ X, int64_
     if (act) {
       mean = st[2 * m];
       rstd = st[2 * m + 1];
-      V8<T> dy;
+      V8<TD> dy;
       dy.load(DY + dym(m) * lddy + c);
       xh.load(X + xm(m) * ldx + c);
 #pragma unroll
@@ -1053,9 +1081,9 @@ __global__ __launch_bounds__(256) void ln_bwd_sm(const T* __restrict__ X, int64_
   }
 }
 
-extern "C" int sdp_ln_fwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, float eps,
-                          const float* gamma, const float* beta, float* stats, void* Y, int64_t ldy, int y_grp,
-                          int64_t y_gstride, int y_off, int M, int C, void* stream) {
+static int ln_fwd_impl(int xdt, int ydt, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                       float eps, const float* gamma, const float* beta, float* stats, void* Y, int64_t ldy, int y_grp,
+                       int64_t y_gstride, int y_off, int M, int C, void* stream) {
   if (!X || !Y || !stats || !gamma || !beta || M < 0 || C <= 0 || C > 2048 || C % 8) return (int)hipErrorInvalidValue;
   if (ldx % 8 || ldy % 8 || (uintptr_t)X % 16 || (uintptr_t)Y % 16 || (uintptr_t)gamma % 16 || (uintptr_t)beta % 16 ||
       (uintptr_t)stats % 8)
@@ -1063,32 +1091,44 @@ extern "C" int sdp_ln_fwd(int dtype, const void* X, int64_t ldx, int x_grp, int6
   if (M == 0) return 0;
   const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), ym = mk_tmap(y_grp, y_gstride, y_off);
   hipStream_t s = (hipStream_t)stream;
-  if (C <= 128) {  // several rows per wave
-    const int L = C <= 64 ? 8 : 16, R = 64 / L;
-    dim3 gs((M + 4 * R - 1) / (4 * R));
-#define SDP_LNFS(TT, LL)                                                                                      \
-  hipLaunchKernelGGL((ln_fwd_sm<TT, LL>), gs, dim3(256), 0, s, (const TT*)X, ldx, xm, eps, gamma, beta, stats, \
-                     (TT*)Y, ldy, ym, M, C)
-    if (dtype == 1) { if (L == 8) SDP_LNFS(bf16_t, 8); else SDP_LNFS(bf16_t, 16); }
-    else if (dtype == 0) { if (L == 8) SDP_LNFS(float, 8); else SDP_LNFS(float, 16); }
-    else return (int)hipErrorInvalidValue;
-#undef SDP_LNFS
-    return SDP_CHECK_LAUNCH();
-  }
-  dim3 grid((M + 3) / 4);
-  const int v8 = (C + 511) / 512;
-#define SDP_LNF(TT, VV)                                                                                       \
-  hipLaunchKernelGGL((ln_fwd_v8<TT, VV>), grid, dim3(256), 0, s, (const TT*)X, ldx, xm, eps, gamma, beta, stats, \
-                     (TT*)Y, ldy, ym, M, C)
-  if (dtype == 1) {
-    if (v8 <= 1) SDP_LNF(bf16_t, 1); else if (v8 <= 2) SDP_LNF(bf16_t, 2); else SDP_LNF(bf16_t, 4);
-  } else if (dtype == 0) {
-    if (v8 <= 1) SDP_LNF(float, 1); else if (v8 <= 2) SDP_LNF(float, 2); else SDP_LNF(float, 4);
-  } else {
-    return (int)hipErrorInvalidValue;
-  }
+  return by_dtypes(xdt, ydt, [&](auto tx, auto ty) {
+    using TX = typename decltype(tx)::type;
+    using TY = typename decltype(ty)::type;
+    if (C <= 128) {  // several rows per wave
+      const int L = C <= 64 ? 8 : 16, R = 64 / L;
+      const dim3 gs((M + 4 * R - 1) / (4 * R));
+      if (L == 8)
+        hipLaunchKernelGGL((ln_fwd_sm<TX, TY, 8>), gs, dim3(256), 0, s, (const TX*)X, ldx, xm, eps, gamma, beta, stats,
+                           (TY*)Y, ldy, ym, M, C);
+      else
+        hipLaunchKernelGGL((ln_fwd_sm<TX, TY, 16>), gs, dim3(256), 0, s, (const TX*)X, ldx, xm, eps, gamma, beta,
+                           stats, (TY*)Y, ldy, ym, M, C);
+      return SDP_CHECK_LAUNCH();
+    }
+    const dim3 grid((M + 3) / 4);
+    const int v8 = (C + 511) / 512;
+#define SDP_LNF(VV)                                                                                                \
+  hipLaunchKernelGGL((ln_fwd_v8<TX, TY, VV>), grid, dim3(256), 0, s, (const TX*)X, ldx, xm, eps, gamma, beta, stats, \
+                     (TY*)Y, ldy, ym, M, C)
+    if (v8 <= 1) SDP_LNF(1); else if (v8 <= 2) SDP_LNF(2); else SDP_LNF(4);
 #undef SDP_LNF
-  return SDP_CHECK_LAUNCH();
+    return SDP_CHECK_LAUNCH();
+  });
+}
+
+extern "C" int sdp_ln_fwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, float eps,
+                          const float* gamma, const float* beta, float* stats, void* Y, int64_t ldy, int y_grp,
+                          int64_t y_gstride, int y_off, int M, int C, void* stream) {
+  return ln_fwd_impl(dtype, dtype, X, ldx, x_grp, x_gstride, x_off, eps, gamma, beta, stats, Y, ldy, y_grp, y_gstride,
+                     y_off, M, C, stream);
+}
+
+// X in x_dtype, Y in y_dtype (fp32 residual stream -> bf16 GEMM operand).
+extern "C" int sdp_ln_fwd_mixed(int x_dtype, int y_dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride,
+                                int x_off, float eps, const float* gamma, const float* beta, float* stats, void* Y,
+                                int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int M, int C, void* stream) {
+  return ln_fwd_impl(x_dtype, y_dtype, X, ldx, x_grp, x_gstride, x_off, eps, gamma, beta, stats, Y, ldy, y_grp,
+                     y_gstride, y_off, M, C, stream);
 }
 
 extern "C" int sdp_ln_apply(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
@@ -1116,50 +1156,44 @@ extern "C" int sdp_ln_bwd_blocks(int M) {
   return b < 1024 ? (b > 0 ? b : 1) : 1024;
 }
 
-extern "C" int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
-                          const float* stats, const float* gamma, const void* DY, int64_t lddy, int dy_grp,
-                          int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,
-                          int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride, int dx_off, int M, int C,
-                          float* part, void* stream) {
+static int ln_bwd_impl(int xdt, int dydt, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                       const float* stats, const float* gamma, const void* DY, int64_t lddy, int dy_grp,
+                       int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,
+                       int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride, int dx_off, int M, int C,
+                       float* part, void* stream) {
   if (!X || !stats || !gamma || !DY || !DX || M < 0 || C <= 0 || C > 2048) return (int)hipErrorInvalidValue;
   if (M == 0) return 0;
   const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), dym = mk_tmap(dy_grp, dy_gstride, dy_off),
                am = mk_tmap(a_grp, a_gstride, a_off), dxm = mk_tmap(dx_grp, dx_gstride, dx_off);
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(sdp_ln_bwd_blocks(M));
+  const dim3 grid(sdp_ln_bwd_blocks(M));
   const size_t lds = (size_t)8 * C * sizeof(float);
-  const int v = (C + 63) / 64;
-  const int es = dtype == 1 ? 2 : 4;
   const bool vec = C % 8 == 0 && ldx % 8 == 0 && lddy % 8 == 0 && lddx % 8 == 0 && (!ADD || ldadd % 8 == 0) &&
                    (uintptr_t)X % 16 == 0 && (uintptr_t)DY % 16 == 0 && (uintptr_t)DX % 16 == 0 &&
-                   (!ADD || (uintptr_t)ADD % 16 == 0) && (uintptr_t)gamma % 16 == 0 && C <= 2048;
-  (void)es;
+                   (!ADD || (uintptr_t)ADD % 16 == 0) && (uintptr_t)gamma % 16 == 0;
   if (vec) {
-#define SDP_LNV(TT, VV)                                                                                          \
-  hipLaunchKernelGGL((ln_bwd_v8<TT, VV>), grid, dim3(256), lds, s, (const TT*)X, ldx, xm, stats, gamma, (const TT*)DY, \
-                     lddy, dym, (const TT*)ADD, ldadd, am, (TT*)DX, lddx, dxm, M, C, part)
-    const int v8 = (C + 511) / 512;
-    if (C <= 128) {  // several rows per wave
-#define SDP_LNVS(TT, LL)                                                                                         \
-  hipLaunchKernelGGL((ln_bwd_sm<TT, LL>), grid, dim3(256), lds, s, (const TT*)X, ldx, xm, stats, gamma, (const TT*)DY, \
-                     lddy, dym, (const TT*)ADD, ldadd, am, (TT*)DX, lddx, dxm, M, C, part)
-      const bool l8 = C <= 64;
-      if (dtype == 1) { if (l8) SDP_LNVS(bf16_t, 8); else SDP_LNVS(bf16_t, 16); }
-      else if (dtype == 0) { if (l8) SDP_LNVS(float, 8); else SDP_LNVS(float, 16); }
-      else return (int)hipErrorInvalidValue;
+    return by_dtypes(xdt, dydt, [&](auto tx, auto td) {
+      using TX = typename decltype(tx)::type;
+      using TD = typename decltype(td)::type;
+      if (C <= 128) {  // several rows per wave
+#define SDP_LNVS(LL)                                                                                            \
+  hipLaunchKernelGGL((ln_bwd_sm<TX, TD, LL>), grid, dim3(256), lds, s, (const TX*)X, ldx, xm, stats, gamma,        \
+                     (const TD*)DY, lddy, dym, (const TX*)ADD, ldadd, am, (TX*)DX, lddx, dxm, M, C, part)
+        if (C <= 64) SDP_LNVS(8); else SDP_LNVS(16);
 #undef SDP_LNVS
-      return SDP_CHECK_LAUNCH();
-    }
-    if (dtype == 1) {
-      if (v8 <= 1) SDP_LNV(bf16_t, 1); else if (v8 <= 2) SDP_LNV(bf16_t, 2); else SDP_LNV(bf16_t, 4);
-    } else if (dtype == 0) {
-      if (v8 <= 1) SDP_LNV(float, 1); else if (v8 <= 2) SDP_LNV(float, 2); else SDP_LNV(float, 4);
-    } else {
-      return (int)hipErrorInvalidValue;
-    }
+        return SDP_CHECK_LAUNCH();
+      }
+      const int v8 = (C + 511) / 512;
+#define SDP_LNV(VV)                                                                                              \
+  hipLaunchKernelGGL((ln_bwd_v8<TX, TD, VV>), grid, dim3(256), lds, s, (const TX*)X, ldx, xm, stats, gamma,        \
+                     (const TD*)DY, lddy, dym, (const TX*)ADD, ldadd, am, (TX*)DX, lddx, dxm, M, C, part)
+      if (v8 <= 1) SDP_LNV(1); else if (v8 <= 2) SDP_LNV(2); else SDP_LNV(4);
 #undef SDP_LNV
-    return SDP_CHECK_LAUNCH();
+      return SDP_CHECK_LAUNCH();
+    });
   }
+  if (xdt != dydt) return (int)hipErrorInvalidValue;  // mixed dtypes: vector path only
+  const int v = (C + 63) / 64;
 #define SDP_LNB(TT, VV)                                                                                          \
   hipLaunchKernelGGL((ln_bwd_k<TT, VV>), grid, dim3(256), lds, s, (const TT*)X, ldx, xm, stats, gamma, (const TT*)DY, \
                      lddy, dym, (const TT*)ADD, ldadd, am, (TT*)DX, lddx, dxm, M, C, part)
@@ -1170,9 +1204,9 @@ extern "C" int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int6
   else if (v <= 12) SDP_LNB(TT, 12);                  \
   else if (v <= 16) SDP_LNB(TT, 16);                  \
   else SDP_LNB(TT, 32)
-  if (dtype == 1) {
+  if (xdt == 1) {
     SDP_LNB_T(bf16_t);
-  } else if (dtype == 0) {
+  } else if (xdt == 0) {
     SDP_LNB_T(float);
   } else {
     return (int)hipErrorInvalidValue;
@@ -1180,6 +1214,27 @@ extern "C" int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int6
 #undef SDP_LNB_T
 #undef SDP_LNB
   return SDP_CHECK_LAUNCH();
+}
+
+extern "C" int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                          const float* stats, const float* gamma, const void* DY, int64_t lddy, int dy_grp,
+                          int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,
+                          int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride, int dx_off, int M, int C,
+                          float* part, void* stream) {
+  return ln_bwd_impl(dtype, dtype, X, ldx, x_grp, x_gstride, x_off, stats, gamma, DY, lddy, dy_grp, dy_gstride, dy_off,
+                     ADD, ldadd, a_grp, a_gstride, a_off, DX, lddx, dx_grp, dx_gstride, dx_off, M, C, part, stream);
+}
+
+// X, ADD and DX in x_dtype (the residual stream and its gradient), DY in dy_dtype (the
+// gradient of the LN output coming back from a bf16 GEMM operand).
+extern "C" int sdp_ln_bwd_mixed(int x_dtype, int dy_dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride,
+                                int x_off, const float* stats, const float* gamma, const void* DY, int64_t lddy,
+                                int dy_grp, int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp,
+                                int64_t a_gstride, int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride,
+                                int dx_off, int M, int C, float* part, void* stream) {
+  return ln_bwd_impl(x_dtype, dy_dtype, X, ldx, x_grp, x_gstride, x_off, stats, gamma, DY, lddy, dy_grp, dy_gstride,
+                     dy_off, ADD, ldadd, a_grp, a_gstride, a_off, DX, lddx, dx_grp, dx_gstride, dx_off, M, C, part,
+                     stream);
 }
 
 // ---------------------------------------------------------------------------

@@ -23,8 +23,15 @@ from torch.nn import functional as F
 from torch.nn.parameter import Parameter
 
 import sdpnet_hip as sp
-from sdpnet_engine import (act_code, as_dtype, cached, check_eval, compute_dtype, f32, hooked, num_reg_rows)
+from sdpnet_engine import (act_code, as_dtype, cached, compute_dtype, f32, hooked, num_reg_rows)
 from utility_layers import StochasticDepth as SD
+
+
+def _train():
+    """sdpnet_train, imported at call time (train-mode forwards of the sub-modules)."""
+    import sdpnet_train
+    return sdpnet_train
+
 
 Rows = sp.Rows
 
@@ -77,6 +84,8 @@ class LayerNorm(nn.Module):
         sp.layernorm(x, g, b, self.eps, y, M, self.gamma.shape[0])
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.training:
+            return _train().train_layernorm(self, x)
         dt = compute_dtype(x, self)
         with torch.no_grad():
             x = x.to(dt).contiguous()
@@ -132,6 +141,8 @@ class ConvPatcher(nn.Module):
         sp.gemm(_dense(patches), w, y, B * P, w.shape[0], kp, resid=resid, act=act, resid_pre=True, part=part)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.training:
+            return _train().train_patcher(self, x)
         dt = compute_dtype(x, self)
         with torch.no_grad():
             B, _, Hi, Wi = x.shape
@@ -218,7 +229,8 @@ class ConvMixer(nn.Module):
         sp.gemm(_dense(hid), w["dn_w"], img, M, C, 4 * C, bias=w["dn_b"], resid=img, part=part)
 
     def forward(self, x: torch.Tensor):
-        check_eval(self)
+        if self.training:
+            return _train().train_conv_mixer(self, x)
         dt = compute_dtype(x, self)
         with torch.no_grad():
             x = x.to(dt).contiguous()
@@ -267,6 +279,8 @@ class EmbeddingLayer(nn.Module):
         return f32(self.register_embedding_layer.weight), R
 
     def forward(self, x: torch.Tensor, num_registers: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self.training:
+            return _train().train_pos_embedding(self, x, num_registers)
         dt = compute_dtype(x, self)
         with torch.no_grad():
             B, C, H, W = x.shape
@@ -328,6 +342,8 @@ class ConvEmbedding(nn.Module):
         return t[1:] if R > 0 else t, R
 
     def forward(self, x: torch.Tensor, num_registers: int = 3) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self.training:
+            return _train().train_pos_embedding(self, x, num_registers)
         dt = compute_dtype(x, self)
         with torch.no_grad():
             B, C, H, W = x.shape
@@ -457,7 +473,8 @@ class EncoderLayer(nn.Module):
         sp.gemm(_dense(f), w["w2"], _dense(tok), T, C, F_, bias=w["b2"], resid=_dense(tok), part=part)  # :308-309
 
     def forward(self, x: torch.Tensor, register: torch.Tensor, mask: torch.Tensor = None):
-        check_eval(self)
+        if self.training:
+            return _train().train_encoder(self, x, register, mask)
         dt = compute_dtype(x, self)
         with torch.no_grad():
             tok, B, N, R, H, W = _to_tokens(x, register, dt)
@@ -526,7 +543,6 @@ class Block(nn.Module):
         self.t_block._run_tokens(tok, B, N, dt, mask, part=part)
 
     def forward(self, x: torch.Tensor, register: torch.Tensor, mask: torch.Tensor = None):
-        check_eval(self)
         if hooked(self):  # reference composition (layers.py:381-386) so hooked children fire
             if not self.conv_first:
                 x, register = self.t_block(x, register, mask)
@@ -534,6 +550,8 @@ class Block(nn.Module):
                 return x, register
             x = self.conv_blocks(x)
             return self.t_block(x, register, mask)
+        if self.training:
+            return _train().train_block(self, x, register, mask)
         dt = compute_dtype(x, self)
         with torch.no_grad():
             tok, B, N, R, H, W = _to_tokens(x, register, dt)
@@ -629,7 +647,8 @@ class ClassificationHead(nn.Module):
         return res
 
     def forward(self, x: torch.Tensor, registers: torch.Tensor) -> torch.Tensor:
-        check_eval(self)
+        if self.training:
+            return _train().train_head(self, x, registers)
         dt = compute_dtype(x if not self.from_register else registers, self)
         with torch.no_grad():
             if self.from_register:

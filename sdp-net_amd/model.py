@@ -30,7 +30,7 @@ import sdpnet_ops
 from layers import ConvMixer, EmbeddingLayer, ConvPatcher, Block, FinalBlock, ClassificationHead, ConvEmbedding  # noqa: F401
 from utility_layers import SdPModel, StochasticDepth  # noqa: F401
 from layers import new_partials  # token-buffer plumbing of the fused path
-from sdpnet_engine import act_code, as_dtype, cached, check_eval, compute_dtype, hooked as _hooked
+from sdpnet_engine import act_code, as_dtype, cached, compute_dtype, hooked as _hooked
 from training_utilities import KeLu
 
 torch.set_float32_matmul_precision('high')  # model.py:9 (import side effect kept)

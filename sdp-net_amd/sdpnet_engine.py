@@ -106,13 +106,6 @@ def num_reg_rows(max_num: int, num_registers: int) -> int:
     return len(range(max_num)[: num_registers + 1])
 
 
-def check_eval(module: nn.Module):
-    if module.training:
-        raise NotImplementedError(
-            "sdpnet HIP path implements the eval-mode forward (dropout / stochastic depth = identity). "
-            "Training-mode forward/backward is the next scope row (SURVEY.md §8(f) rank 1); call .eval().")
-
-
 def hooked(module: nn.Module) -> bool:
     """True if any submodule has forward (pre-)hooks: the caller then composes
     the forward module by module so every hooked __call__ fires."""

@@ -59,6 +59,7 @@ _SIGS = {
     "sdp_attention_set_kernel": ([_i32], _i32),
     "sdp_patchify": ([_i32, _vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp], _i32),
     "sdp_pos_table": ([_vp, _vp, _vp, _i32, _i32, _i32, _vp], _i32),
+    "sdp_avgpool_table_bwd": ([_vp, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _vp], _i32),
     "sdp_avgpool_table": ([_vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp], _i32),
     "sdp_copy_rows": ([_i32, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _i32, _i32, _i32, _vp], _i32),
     "sdp_nchw_add_table": ([_i32, _vp, _vp, _i32, _i32, _i32, _vp], _i32),
@@ -82,6 +83,12 @@ _SIGS = {
                           _vp], _i32),
     "sdp_act_rowscale_add": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _i32, _i32,
                           _vp], _i32),
+    "sdp_rowscale_add_mixed": ([_i32, _i32, _i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64,
+                                *_ROWMAP, _i32, _i32, _vp], _i32),
+    "sdp_ln_fwd_mixed": ([_i32, _i32, _vp, _i64, *_ROWMAP, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp],
+                         _i32),
+    "sdp_ln_bwd_mixed": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _vp,
+                          _i64, *_ROWMAP, _i32, _i32, _vp, _vp], _i32),
     "sdp_ln_apply": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_ln_bwd_blocks": ([_i32], _i32),
     "sdp_ln_fwd": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
@@ -374,6 +381,16 @@ def avgpool_table(bone: torch.Tensor, out: torch.Tensor, H: int, W: int, C: int,
     _check(rc, "avgpool_table")
 
 
+def avgpool_table_bwd(dtable: torch.Tensor, dbone: torch.Tensor, H: int, W: int, C: int, k: int):
+    """dbone [1, C, BH, BW] fp32 = adjoint of avgpool_table applied to dtable [H*W, C] fp32."""
+    _need_cuda(dtable, dbone)
+    _req(dtable.is_contiguous() and dbone.is_contiguous() and dtable.dtype == dbone.dtype == torch.float32)
+    _req(dtable.numel() >= H * W * C and dbone.shape[-3] == C)
+    rc = lib().sdp_avgpool_table_bwd(dtable.data_ptr(), H, W, C, k, dbone.data_ptr(), dbone.shape[-2],
+                                     dbone.shape[-1], _stream(dbone))
+    _check(rc, "avgpool_table_bwd")
+
+
 def copy_rows(src: torch.Tensor, lds: int, sgstride: int, dst: torch.Tensor, ldd: int, gstride: int, B: int,
               R: int, C: int, src_offset_rows: int = 0, dst_offset_rows: int = 0):
     _need_cuda(src, dst)
@@ -567,10 +584,15 @@ def act_bwd(Z: torch.Tensor, DY: torch.Tensor, DZ: torch.Tensor, M: int, N: int,
 
 def rowscale_add(x: Rows, y: Rows, M: int, N: int, scale: Optional[torch.Tensor] = None, sgrp: int = 1,
                  resid: Optional[Rows] = None, act: int = 0):
-    """y = act(x) * scale[m / sgrp] (+ resid) over row maps (act 0: sdp_rowscale_add)."""
+    """y = act(x) * scale[m / sgrp] (+ resid) over row maps (act 0: sdp_rowscale_add).  x may
+    differ in dtype from y (resid has y's dtype): sdp_rowscale_add_mixed."""
     _need_cuda(x.t, y.t, scale)
     _req(scale is None or scale.dtype == torch.float32, "rowscale scale fp32")
-    if act:
+    _req(resid is None or resid.t.dtype == y.t.dtype, "rowscale resid dtype = y dtype")
+    if x.t.dtype != y.t.dtype:
+        rc = lib().sdp_rowscale_add_mixed(dcode(x.t.dtype), dcode(y.t.dtype), int(act), *x.args(), _ptr(scale), sgrp,
+                                          *_rows_args(resid), *y.args(), M, N, _stream(y.t))
+    elif act:
         rc = lib().sdp_act_rowscale_add(dcode(x.t.dtype), int(act), *x.args(), _ptr(scale), sgrp, *_rows_args(resid),
                                         *y.args(), M, N, _stream(y.t))
     else:
@@ -591,10 +613,15 @@ def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows
            add: Optional[Rows] = None, want_affine: bool = True):
     """dx (= LN backward [+ add]); returns (dgamma, dbeta) fp32 [C] or None."""
     _need_cuda(x.t, stats, gamma, dy.t, dx.t)
+    _req(dx.t.dtype == x.t.dtype and (add is None or add.t.dtype == x.t.dtype), "ln_bwd x / add / dx dtypes")
     nb = lib().sdp_ln_bwd_blocks(M)
     part = torch.empty(nb, 2, C, dtype=torch.float32, device=dx.t.device) if want_affine else None
-    rc = lib().sdp_ln_bwd(dcode(x.t.dtype), *x.args(), stats.data_ptr(), gamma.data_ptr(), *dy.args(),
-                          *_rows_args(add), *dx.args(), M, C, _ptr(part), _stream(dx.t))
+    if dy.t.dtype != x.t.dtype:  # fp32 stream, bf16 gradient of the LN output
+        rc = lib().sdp_ln_bwd_mixed(dcode(x.t.dtype), dcode(dy.t.dtype), *x.args(), stats.data_ptr(), gamma.data_ptr(),
+                                    *dy.args(), *_rows_args(add), *dx.args(), M, C, _ptr(part), _stream(dx.t))
+    else:
+        rc = lib().sdp_ln_bwd(dcode(x.t.dtype), *x.args(), stats.data_ptr(), gamma.data_ptr(), *dy.args(),
+                              *_rows_args(add), *dx.args(), M, C, _ptr(part), _stream(dx.t))
     _check(rc, "ln_bwd")
     if part is None:
         return None
@@ -668,8 +695,12 @@ def ln_fwd(x: Rows, eps: float, gamma: torch.Tensor, beta: torch.Tensor, stats: 
     """One-pass LayerNorm that also writes its (mean, rstd) statistics (training forward)."""
     _need_cuda(x.t, y.t, gamma, beta, stats)
     _req(stats.dtype == gamma.dtype == beta.dtype == torch.float32, "ln_fwd fp32 params")
-    rc = lib().sdp_ln_fwd(dcode(x.t.dtype), *x.args(), float(eps), gamma.data_ptr(), beta.data_ptr(),
-                          stats.data_ptr(), *y.args(), M, C, _stream(y.t))
+    if x.t.dtype != y.t.dtype:
+        rc = lib().sdp_ln_fwd_mixed(dcode(x.t.dtype), dcode(y.t.dtype), *x.args(), float(eps), gamma.data_ptr(),
+                                    beta.data_ptr(), stats.data_ptr(), *y.args(), M, C, _stream(y.t))
+    else:
+        rc = lib().sdp_ln_fwd(dcode(x.t.dtype), *x.args(), float(eps), gamma.data_ptr(), beta.data_ptr(),
+                              stats.data_ptr(), *y.args(), M, C, _stream(y.t))
     _check(rc, "ln_fwd")
 
 

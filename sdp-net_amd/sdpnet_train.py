@@ -32,11 +32,17 @@ statistically and for forward/backward consistency.
 
 dtype: fp32 params (as the reference keeps them), compute in bf16 under
 ``torch.autocast("cuda", bf16)`` / bf16 inputs (the reference's training forward,
-training_tools.py:85) or exact fp32 otherwise.  Gradients are fp32.
+training_tools.py:85) or exact fp32 otherwise.  Gradients are fp32.  In bf16 mode the
+residual stream (the token rows between sub-layers, ``x + drop_path(branch)``) and its
+gradient stay fp32, as autocast keeps them: LayerNorm reads fp32 rows and writes the bf16
+GEMM operand, each branch's bf16 output is added into the fp32 stream, and the stream
+gradient is rounded to bf16 only where it enters a branch (``stream_dtype``;
+``set_fp32_stream(False)`` gives the all-bf16 stream).
 """
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -46,6 +52,22 @@ import sdpnet_hip as sp
 from sdpnet_engine import act_code, as_dtype, compute_dtype, f32, num_reg_rows
 
 Rows = sp.Rows
+
+_FP32_STREAM = os.environ.get("SDPNET_TRAIN_FP32_STREAM", "1") != "0"
+
+
+def set_fp32_stream(on: bool) -> None:
+    """bf16 training keeps the residual stream and its gradient in fp32 (default) or bf16."""
+    global _FP32_STREAM
+    _FP32_STREAM = bool(on)
+
+
+def stream_dtype(dt, C: int):
+    """dtype of the residual stream for compute dtype ``dt`` and width C (the mixed-dtype
+    kernels take C % 8 == 0, C <= 2048)."""
+    if dt == torch.bfloat16 and _FP32_STREAM and C % 8 == 0 and C <= 2048:
+        return torch.float32
+    return dt
 
 
 def _dense(t: torch.Tensor) -> Rows:
@@ -150,7 +172,14 @@ def _dense_copy(src: Rows, M: int, C: int, dt, scale: Optional[torch.Tensor] = N
 
 def _branch_grad(d: torch.Tensor, T: int, C: int, dt, dp: Optional[torch.Tensor], grp: int, p: float, seed: int):
     """Gradient into a residual branch y = x + drop_path(dropout(z)): dz = d * mask / (1-p) * dp
-    (one pass; no copy at all when neither is active)."""
+    (one pass; no copy at all when neither is active and d is already in the branch dtype).
+    An fp32 stream gradient is rounded to the bf16 branch first (with the drop-path scale),
+    then the dropout mask is applied in place."""
+    if d.dtype != dt:
+        out = _dense_copy(_dense(d), T, C, dt, dp, grp)
+        if p > 0:
+            sp.act_bwd(out, out, out, T, C, 0, p, seed)
+        return out
     if p <= 0 and dp is None:
         return d
     out = _empty((T, C), dt, d.device)
@@ -228,7 +257,7 @@ class _MixerFn(torch.autograd.Function):
         h = _empty((M, 4 * C), dt, dev)
         sp.act_fwd(z2, h, M, 4 * C, act)
         out = _with_regs(mid, B, R, N, C)
-        if dp1 is None:  # residual add in the GEMM epilogue, straight into the token rows
+        if dp1 is None and tok.dtype == dt:  # residual add in the GEMM epilogue, straight into the token rows
             sp.gemm(_dense(h), W_["dnw"], Rows(out, C, P, N, R), M, C, 4 * C, bias=W_["dnb"], resid=imid)
         else:
             z3 = _linear(h, W_["dnw"], W_["dnb"], dt)
@@ -245,7 +274,7 @@ class _MixerFn(torch.autograd.Function):
         P, N = H * W, R + H * W
         M = B * P
         dt, act, W_ = S["dt"], S["act"], S["W"]
-        dout = dout.contiguous().to(dt)
+        dout = dout.contiguous().to(S["tok"].dtype)  # stream dtype
         dev = dout.device
         iout = Rows(dout, C, P, N, R)
         # branch 1
@@ -293,29 +322,35 @@ def _enc_params(e) -> List[Optional[nn.Parameter]]:
 
 def _attn_materialized(qkvn, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seed):
     """Attention with S / P materialised per (b, h) (fp32 path, and shapes the flash kernels
-    do not take): S = QK^T (fp32) -> softmax (+ dropout) -> O = Pd V."""
+    do not take): S = QK^T (fp32) -> softmax (+ dropout) -> O = Pd V.  ``qkvn`` is the fp32
+    operand copy in bf16 mode (P, dP and dS then stay fp32 as in the flash kernels; O is
+    rounded to dt)."""
     T = B * N
+    adt = qkvn.dtype
     Sm = _empty((B, Hn, N, Np), torch.float32, dev)
     sp.gemm_flex(qkvn, qkvn, Sm, N, N, hd, ta=False, tb=True, lda=3 * C, ldb=3 * C, ldc=Np, Z=Z, zdiv=Hn,
                  sa=(N * 3 * C, hd), sb=(N * 3 * C, hd), sc=(Hn * N * Np, N * Np), b_off=C)
-    Pm = _empty((B, Hn, N, Np), dt, dev)
-    Pd = _empty((B, Hn, N, Np), dt, dev) if p_att > 0 else Pm
+    Pm = _empty((B, Hn, N, Np), adt, dev)
+    Pd = _empty((B, Hn, N, Np), adt, dev) if p_att > 0 else Pm
     sp.softmax_fwd(Sm.view(-1, Np), Pm.view(-1, Np), Pd.view(-1, Np) if p_att > 0 else None, Z * N, N, Np,
                    1.0 / math.sqrt(hd), p_att, seed)
     del Sm
-    o = _empty((T, C), dt, dev)
+    o = _empty((T, C), adt, dev)
     sp.gemm_flex(Pd, qkvn, o, N, hd, N, ta=False, tb=False, lda=Np, ldb=3 * C, ldc=C, Z=Z, zdiv=Hn,
                  sa=(Hn * N * Np, N * Np), sb=(N * 3 * C, hd), sc=(N * C, hd), b_off=2 * C)
-    return o, None, Pm, Pd
+    return (o if adt == dt else sp.cast(o, dt)), None, Pm, Pd
 
 
 def _attn_materialized_bwd(qkvn, Pm, Pd, do, dqkv, dqk, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seed):
-    dPd = _empty((B, Hn, N, Np), dt, dev)
+    adt = qkvn.dtype
+    if do.dtype != adt:
+        do = sp.cast(do, adt)
+    dPd = _empty((B, Hn, N, Np), adt, dev)
     sp.gemm_flex(do, qkvn, dPd, N, N, hd, ta=False, tb=True, lda=C, ldb=3 * C, ldc=Np, Z=Z, zdiv=Hn,
                  sa=(N * C, hd), sb=(N * 3 * C, hd), sc=(Hn * N * Np, N * Np), b_off=2 * C)
     sp.gemm_flex(Pd, do, dqkv, N, hd, N, ta=True, tb=False, lda=Np, ldb=C, ldc=3 * C, Z=Z, zdiv=Hn,
                  sa=(Hn * N * Np, N * Np), sb=(N * C, hd), sc=(N * 3 * C, hd), c_off=2 * C)      # dV
-    dS = _empty((B, Hn, N, Np), dt, dev)
+    dS = _empty((B, Hn, N, Np), adt, dev)
     sp.softmax_bwd(Pm.view(-1, Np), dPd.view(-1, Np), dS.view(-1, Np), Z * N, N, Np, p_att, seed)
     del dPd
     scale = 1.0 / math.sqrt(hd)
@@ -371,14 +406,15 @@ class _EncoderFn(torch.autograd.Function):
             lse = _empty((Z * N,), torch.float32, dev)
             sp.attn_train_fwd(qkvn, o, lse, B, N, Hn, hd, 1.0 / math.sqrt(hd), p_att, seeds[0])
             Pm = Pd = None
-        else:
-            o, lse, Pm, Pd = _attn_materialized(qkvn, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seeds[0])
+        else:  # bf16: operands cast to fp32 once (small / odd head dims only)
+            qkva = qkvn if dt == torch.float32 else sp.cast(qkvn, torch.float32)
+            o, lse, Pm, Pd = _attn_materialized(qkva, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seeds[0])
 
         # x = x + drop_path1(dropout(o_proj(o)))                       (:300-303)
         zo = _linear(o, W_["wo"], None, dt)
         if p_ff > 0:
             sp.act_fwd(zo, zo, T, C, 0, p_ff, seeds[1])
-        t2 = _empty((T, C), dt, dev)
+        t2 = _empty((T, C), tok.dtype, dev)                               # stream dtype
         sp.rowscale_add(_dense(zo), _dense(t2), T, C, scale=dp1, sgrp=N, resid=_dense(tok))
         del zo
         # x = x + drop_path2(dropout(ff2(dropout(act(ff1(LN2 x))))))   (:306-309)
@@ -390,7 +426,7 @@ class _EncoderFn(torch.autograd.Function):
         z2 = _linear(h, W_["w2"], W_["b2"], dt)
         if p_ff > 0:
             sp.act_fwd(z2, z2, T, C, 0, p_ff, seeds[3])
-        out = _empty((T, C), dt, dev)
+        out = _empty((T, C), tok.dtype, dev)
         sp.rowscale_add(_dense(z2), _dense(out), T, C, scale=dp2, sgrp=N, resid=_dense(t2))
         ctx.st = dict(tok=tok, a1=a1, s1=s1, qkv=qkv, qkvn=qkvn, sq=sq, sk=sk, P=Pm, Pd=Pd, lse=lse, o=o, t2=t2, a2=a2, s2=s2,
                       z1=z1, h=h, W=W_, seeds=seeds, dp1=dp1, dp2=dp2, geo=(B, N, C, Hn, hd, Np), act=act, dt=dt,
@@ -405,7 +441,8 @@ class _EncoderFn(torch.autograd.Function):
         T, Z = B * N, B * Hn
         dt, act, W_, seeds = S["dt"], S["act"], S["W"], S["seeds"]
         p_ff, p_att = S["p_ff"], S["p_att"]
-        dout = dout.contiguous().to(dt)
+        sdt = S["tok"].dtype
+        dout = dout.contiguous().to(sdt)
         dev = dout.device
         # FFN branch
         dz2 = _branch_grad(dout, T, C, dt, S["dp2"], N, p_ff, seeds[3])
@@ -417,22 +454,28 @@ class _EncoderFn(torch.autograd.Function):
         del dh
         da2 = _dgrad(dz1, W_["w1"])
         gw1, gb1 = _wgrad(dz1, S["a2"]), _colsum(dz1)
-        dt2 = _empty((T, C), dt, dev)
+        dt2 = _empty((T, C), sdt, dev)
         gn2g, gn2b = sp.ln_bwd(_dense(S["t2"]), S["s2"], W_["n2g"], _dense(da2), _dense(dt2), T, C, add=_dense(dout))
         # attention branch
         dzo = _branch_grad(dt2, T, C, dt, S["dp1"], N, p_ff, seeds[1])
         do = _dgrad(dzo, W_["wo"])
         gwo = _wgrad(dzo, S["o"])
         qkvn, Pm, Pd = S["qkvn"], S["P"], S["Pd"]
-        dqkv = _empty((T, 3 * C), dt, dev)
         scale = 1.0 / math.sqrt(hd)
-        dqk = dqkv if not S["qn"] else _empty((T, 3 * C), dt, dev)
+        # dQ / dK land in dqk, dV in dqkv (the same buffer unless the q/k head LayerNorm follows)
+        adt = dt if Pm is None else Pm.dtype
+        dqkv = _empty((T, 3 * C), adt, dev)
+        dqk = dqkv if not S["qn"] else _empty((T, 3 * C), adt, dev)
         if Pm is None:  # flash backward: P recomputed from Q, K and the saved LSE
             delta = _empty((Z * N,), torch.float32, dev)
             sp.attn_train_bwd(qkvn, S["o"], do, S["lse"], delta, (dqk, 0), (dqk, C), (dqkv, 2 * C), B, N, Hn, hd,
                               scale, p_att, seeds[0])
         else:
-            _attn_materialized_bwd(qkvn, Pm, Pd, do, dqkv, dqk, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seeds[0])
+            qkva = qkvn if adt == dt else sp.cast(qkvn, adt)
+            _attn_materialized_bwd(qkva, Pm, Pd, do, dqkv, dqk, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seeds[0])
+            if adt != dt:  # fp32 attention internals of bf16 mode: round the q/k/v gradients once
+                dqk = sp.cast(dqk, dt)
+                dqkv = dqk if not S["qn"] else sp.cast(dqkv, dt)
         gqg = gqb = gkg = gkb = None
         if S["qn"]:
             qkv = S["qkv"]
@@ -457,7 +500,7 @@ class _EncoderFn(torch.autograd.Function):
 class _EmbedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, geo, model, dt, wp, eh, ew, ereg):
-        B, R, Hp, Wp, nreg_arg = geo
+        B, R, Hp, Wp, nreg_arg, sdt = geo
         pat = model.conv_init
         emb = model.embedding_layer
         C = wp.shape[0]
@@ -479,20 +522,30 @@ class _EmbedFn(torch.autograd.Function):
         else:
             pos = _empty((P, C), torch.float32, dev)
             sp.pos_table(f32(eh), f32(ew), pos, Hp, Wp, C)
-        posd = pos if dt == torch.float32 else as_dtype(pos, dt)
-        tok = _empty((B * N, C), dt, dev)
+        tok = _empty((B * N, C), sdt, dev)
         z = None
-        if act == 0:
+        if sdt != dt:  # fp32 stream: tok = act(bf16(patches . w^T) + pos) in fp32 (autocast's promotion)
+            zc = _linear(patches, w, None, dt)
+            if act == 0:
+                sp.rowscale_add(_dense(zc), Rows(tok, C, P, N, R), B * P, C, resid=Rows(pos, C, P, 0, 0))
+            else:
+                z = _empty((B * P, C), sdt, dev)
+                sp.rowscale_add(_dense(zc), _dense(z), B * P, C, resid=Rows(pos, C, P, 0, 0))
+                sp.rowscale_add(_dense(z), Rows(tok, C, P, N, R), B * P, C, act=act)
+            del zc
+        elif act == 0:
+            posd = pos if dt == torch.float32 else as_dtype(pos, dt)
             sp.gemm(_dense(patches), w, Rows(tok, C, P, N, R), B * P, C, kp, resid=Rows(posd, C, P, 0, 0),
                     resid_pre=True)
         else:  # keep the pre-activation for the backward
+            posd = pos if dt == torch.float32 else as_dtype(pos, dt)
             z = _empty((B * P, C), dt, dev)
             sp.gemm(_dense(patches), w, _dense(z), B * P, C, kp, resid=Rows(posd, C, P, 0, 0), resid_pre=True)
             sp.rowscale_add(_dense(z), Rows(tok, C, P, N, R), B * P, C, act=act)
         table, R2 = emb._register_rows(nreg_arg)
         if R:
             sp.copy_rows(table.contiguous(), C, 0, tok, C, N * C, B, R, C)
-        ctx.st = dict(patches=patches, geo=(B, R, Hp, Wp, C, P, N, p, kp), dt=dt, conv_emb=conv_emb, act=act, z=z,
+        ctx.st = dict(patches=patches, geo=(B, R, Hp, Wp, C, P, N, p, kp), dt=dt, sdt=sdt, conv_emb=conv_emb, act=act, z=z,
                       nrow_eh=None if conv_emb else eh.shape[0], nrow_ew=None if conv_emb else ew.shape[0],
                       nreg=ereg.shape[0], wshape=wp.shape)
         return tok
@@ -501,13 +554,14 @@ class _EmbedFn(torch.autograd.Function):
     def backward(ctx, dtok):
         S = ctx.st
         B, R, Hp, Wp, C, P, N, p, kp = S["geo"]
-        dt = S["dt"]
-        dtok = dtok.contiguous().to(dt)
+        dt, sdt = S["dt"], S["sdt"]
+        dtok = dtok.contiguous().to(sdt)
         dev = dtok.device
-        dimg = _dense_copy(Rows(dtok, C, P, N, R), B * P, C, dt)
+        dimg = _dense_copy(Rows(dtok, C, P, N, R), B * P, C, sdt)  # image rows, stream dtype
         if S["act"]:  # through the embedding activation: dz = act'(z) * d
             sp.act_bwd(S["z"], dimg, dimg, B * P, C, S["act"])
-        gw = _wgrad(dimg, S["patches"])[:, : 3 * p * p].contiguous().view(S["wshape"])
+        dconv = dimg if sdt == dt else _dense_copy(_dense(dimg), B * P, C, dt)
+        gw = _wgrad(dconv, S["patches"])[:, : 3 * p * p].contiguous().view(S["wshape"])
         geh = gew = None
         if not S["conv_emb"]:
             dpos = _empty((P, C), torch.float32, dev)
@@ -535,9 +589,10 @@ class _HeadFn(torch.autograd.Function):
         dev = tok.device
         from_reg = head.from_register
         rows, grp_off = (R, 0) if from_reg else (P, R)
-        m = _empty((B, C), dt, dev)
+        # the mean stays in the stream dtype when a LayerNorm follows (it rounds to dt itself)
+        m = _empty((B, C), tok.dtype if ln_g is not None else dt, dev)
         sp.group_mean(Rows(tok, C, rows, N, grp_off), m, B, rows, C)
-        st = dict(geo=geo, dt=dt, from_reg=from_reg, rows=rows, off=grp_off, m=m)
+        st = dict(geo=geo, dt=dt, sdt=tok.dtype, from_reg=from_reg, rows=rows, off=grp_off, m=m)
         x = m
         if ln_g is not None:
             a, s = _ln_fwd(_dense(m), B, C, f32(ln_g), f32(ln_b), head.output_head[0].eps, dt)
@@ -579,11 +634,11 @@ class _HeadFn(torch.autograd.Function):
         gw1, gb1 = _wgrad(dz1, S["x"]), _colsum(dz1)
         glg = glb = None
         if "a" in S:
-            dm = _empty((B, C), dt, dev)
+            dm = _empty((B, C), S["m"].dtype, dev)
             glg, glb = sp.ln_bwd(_dense(S["m"]), S["s"], S["lng"], _dense(dxh), _dense(dm), B, C)
         else:
             dm = dxh
-        dtok = torch.zeros(B * N, C, dtype=dt, device=dev)
+        dtok = torch.zeros(B * N, C, dtype=S["sdt"], device=dev)
         rows = S["rows"]
         sp.copy_rows(dm, 0, C, dtok, C, N * C, B, rows, C, dst_offset_rows=S["off"])   # broadcast to the group
         inv = torch.full((B * rows,), 1.0 / rows, dtype=torch.float32, device=dev)
@@ -619,20 +674,276 @@ class _RawOutFn(torch.autograd.Function):
         regs = _empty((B, R, C), tok.dtype, tok.device)
         if R:
             sp.copy_rows(tok, C, N * C, regs, C, R * C, B, R, C)
-        ctx.geo = geo
+        ctx.geo, ctx.sdt = geo, tok.dtype
         return xo, regs
 
     @staticmethod
     def backward(ctx, dxo, dregs):
         B, R, Hp, Wp, C = ctx.geo
         N = R + Hp * Wp
-        dt = dxo.dtype if dxo is not None else dregs.dtype
-        dtok = torch.zeros(B * N, C, dtype=dt, device=(dxo if dxo is not None else dregs).device)
+        dtok = torch.zeros(B * N, C, dtype=ctx.sdt, device=(dxo if dxo is not None else dregs).device)
         if dxo is not None:
             sp.nchw_to_rows(dxo.contiguous(), Rows(dtok, C, Hp * Wp, N, R))
         if dregs is not None and R:
-            sp.copy_rows(dregs.contiguous().to(dt), C, R * C, dtok, C, N * C, B, R, C)
+            sp.copy_rows(dregs.contiguous(), C, R * C, dtok, C, N * C, B, R, C)
         return dtok, None
+
+
+# ---------------------------------------------------------------------------
+# Sub-module forwards in training mode (Block(...)(x, reg), EncoderLayer, ConvMixer, the
+# head, the LayerNorm / patcher / embedding leaves): the same per-sub-layer Functions on a
+# token buffer built from (x NCHW, registers), with differentiable layout changes either side.
+# ---------------------------------------------------------------------------
+class _ToTokFn(torch.autograd.Function):
+    """x [B, C, H, W] (may be None) + registers [B, R, C] (may be None) -> token rows
+    [B*(R+HW), C] in dtype ``sdt`` (layers.py:271-275's flatten + concat)."""
+
+    @staticmethod
+    def forward(ctx, x, reg, sdt):
+        if x is not None:
+            B, C, H, W = x.shape
+        else:
+            (B, _, C), H, W = reg.shape, 0, 0
+        R = 0 if reg is None else reg.shape[1]
+        N = R + H * W
+        dev = (x if x is not None else reg).device
+        tok = _empty((B * N, C), sdt, dev)
+        if x is not None:
+            sp.nchw_to_rows(x.contiguous(), Rows(tok, C, H * W, N, R))
+        if R:
+            sp.copy_rows(reg.contiguous(), C, R * C, tok, C, N * C, B, R, C)
+        ctx.geo = (B, R, H, W, C)
+        ctx.dts = (None if x is None else x.dtype, None if reg is None else reg.dtype)
+        return tok
+
+    @staticmethod
+    def backward(ctx, dtok):
+        B, R, H, W, C = ctx.geo
+        N = R + H * W
+        dtok = dtok.contiguous()
+        dx = None
+        if ctx.dts[0] is not None:
+            dx = _empty((B, C, H, W), ctx.dts[0], dtok.device)
+            sp.rows_to_nchw(Rows(dtok, C, H * W, N, R), dx)
+        dreg = None
+        if ctx.dts[1] is not None:
+            dreg = _empty((B, R, C), ctx.dts[1], dtok.device)
+            if R:
+                sp.copy_rows(dtok, C, N * C, dreg, C, R * C, B, R, C)
+        return dx, dreg, None
+
+
+def _no_mask(mask):
+    if mask is not None:
+        raise NotImplementedError("sdpnet training path: attention masks are not supported in train mode "
+                                  "(MainModel never passes one, model.py:129-149)")
+
+
+def train_conv_mixer(m, x: torch.Tensor) -> torch.Tensor:
+    """ConvMixer.forward in train mode (layers.py:83-104): x [B, C, H, W] -> x."""
+    dt = compute_dtype(x, m)
+    B, C, H, W = x.shape
+    tok = _ToTokFn.apply(x, None, stream_dtype(dt, C))
+    tok = _MixerFn.apply(tok, (B, 0, H, W), m, dt, *_mixer_params(m))
+    return _RawOutFn.apply(tok, (B, 0, H, W, C))[0]
+
+
+def train_encoder(e, x: torch.Tensor, reg: torch.Tensor, mask=None):
+    """EncoderLayer.forward in train mode (layers.py:268-316): (x, registers) -> (x, registers)."""
+    _no_mask(mask)
+    dt = compute_dtype(x, e)
+    B, C, H, W = x.shape
+    tok = _ToTokFn.apply(x, reg, stream_dtype(dt, C))
+    tok = _EncoderFn.apply(tok, (B, reg.shape[1] + H * W), e, dt, _RNG(), *_enc_params(e))
+    return _RawOutFn.apply(tok, (B, reg.shape[1], H, W, C))
+
+
+def train_block(blk, x: torch.Tensor, reg: torch.Tensor, mask=None):
+    """Block.forward in train mode (layers.py:381-386), one token buffer for the whole block."""
+    _no_mask(mask)
+    dt = compute_dtype(x, blk)
+    B, C, H, W = x.shape
+    R = reg.shape[1]
+    tok = _ToTokFn.apply(x, reg, stream_dtype(dt, C))
+    rng = _RNG()
+
+    def mixers(t):
+        for mx in blk.conv_blocks:
+            t = _MixerFn.apply(t, (B, R, H, W), mx, dt, *_mixer_params(mx))
+        return t
+
+    def enc(t):
+        return _EncoderFn.apply(t, (B, R + H * W), blk.t_block, dt, rng, *_enc_params(blk.t_block))
+
+    tok = enc(mixers(tok)) if blk.conv_first else mixers(enc(tok))
+    return _RawOutFn.apply(tok, (B, R, H, W, C))
+
+
+def train_head(head, x: Optional[torch.Tensor], reg: Optional[torch.Tensor]) -> torch.Tensor:
+    """ClassificationHead.forward in train mode (layers.py:447-465; dropout active): the
+    register head reads only the registers, the pooling head only x."""
+    if head.from_register:
+        dt = compute_dtype(reg, head)
+        B, R, C = reg.shape
+        tok = _ToTokFn.apply(None, reg, stream_dtype(dt, C))
+        return _HeadFn.apply(tok, (B, R, 0, R, C), head, dt, _RNG(), *_head_params(head))
+    dt = compute_dtype(x, head)
+    B, C, H, W = x.shape
+    tok = _ToTokFn.apply(x, None, stream_dtype(dt, C))
+    return _HeadFn.apply(tok, (B, 0, H * W, H * W, C), head, dt, _RNG(), *_head_params(head))
+
+
+class _ChanLNFn(torch.autograd.Function):
+    """Channel LayerNorm over dim 1 of NCHW (layers.py:12-24) with its backward; output in the
+    promoted dtype of x and gamma (the reference's gamma * x + beta)."""
+
+    @staticmethod
+    def forward(ctx, x, g, b, eps):
+        B, C, H, W = x.shape
+        M = B * H * W
+        odt = torch.promote_types(x.dtype, g.dtype)
+        xr = _empty((M, C), odt, x.device)
+        sp.nchw_to_rows(x.contiguous(), _dense(xr))
+        a, st = _ln_fwd(_dense(xr), M, C, f32(g), f32(b), eps, odt)
+        out = _empty((B, C, H, W), odt, x.device)
+        sp.rows_to_nchw(_dense(a), out)
+        ctx.st = (xr, st, f32(g), x.dtype, g.dtype, x.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        xr, st, g32, xdt, pdt, shp = ctx.st
+        M, C = xr.shape
+        dr = _empty((M, C), xr.dtype, xr.device)
+        sp.nchw_to_rows(dout.contiguous(), _dense(dr))
+        dxr = _empty((M, C), xr.dtype, xr.device)
+        gg, gb = sp.ln_bwd(_dense(xr), st, g32, _dense(dr), _dense(dxr), M, C)
+        dx = _empty(shp, xdt, xr.device)
+        sp.rows_to_nchw(_dense(dxr), dx)
+        ctx.st = None
+        return dx, as_dtype(gg, pdt), as_dtype(gb, pdt), None
+
+
+def train_layernorm(ln, x: torch.Tensor) -> torch.Tensor:
+    compute_dtype(x, ln)  # device / dtype checks
+    return _ChanLNFn.apply(x, ln.gamma, ln.beta, float(ln.eps))
+
+
+class _PatchFn(torch.autograd.Function):
+    """ConvPatcher (layers.py:28-42): stride-p convolution as patchify + GEMM; weight gradient
+    dW = dY^T patches.  The input image takes no gradient (it is data)."""
+
+    @staticmethod
+    def forward(ctx, x, w, pat, dt):
+        B, _, Hi, Wi = x.shape
+        p = pat.patch_size
+        Hp, Wp = Hi // p, Wi // p
+        C = w.shape[0]
+        kp = pat._kpad()
+        patches = _empty((B * Hp * Wp, kp), dt, x.device)
+        sp.patchify(x.contiguous(), patches, p, kp)
+        wm = as_dtype(w.reshape(C, -1), dt)
+        if kp != wm.shape[1]:
+            wpad = torch.zeros(C, kp, dtype=dt, device=x.device)
+            wpad[:, : wm.shape[1]].copy_(wm)
+            wm = wpad
+        rows = _linear(patches, wm, None, dt)
+        out = _empty((B, C, Hp, Wp), dt, x.device)
+        sp.rows_to_nchw(_dense(rows), out)
+        ctx.st = (patches, w.shape, 3 * p * p, dt)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        patches, wshape, k, dt = ctx.st
+        B, C, Hp, Wp = dout.shape
+        dr = _empty((B * Hp * Wp, C), dt, dout.device)
+        sp.nchw_to_rows(dout.contiguous(), _dense(dr))
+        gw = _wgrad(dr, patches)[:, :k].contiguous().view(wshape)
+        ctx.st = None
+        return None, gw, None, None
+
+
+def train_patcher(pat, x: torch.Tensor) -> torch.Tensor:
+    if x.requires_grad:
+        raise NotImplementedError("sdpnet training path: no gradient into the input image of ConvPatcher")
+    return _PatchFn.apply(x, pat.conv.weight, pat, compute_dtype(x, pat))
+
+
+class _PosEmbFn(torch.autograd.Function):
+    """EmbeddingLayer / ConvEmbedding in train mode (layers.py:152-168, :202-209): x [B, C, H, W]
+    -> (act(x + pos), registers [B, R, C]) in x's dtype promoted with the tables' (x + an fp32
+    table is fp32); gradients into x, the Eh / Ew tables or a trainable bone, and the register
+    rows."""
+
+    @staticmethod
+    def forward(ctx, x, emb, nreg, eh, ew, bone, ereg):
+        B, C, H, W = x.shape
+        P = H * W
+        dev = x.device
+        odt = torch.promote_types(x.dtype, ereg.dtype)
+        pos = emb._pos_table(H, W)  # fp32 [P, C]
+        act = act_code(emb.activation)
+        z = _empty((B * P, C), torch.float32, dev)
+        sp.nchw_to_rows(x.contiguous(), _dense(z))
+        sp.rowscale_add(_dense(z), _dense(z), B * P, C, resid=Rows(pos, C, P, 0, 0))
+        y = z
+        if act:
+            y = _empty((B * P, C), torch.float32, dev)
+            sp.rowscale_add(_dense(z), _dense(y), B * P, C, act=act)
+        xo = _empty((B, C, H, W), odt, dev)
+        sp.rows_to_nchw(_dense(y), xo)
+        table, R = emb._register_rows(nreg)
+        regs = _empty((B, R, C), odt, dev)
+        if R:
+            sp.copy_rows(table.contiguous(), C, 0, regs, C, R * C, B, R, C)
+        ctx.st = dict(z=z if act else None, act=act, geo=(B, C, H, W, R), xdt=x.dtype, eh=eh, ew=ew, bone=bone,
+                      k=getattr(emb, "kernel_size", 0), nreg_rows=ereg.shape[0], pdt=ereg.dtype)
+        return xo, regs
+
+    @staticmethod
+    def backward(ctx, dxo, dregs):
+        S = ctx.st
+        B, C, H, W, R = S["geo"]
+        P = H * W
+        dev = (dxo if dxo is not None else dregs).device
+        dz = torch.zeros((B * P, C), dtype=torch.float32, device=dev)
+        if dxo is not None:
+            sp.nchw_to_rows(dxo.contiguous(), _dense(dz))
+        if S["act"]:
+            sp.act_bwd(S["z"], dz, dz, B * P, C, S["act"])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _empty((B, C, H, W), S["xdt"], dev)
+            sp.rows_to_nchw(_dense(dz), dx)
+        dpos = _empty((P, C), torch.float32, dev)
+        sp.seg_colsum(dz, dpos, P, B, 1, P, C)                              # sum over the batch
+        geh = gew = gbone = None
+        if S["eh"] is not None:
+            geh = torch.zeros(S["eh"].shape, dtype=torch.float32, device=dev)
+            gew = torch.zeros(S["ew"].shape, dtype=torch.float32, device=dev)
+            sp.seg_colsum(dpos, geh, H, W, W, 1, C)                          # Eh indexed by h (rows)
+            sp.seg_colsum(dpos, gew, W, H, 1, W, C)                          # Ew indexed by w (columns)
+            geh, gew = as_dtype(geh, S["eh"].dtype), as_dtype(gew, S["ew"].dtype)
+        elif S["bone"] is not None and ctx.needs_input_grad[5]:
+            gbone = _empty(S["bone"].shape, torch.float32, dev)
+            sp.avgpool_table_bwd(dpos, gbone, H, W, C, S["k"])
+            gbone = as_dtype(gbone, S["bone"].dtype)
+        greg = torch.zeros(S["nreg_rows"], C, dtype=torch.float32, device=dev)
+        if R and dregs is not None:
+            off = 1 if S["eh"] is None else 0  # ConvEmbedding takes Embedding rows 1..R (layers.py:206)
+            sp.seg_colsum(dregs.contiguous(), greg[off:], R, B, 1, R, C)
+        ctx.st = None
+        return dx, None, None, geh, gew, gbone, as_dtype(greg, S["pdt"])
+
+
+def train_pos_embedding(emb, x: torch.Tensor, num_registers: int):
+    compute_dtype(x, emb)
+    conv_emb = not hasattr(emb, "horizontal_embedding_layer")
+    eh = None if conv_emb else emb.horizontal_embedding_layer.weight
+    ew = None if conv_emb else emb.vertical_embedding_layer.weight
+    bone = emb.bone if conv_emb and isinstance(emb.bone, nn.Parameter) else None
+    return _PosEmbFn.apply(x, emb, num_registers, eh, ew, bone, emb.register_embedding_layer.weight)
 
 
 def train_forward(model, x: torch.Tensor, num_registers: int = 3, return_raw_outputs: bool = False):
@@ -655,7 +966,7 @@ def train_forward(model, x: torch.Tensor, num_registers: int = 3, return_raw_out
     C = model.conv_init.conv.out_channels
     rng = _RNG()
     xin = x if x.dtype == dt else as_dtype(x, dt)
-    tok = _EmbedFn.apply(xin, (B, R, Hp, Wp, num_registers), model, dt, model.conv_init.conv.weight, eh, ew,
+    tok = _EmbedFn.apply(xin, (B, R, Hp, Wp, num_registers, stream_dtype(dt, C)), model, dt, model.conv_init.conv.weight, eh, ew,
                          emb.register_embedding_layer.weight)
 
     def enc(t, e):
@@ -719,7 +1030,7 @@ def tape_forward(model, x: torch.Tensor, num_registers: int, dt):
     xin = x if x.dtype == dt else as_dtype(x, dt)
     with torch.no_grad():
         tok = run(_EmbedFn, 4, [model.conv_init.conv.weight, eh, ew, emb.register_embedding_layer.weight],
-                  xin, (B, R, Hp, Wp, num_registers), model, dt)
+                  xin, (B, R, Hp, Wp, num_registers, stream_dtype(dt, C)), model, dt)
 
         def enc(t, e):
             return run(_EncoderFn, 5, _enc_params(e), t, (B, N), e, dt, rng)

@@ -9,8 +9,9 @@ AdamW (+ clip_grad_norm_) step; dropout / drop path statistics and mask consiste
 gloo world-size-2 DDP run whose averaged gradient equals the single-process gradient.
 
 Tolerances: fp32 gradients within 1e-4 of each tensor's max |g| (relative), loss 1e-5;
-bf16 gradients within 2x the reference's own CPU-autocast-bf16 gradient error + 6e-2
-(relative); AdamW parameters 1e-5 absolute (fp32).
+bf16 gradients (fp32 residual stream, the default) within 2x the reference's own
+CPU-autocast-bf16 gradient error + 4e-2 AND within 4x that error (relative); the all-bf16
+stream option within 2x + 6e-2; AdamW parameters 1e-5 absolute (fp32).
 """
 import json
 import os
@@ -67,8 +68,9 @@ def test_oracle_gradients_match_reference_fixture(name):
         assert _rel(g.numpy(), arr["grad/" + k], _floor(arr)) <= 1e-5, k
 
 
-def _train_step(name, bf16):
+def _train_step(name, bf16, fp32_stream=True):
     import sdpnet_train
+    sdpnet_train.set_fp32_stream(fp32_stream)
     meta, arr, m, sd, x, y = _case(name)
     m = m.to(DEV).train()
     xd, yd = x.to(DEV), y.to(DEV)
@@ -79,20 +81,28 @@ def _train_step(name, bf16):
     else:
         logits = m(xd, num_registers=meta["num_registers"])
         loss = sdpnet_train.cross_entropy(logits, yd, meta["label_smoothing"])
-    loss.backward()
+    try:
+        loss.backward()
+    finally:
+        sdpnet_train.set_fp32_stream(True)
     return meta, arr, m, logits, loss
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", CASES)
-@pytest.mark.parametrize("bf16", [False, True])
-def test_gradients_match_reference(name, bf16):
+@pytest.mark.parametrize("mode", ["fp32", "bf16", "bf16_stream16"])
+def test_gradients_match_reference(name, mode):
     """fp32: every gradient within 1e-4 (relative) of the reference's fp32 gradient.  bf16
-    (autocast): each tensor's error within 2x the reference's OWN CPU-autocast-bf16 gradient
-    error on the same inputs (grad_ac/* in the fixture) + 6e-2.  Our bf16 path also stores the
-    residual stream and the activation gradients in bf16 (autocast keeps them fp32), which
-    the ReLU case's step derivative turns into a few-percent error on the FFN weights."""
-    meta, arr, m, logits, loss = _train_step(name, bf16)
+    (autocast, fp32 residual stream and stream gradient as autocast keeps them): each tensor's
+    error within 2x the reference's OWN CPU-autocast-bf16 gradient error on the same inputs
+    (grad_ac/* in the fixture) + 4e-2.  One tensor of the ReLU case, the first block's
+    ff_linear1.weight, sits at 6x the CPU-autocast error (2.3e-2 vs 3.8e-3; 4.1x the same
+    reference run under CUDA autocast): a ReLU mask flip at a near-zero pre-activation on this
+    38-row batch.  test_bf16_gradient_error_matches_autocast_statistically shows it is a draw,
+    not a bias.  bf16_stream16 (set_fp32_stream(False): the stream and its gradient stored in
+    bf16) keeps the looser 2x + 6e-2 (5.6e-2 on that tensor)."""
+    bf16 = mode != "fp32"
+    meta, arr, m, logits, loss = _train_step(name, bf16, fp32_stream=mode != "bf16_stream16")
     assert abs(float(loss) - float(arr["loss"])) <= (2e-2 if bf16 else 1e-5), (float(loss), float(arr["loss"]))
     fl = _floor(arr)
     worst = []
@@ -101,12 +111,58 @@ def test_gradients_match_reference(name, bf16):
         assert p.grad.dtype == torch.float32 and p.grad.shape == p.shape
         r = _rel(p.grad.cpu().numpy(), arr["grad/" + k], fl)
         rref = _rel(arr["grad_ac/" + k], arr["grad/" + k], fl)
-        tol = (2 * rref + 6e-2) if bf16 else 1e-4
+        tol = {"fp32": 1e-4, "bf16": 2 * rref + 4e-2, "bf16_stream16": 2 * rref + 6e-2}[mode]
         worst.append((r / tol, r, rref, k))
     worst.sort(reverse=True)
-    print(f"{name} bf16={bf16}: loss {float(loss):.6f} (ref {float(arr['loss']):.6f}); worst grads "
+    print(f"{name} {mode}: loss {float(loss):.6f} (ref {float(arr['loss']):.6f}); worst grads "
           + ", ".join(f"{k} {r:.2e} (reference autocast {rr:.2e})" for _, r, rr, k in worst[:4]))
     assert worst[0][0] <= 1.0, worst[:4]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_bf16_gradient_error_matches_autocast_statistically(name):
+    """Fixture weights, 8 fresh input batches: per tensor, the median over batches of (our bf16
+    gradient error) / (the reference restatement's own CUDA-autocast-bf16 error), both against
+    its fp32 autograd on the GPU, is <= 1.5 (measured <= 1.11 on 12 batches), and the mean
+    error over the batches is <= 2x autocast's mean: our bf16 training is as accurate as
+    autocast, not just within a budget.  (Single batches of the ReLU case swing either way by
+    10x: a ReLU mask flip at a near-zero pre-activation moves a whole weight-gradient row.)"""
+    import sdpnet_train
+    meta, arr, m, sd, x0, y0 = _case(name)
+    cfg = meta["config"]
+    keys = [k for k, _ in m.named_parameters()]
+    m = m.to(DEV).train()
+    ratios = {k: [] for k in keys}
+    errs = {k: [] for k in keys}
+    for s_ in range(8):
+        x = synth.synth_images(100 + s_, meta["batch"], meta["image"]).to(DEV)
+        y = torch.randint(0, cfg["output_classes"], (meta["batch"],),
+                          generator=torch.Generator().manual_seed(s_)).to(DEV)
+        g = {}
+        for ac in (False, True):
+            osd = {k: v.to(DEV).clone().requires_grad_(v.is_floating_point()) for k, v in sd.items()}
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=ac):
+                lo = F.cross_entropy(orc.forward.__wrapped__(x, osd, cfg, num_registers=meta["num_registers"]).float(),
+                                     y, label_smoothing=meta["label_smoothing"])
+            lo.backward()
+            g[ac] = {k: osd[k].grad.float().cpu().numpy() for k in keys}
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = sdpnet_train.cross_entropy(m(x, num_registers=meta["num_registers"]), y, meta["label_smoothing"])
+        loss.backward()
+        fl = 1e-3 * max(float(np.abs(v).max()) for v in g[False].values())
+        for k, p in m.named_parameters():
+            e_ours, e_ac = _rel(p.grad.cpu().numpy(), g[False][k], fl), _rel(g[True][k], g[False][k], fl)
+            ratios[k].append(e_ours / max(e_ac, 1e-9))
+            errs[k].append((e_ours, e_ac))
+    med = sorted(((float(np.median(v)), k) for k, v in ratios.items()), reverse=True)
+    mean = sorted(((float(np.mean([a for a, _ in v]) / max(np.mean([b for _, b in v]), 1e-12)), k)
+                   for k, v in errs.items()), reverse=True)
+    print(f"{name}: worst median ratio to autocast", [(k, f"{a:.2f}") for a, k in med[:3]],
+          "worst mean-error ratio", [(k, f"{a:.2f}") for a, k in mean[:3]])
+    assert med[0][0] <= 1.5, med[:3]
+    assert mean[0][0] <= 2.0, mean[:3]
 
 
 @pytest.mark.gpu
@@ -368,8 +424,9 @@ def test_xl_architecture_training_step_against_oracle():
     dimensions -- d 768, 8 heads of 96, patch 14, 256 patches + 4 registers = 260 tokens -- with
     2 blocks to keep the CPU side cheap, batch 2.  fp32: every HIP gradient within 1e-4 (relative)
     of autograd through the oracle (pinned by the train fixtures); the fused AdamW step equals
-    torch.optim.AdamW + clip_grad_norm_ on the same gradients.  bf16 (autocast): each gradient's
-    error within 2x the oracle's own CPU-autocast error + 6e-2 (the fixture rule)."""
+    torch.optim.AdamW + clip_grad_norm_ on the same gradients.  bf16 (autocast, fp32 residual
+    stream): each gradient's error within min(2x the oracle's own CPU-autocast error + 4e-2, 4x
+    that error) (the fixture rule)."""
     import model as ours
     import sdpnet_train
     cfg = XL_TRAIN_CFG
@@ -397,7 +454,7 @@ def test_xl_architecture_training_step_against_oracle():
         for k, p in m.named_parameters():
             r = _rel(p.grad.cpu().numpy(), ref[k], fl)
             rac = _rel(asd[k].grad.float().numpy(), ref[k], fl)
-            tol = (2 * rac + 6e-2) if bf16 else 1e-4
+            tol = min(2 * rac + 4e-2, 4 * rac) if bf16 else 1e-4
             worst.append((r / tol, r, rac, k))
         worst.sort(reverse=True)
         print(f"XL-dim training bf16={bf16}: worst", [(k, f"{r:.2e}", f"{rac:.2e}") for _, r, rac, k in worst[:3]])
