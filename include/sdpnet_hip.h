@@ -66,6 +66,15 @@ int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride
  *   part != NULL: part[(phys_out_row * ceil(N/64) + c) * 2 + {0,1}] = {mean, M2}
  *   of the stored output row's columns [64c, 64c+64) (combine with sdp_ln_stats).
  */
+/* Training GEMM epilogues on the fast kernel (bf16, dense rows; training_tools.py:77-103 with
+ * layers.py:83-91 / :306-309): mode 1: Y = X W^T + bias and Y2 = dropout_p(act(Y)) (the
+ * ConvMixer up-projection / FFN first layer with sdp_act_fwd fused); mode 2: Y = dropout_p(X W^T)
+ * * act'(Z) (the input gradient of the next layer with sdp_act_bwd fused; no bias).  Masks as
+ * sdp_act_fwd / sdp_act_bwd (index m * N + n, same seed).  Returns hipErrorNotSupported
+ * without launching when the fast kernel does not take the shape or alignment. */
+int sdp_gemm_train_epi(int mode, const void* X, int64_t ldx, const void* W, int64_t ldw, const float* bias,
+                       const void* Z, int64_t ldz, void* Y, int64_t ldy, void* Y2, int64_t ldy2, int M, int N, int K,
+                       int act, float p, uint64_t seed, void* stream);
 int sdp_gemm_ln(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
                 const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
                 int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
@@ -382,7 +391,7 @@ int sdp_softmax_bwd(int dtype, const void* P, int64_t ldp, const void* DPd, int6
 
 /* Depthwise-conv weight gradient (layers.py:73-78): part[chunk][c][t] = sum over the chunk's
  * images of DY[b, h, w, c] * A[b, h + ty - k/2, w + tx - k/2, c] (zero padded), NHWC rows,
- * chunk < sdp_dw_wgrad_chunks(B); H * W <= 256, odd k <= 9.  The input gradient is
+ * chunk < sdp_dw_wgrad_chunks(B); H * W <= 640 (bf16) / 320 (fp32), any W, odd k <= 9.  The input gradient is
  * sdp_dwconv with the kernel flipped. */
 int sdp_dw_wgrad_chunks(int B);
 int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, int64_t a_gstride, int a_off, const void* DY,

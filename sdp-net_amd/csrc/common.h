@@ -78,6 +78,47 @@ SDP_DEV float apply_act(int act, float x) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// counter-hash RNG for dropout / drop-path masks: keep(seed, idx) = u(seed, idx) >= p
+// ---------------------------------------------------------------------------
+SDP_DEV uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+SDP_DEV float uniform01(uint64_t seed, uint64_t idx) {
+  const uint32_t h = mix32((uint32_t)idx ^ mix32((uint32_t)seed ^ mix32((uint32_t)(idx >> 32) + (uint32_t)(seed >> 32) * 0x9e3779b9U)));
+  return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+// act'(x) of apply_act (training backward; exact-erf GELU).
+SDP_DEV float act_grad(int act, float x) {
+  switch (act) {
+    case ACT_GELU: {
+      const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+      return cdf + x * 0.3989422804014327f * expf(-0.5f * x * x);
+    }
+    case ACT_RELU: return x > 0.0f ? 1.0f : 0.0f;
+    case ACT_TANH: { const float t = tanhf(x); return 1.0f - t * t; }
+    case ACT_SIGMOID: { const float s = 1.0f / (1.0f + expf(-x)); return s * (1.0f - s); }
+    case ACT_LEAKY_RELU: return x > 0.0f ? 1.0f : 0.01f;
+    case ACT_SELU: {
+      const float alpha = 1.6732632423543772848f, scale = 1.0507009873554804934f;
+      return x > 0.0f ? scale : scale * alpha * expf(x);
+    }
+    case ACT_KELU: {
+      const float a = 3.5f, k = 3.14159265358979323846f / a;
+      if (x < -a) return 0.0f;
+      if (x > a) return 1.0f;
+      return 0.5f * (1.0f + 2.0f * x / a + 0.31830988618379067f * sinf(k * x) + x * cosf(k * x) / a);
+    }
+    default: return 1.0f;
+  }
+}
+
 // Grouped row map: logical row m -> physical row (m / grp) * gstride + off + (m % grp).
 // Lets one kernel address the image rows of a [B, R+P, C] token buffer (grp=P,
 // gstride=R+P, off=R), a plain dense matrix (grp=huge, gstride=0, off=0), or a

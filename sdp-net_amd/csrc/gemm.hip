@@ -29,6 +29,7 @@
 // access (bias, residual, output) is an 8/16-byte vector per lane.
 #include "common.h"
 #include <mutex>
+#include <type_traits>
 
 
 template <typename T>
@@ -51,6 +52,15 @@ struct Epi {
   float* part;
   int nt_store = 0;  // whole-line epilogue: non-temporal (streaming) output stores
   int group_m = 1;   // 8ph tile raster: M-blocks per group (1 = row-major tiles)
+  // training epilogues (EPI 5 / 6 of the 8-phase kernel, dense rows), act2 / p2 / seed2 as
+  // sdp_act_fwd / sdp_act_bwd (mask index m * N + n):
+  //   EPI 5: out = z (pre-activation), out2[m * ld2 + n] = dropout(act2(z))
+  //   EPI 6: out = dropout(acc) * act2'(resid)       (resid = the stored pre-activation z)
+  T* out2 = nullptr;
+  int64_t ld2 = 0;
+  int act2 = 0;
+  float p2 = 0.f;
+  uint64_t seed2 = 0;
 };
 
 // fold: v = r * acc + (b - r * mu * s) for one element (generic paths)
@@ -318,7 +328,19 @@ struct RowWalk {
   }
 };
 
-template <int ACT, int JB = 4, bool ALL = false>
+// f(std::integral_constant<int, I>) for I = B .. E-1, unrolled by construction (a plain
+// `#pragma unroll` gives up once the body is large, and the arrays it indexes go to scratch).
+template <int B, int E, typename F>
+SDP_DEV void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// TRN 1 / 2 (training epilogues, EPI 5 / 6): rows are staged without an activation and ACT is
+// the activation of the training epilogue (-1: epi.act2 at run time).
+template <int ACT, int JB = 4, bool ALL = false, int TRN = 0>
 SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int M, int N, int wm,
                                 int wn, int lane, int fr, int fq, char* stg) {
   // Ragged tiles take the same arithmetic with masked rows / 8-column chunks
@@ -385,7 +407,9 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
         } else {
           x2 = f32x2{v[e], v[e + 1]} + b2;
         }
-        if constexpr (ACT == ACT_GELU) {
+        if constexpr (TRN != 0) {
+          // stored pre-activation z: no activation in the staging
+        } else if constexpr (ACT == ACT_GELU) {
           x2 = gelu_fast2(x2);
         } else {
           x2.x = epi_act<ACT>(epi.act, x2.x);
@@ -405,17 +429,37 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
     for (int q = 0; q < 2; ++q) {
       const int r = rlo + 8 * q;
       bf16x8 o = *(const bf16x8*)(sl + r * 128 + ((ch ^ (r & 7)) << 4));
-      if (epi.resid) {
+      const int m = mb + j * 16 + 8 * q;
+      if constexpr (TRN == 2) {  // dz = dropout(bf16 dh) * act'(z): sdp_act_bwd's arithmetic on the stored dh
+        const float inv = epi.p2 > 0.f ? 1.0f / (1.0f - epi.p2) : 1.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float d = bf2f((bf16_t)o[e]);
+          if (epi.p2 > 0.f) d = uniform01(epi.seed2, (uint64_t)m * N + col + e) >= epi.p2 ? d * inv : 0.f;
+          const int a2 = ACT >= 0 ? ACT : epi.act2;
+          o[e] = (short)f2bf(a2 == ACT_NONE ? d : d * act_grad(a2, bf2f((bf16_t)rr[q][e])));
+        }
+      } else if (epi.resid) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(bf2f((bf16_t)o[e]) + bf2f((bf16_t)rr[q][e]));
       }
-      const int m = mb + j * 16 + 8 * q;
       const int64_t prow = ow.phys();
       ow.step8();
       if (m < M && col_ok) {
         bf16x8* dst = (bf16x8*)(epi.out + (uint64_t)prow * (uint32_t)epi.ldc + col);
         if (epi.nt_store) __builtin_nontemporal_store(o, dst);
         else *dst = o;
+      }
+      if constexpr (TRN == 1) {  // h = dropout(act(z)) from the stored z: sdp_act_fwd's arithmetic
+        const float inv = epi.p2 > 0.f ? 1.0f / (1.0f - epi.p2) : 1.0f;
+        bf16x8 h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float v = apply_act(ACT >= 0 ? ACT : epi.act2, bf2f((bf16_t)o[e]));
+          if (epi.p2 > 0.f) v = uniform01(epi.seed2, (uint64_t)m * N + col + e) >= epi.p2 ? v * inv : 0.f;
+          h[e] = (short)f2bf(v);
+        }
+        if (m < M && col_ok) *(bf16x8*)(epi.out2 + (uint64_t)m * (uint64_t)epi.ld2 + col) = h;
       }
       if (epi.part) {  // {mean, M2} of the row's 64 stored columns (8 lanes x 8)
         float f[8], sum = 0.f;
@@ -458,14 +502,9 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
     }
   };
   if constexpr (ALL) {
-    if (epi.resid) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) load_res(j, j);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) stage(j);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) drain(j, rres[j]);
+    if (epi.resid) static_for<0, 8>([&](auto j) { load_res(j, j); });
+    static_for<0, 8>([&](auto j) { stage(j); });
+    static_for<0, 8>([&](auto j) { drain(j, rres[j]); });
   } else {
 #pragma unroll
     for (int j0 = 0; j0 < 8; j0 += JB) {
@@ -816,6 +855,8 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     // per wave: both K buffers, free once the balancing barrier above has passed); the host
     // routes resid_pre-with-activation and unaligned calls to EPI 1
     tile_epilogue_rows<ACT, 4, true>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + wave * 16384);
+  } else if constexpr (EPI == 5 || EPI == 6) {  // training epilogues (same staging)
+    tile_epilogue_rows<ACT, 4, true, EPI - 4>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + wave * 16384);
   } else {
     tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
   }
@@ -1066,6 +1107,55 @@ extern "C" int sdp_gemm(int dtype, const void* X, int64_t ldx, int x_grp, int64_
                         void* stream) {
   return gemm_impl(dtype, X, ldx, x_grp, x_gstride, x_off, W, ldw, bias, R, ldr, r_grp, r_gstride, r_off, Y, ldy,
                    y_grp, y_gstride, y_off, M, N, K, act, resid_pre, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+// Training GEMM epilogues on the 8-phase kernel (bf16, dense rows).  mode 1: Y = X W^T + bias
+// and Y2 = dropout(act(Y)) (sdp_act_fwd fused: the activation input is not re-read);
+// mode 2: Y = dropout(X W^T) * act'(Z) (sdp_act_bwd fused into the input-gradient GEMM; no
+// bias).  hipErrorNotSupported when the fast kernel does not take the shape / alignment (the
+// caller then runs the GEMM and the activation kernel separately).
+extern "C" int sdp_gemm_train_epi(int mode, const void* X, int64_t ldx, const void* W, int64_t ldw,
+                                  const float* bias, const void* Z, int64_t ldz, void* Y, int64_t ldy, void* Y2,
+                                  int64_t ldy2, int M, int N, int K, int act, float p, uint64_t seed,
+                                  void* stream) {
+  if (M < 0 || N <= 0 || K <= 0 || !X || !W || !Y || act < 0 || act > ACT_KELU || p < 0.f || p >= 1.f)
+    return (int)hipErrorInvalidValue;
+  if ((mode == 1 && (!Y2 || Z)) || (mode == 2 && (!Z || Y2 || bias)) || (mode != 1 && mode != 2))
+    return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  auto a16 = [](const void* q) { return (uintptr_t)q % 16 == 0; };
+  const bool ok = !g_force_generic && sdp_gemm_variant(1, M, N, K) == 1 && N % 8 == 0 && ldx % 8 == 0 &&
+                  ldw % 8 == 0 && ldy % 8 == 0 && a16(X) && a16(W) && a16(Y) && (!bias || a16(bias)) &&
+                  (mode != 1 || (ldy2 % 8 == 0 && a16(Y2))) && (mode != 2 || (ldz % 8 == 0 && a16(Z)));
+  if (!ok) return (int)hipErrorNotSupported;
+  const RowMap dm = mk_map(0, 0, 0);
+  Epi<bf16_t> e{bias, (const bf16_t*)Z, ldz, dm, (bf16_t*)Y, ldy, dm, ACT_NONE, 0, nullptr, nullptr, nullptr};
+  e.nt_store = g_nt_store;
+  const int tm = (M + fast::BM - 1) / fast::BM, tn = (N + fast::BN - 1) / fast::BN;
+  e.group_m = g_group_m >= 1 ? g_group_m : (tn >= 12 ? 8 : 1);
+  e.out2 = (bf16_t*)Y2;
+  e.ld2 = ldy2;
+  e.act2 = act;
+  e.p2 = p;
+  e.seed2 = seed;
+  const fast::SkArgs sk{};
+  hipStream_t s = (hipStream_t)stream;
+  // the model's activations get their own instantiation (the activation folds at compile
+  // time); any other code goes through the run-time switch on epi.act2
+#define SDP_TRN(A, E)                                                                                           \
+  hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,             \
+                     (const bf16_t*)X, ldx, dm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk)
+  if (mode == 1) {
+    if (act == ACT_GELU) SDP_TRN(ACT_GELU, 5);
+    else if (act == ACT_RELU) SDP_TRN(ACT_RELU, 5);
+    else SDP_TRN(-1, 5);
+  } else {
+    if (act == ACT_GELU) SDP_TRN(ACT_GELU, 6);
+    else if (act == ACT_RELU) SDP_TRN(ACT_RELU, 6);
+    else SDP_TRN(-1, 6);
+  }
+#undef SDP_TRN
+  return SDP_CHECK_LAUNCH();
 }
 
 extern "C" int sdp_gemm_ln(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,

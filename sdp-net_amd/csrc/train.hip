@@ -33,21 +33,6 @@ static RowMap mk_tmap(int grp, int64_t gstride, int off) {
   return r;
 }
 
-// ---------------------------------------------------------------------------
-// counter-hash RNG for dropout / drop-path masks: keep(seed, idx) = u(seed, idx) >= p
-// ---------------------------------------------------------------------------
-SDP_DEV uint32_t mix32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7feb352dU;
-  x ^= x >> 15;
-  x *= 0x846ca68bU;
-  x ^= x >> 16;
-  return x;
-}
-SDP_DEV float uniform01(uint64_t seed, uint64_t idx) {
-  const uint32_t h = mix32((uint32_t)idx ^ mix32((uint32_t)seed ^ mix32((uint32_t)(idx >> 32) + (uint32_t)(seed >> 32) * 0x9e3779b9U)));
-  return (float)(h >> 8) * (1.0f / 16777216.0f);
-}
 
 // ---------------------------------------------------------------------------
 // gemm_flex
@@ -422,29 +407,6 @@ extern "C" int sdp_seg_colsum(int dtype, const void* X, int64_t ldx, int G, int 
 //   bwd: dz = dy * (keep ? 1 / (1 - p) : 0) * act'(z)
 // keep = uniform01(seed, m * N + n) >= p.  Exact-erf GELU (nn.GELU(), model.py:15).
 // ---------------------------------------------------------------------------
-SDP_DEV float act_grad(int act, float x) {
-  switch (act) {
-    case ACT_GELU: {
-      const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-      return cdf + x * 0.3989422804014327f * expf(-0.5f * x * x);
-    }
-    case ACT_RELU: return x > 0.0f ? 1.0f : 0.0f;
-    case ACT_TANH: { const float t = tanhf(x); return 1.0f - t * t; }
-    case ACT_SIGMOID: { const float s = 1.0f / (1.0f + expf(-x)); return s * (1.0f - s); }
-    case ACT_LEAKY_RELU: return x > 0.0f ? 1.0f : 0.01f;
-    case ACT_SELU: {
-      const float alpha = 1.6732632423543772848f, scale = 1.0507009873554804934f;
-      return x > 0.0f ? scale : scale * alpha * expf(x);
-    }
-    case ACT_KELU: {
-      const float a = 3.5f, k = 3.14159265358979323846f / a;
-      if (x < -a) return 0.0f;
-      if (x > a) return 1.0f;
-      return 0.5f * (1.0f + 2.0f * x / a + 0.31830988618379067f * sinf(k * x) + x * cosf(k * x) / a);
-    }
-    default: return 1.0f;
-  }
-}
 
 // 8 consecutive elements of a row per work item (16-B bf16 / 2 x 16-B fp32 accesses); the
 // host takes this form when N % 8 == 0 and every row stride / base is 8-element aligned.
@@ -1473,18 +1435,21 @@ extern "C" int sdp_softmax_bwd(int dtype, const void* P, int64_t ldp, const void
 // planes of one image staged in LDS as fp32 [pixel][64].  Reduce the chunk slabs with
 // sdp_seg_colsum.
 // ---------------------------------------------------------------------------
-// Thread (channel cl, tap row ty): for every output row h it loads the 16-wide DY row and the
-// (16 + KS - 1)-wide zero-padded A row hh = h + ty - KS/2 into registers once and does the
-// KS x W FMAs of that row pair from registers (LDS reads per FMA ~ 1/3.5 instead of 2).
+// Thread (channel cl, tap row ty): for every output row h (in 16-column segments) it loads the
+// 16-wide DY row and the (16 + KS - 1)-wide zero-padded A row hh = h + ty - KS/2 into registers
+// once and does the KS x 16 FMAs of that row pair from registers.  Both planes are staged in
+// the input dtype (bf16: 2 x HW x 128 B = 64 KiB at 16 x 16, so two workgroups share a CU and one
+// stages while the other computes), with all of a thread's staging loads of an image issued
+// before its LDS stores.
 template <typename T, int KS>
 __global__ __launch_bounds__(64 * KS) void dw_wgrad_k(const T* __restrict__ A, int64_t lda, RowMap am,
                                                       const T* __restrict__ DY, int64_t lddy, RowMap dym, int B, int H,
                                                       int W, int C, int ipb, float* __restrict__ part) {
-  extern __shared__ float sm[];
-  constexpr int P = KS / 2, MW = 16;
+  extern __shared__ __attribute__((aligned(16))) char dw_sm[];
+  constexpr int P = KS / 2, MW = 16, NT = 64 * KS, U = 4;
   const int HW = H * W;
-  float* ap = sm;            // [HW][64]
-  float* dp = sm + HW * 64;  // [HW][64]
+  T* ap = (T*)dw_sm;   // [HW][64]
+  T* dp = ap + HW * 64;  // [HW][64]
   const int c0 = blockIdx.x * 64, chunk = blockIdx.y;
   const int cl = threadIdx.x & 63, ty = threadIdx.x / 64;
   float acc[KS];
@@ -1495,42 +1460,52 @@ __global__ __launch_bounds__(64 * KS) void dw_wgrad_k(const T* __restrict__ A, i
                   (((uintptr_t)A & 15) == 0) && (((uintptr_t)DY & 15) == 0);
   for (int b = b0; b < b1; ++b) {
     __syncthreads();
-    if (v8) {  // 16-B loads: 8 chunks of 8 channels per pixel
-      for (int e = threadIdx.x; e < HW * 8; e += 64 * KS) {
-        const int px = e >> 3, ch = e & 7;
-        const int64_t m = (int64_t)b * HW + px;
-        const bf16x8 va = *(const bf16x8*)(A + am(m) * lda + c0 + ch * 8);
-        const bf16x8 vd = *(const bf16x8*)(DY + dym(m) * lddy + c0 + ch * 8);
+    if (v8) {  // 16-B loads: 8 chunks of 8 channels per pixel, U chunk pairs in flight per thread
+      const int n = HW * 8;
+      for (int e0 = threadIdx.x; e0 < n; e0 += NT * U) {
+        bf16x8 va[U], vd[U];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          ap[px * 64 + ch * 8 + q] = bf2f((bf16_t)va[q]);
-          dp[px * 64 + ch * 8 + q] = bf2f((bf16_t)vd[q]);
+        for (int u = 0; u < U; ++u) {
+          const int e = min(e0 + u * NT, n - 1);
+          const int64_t m = (int64_t)b * HW + (e >> 3);
+          va[u] = *(const bf16x8*)(A + am(m) * lda + c0 + (e & 7) * 8);
+          vd[u] = *(const bf16x8*)(DY + dym(m) * lddy + c0 + (e & 7) * 8);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = e0 + u * NT;
+          if (e < n) {
+            *(bf16x8*)(ap + (e >> 3) * 64 + (e & 7) * 8) = va[u];
+            *(bf16x8*)(dp + (e >> 3) * 64 + (e & 7) * 8) = vd[u];
+          }
         }
       }
     } else {
-      for (int e = threadIdx.x; e < HW * 64; e += 64 * KS) {
+      for (int e = threadIdx.x; e < HW * 64; e += NT) {
         const int px = e >> 6, c = c0 + (e & 63);
         const int64_t m = (int64_t)b * HW + px;
-        ap[e] = c < C ? to_f<T>(A[am(m) * lda + c]) : 0.f;
-        dp[e] = c < C ? to_f<T>(DY[dym(m) * lddy + c]) : 0.f;
+        ap[e] = c < C ? A[am(m) * lda + c] : from_f<T>(0.f);
+        dp[e] = c < C ? DY[dym(m) * lddy + c] : from_f<T>(0.f);
       }
     }
     __syncthreads();
     for (int h = 0; h < H; ++h) {
       const int hh = h + ty - P;
       if (hh < 0 || hh >= H) continue;
-      float ar[MW + KS - 1], dr[MW];
+      for (int w0 = 0; w0 < W; w0 += MW) {
+        float ar[MW + KS - 1], dr[MW];
 #pragma unroll
-      for (int q = 0; q < MW + KS - 1; ++q) {
-        const int ww = q - P;
-        ar[q] = (ww >= 0 && ww < W) ? ap[(hh * W + ww) * 64 + cl] : 0.f;
+        for (int q = 0; q < MW + KS - 1; ++q) {
+          const int ww = w0 + q - P;
+          ar[q] = (ww >= 0 && ww < W) ? to_f<T>(ap[(hh * W + ww) * 64 + cl]) : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < MW; ++q) dr[q] = w0 + q < W ? to_f<T>(dp[(h * W + w0 + q) * 64 + cl]) : 0.f;
+#pragma unroll
+        for (int q = 0; q < MW; ++q)
+#pragma unroll
+          for (int tx = 0; tx < KS; ++tx) acc[tx] = fmaf(dr[q], ar[q + tx], acc[tx]);
       }
-#pragma unroll
-      for (int q = 0; q < MW; ++q) dr[q] = q < W ? dp[(h * W + q) * 64 + cl] : 0.f;
-#pragma unroll
-      for (int q = 0; q < MW; ++q)
-#pragma unroll
-        for (int tx = 0; tx < KS; ++tx) acc[tx] = fmaf(dr[q], ar[q + tx], acc[tx]);
     }
   }
   if (c0 + cl >= C) return;
@@ -1543,10 +1518,10 @@ extern "C" int sdp_dw_wgrad_chunks(int B) { return B < 64 ? (B > 0 ? B : 1) : 64
 extern "C" int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, int64_t a_gstride, int a_off,
                             const void* DY, int64_t lddy, int dy_grp, int64_t dy_gstride, int dy_off, int B, int H,
                             int W, int C, int k, float* part, void* stream) {
-  if (!A || !DY || !part || B < 0 || H <= 0 || W <= 0 || W > 16 || C <= 0 || (k != 3 && k != 5 && k != 7 && k != 9))
+  if (!A || !DY || !part || B < 0 || H <= 0 || W <= 0 || C <= 0 || (k != 3 && k != 5 && k != 7 && k != 9))
     return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
-  const size_t lds = (size_t)H * W * 64 * 2 * sizeof(float);
+  const size_t lds = (size_t)H * W * 64 * 2 * (dtype == 1 ? 2 : 4);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   if ((a_grp > 0 && a_grp % (H * W)) || (dy_grp > 0 && dy_grp % (H * W))) return (int)hipErrorInvalidValue;
   const RowMap am = mk_tmap(a_grp, a_gstride, a_off), dym = mk_tmap(dy_grp, dy_gstride, dy_off);

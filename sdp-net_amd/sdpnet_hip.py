@@ -83,6 +83,8 @@ _SIGS = {
                           _vp], _i32),
     "sdp_act_rowscale_add": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _i32, _i32,
                           _vp], _i32),
+    "sdp_gemm_train_epi": ([_i32, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32,
+                            _i32, _f32, _u64, _vp], _i32),
     "sdp_rowscale_add_mixed": ([_i32, _i32, _i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64,
                                 *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_ln_fwd_mixed": ([_i32, _i32, _vp, _i64, *_ROWMAP, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp],
@@ -518,6 +520,31 @@ _NOMAP = [None, 0, 0, 0, 0]
 
 def _rows_args(r: Optional[Rows]):
     return _NOMAP if r is None else r.args()
+
+
+HIP_ERROR_NOT_SUPPORTED = 801
+
+
+def gemm_train_epi(mode: int, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, M: int, N: int, K: int,
+                   bias: Optional[torch.Tensor] = None, z: Optional[torch.Tensor] = None,
+                   y2: Optional[torch.Tensor] = None, act: int = 0, p: float = 0.0, seed: int = 0) -> bool:
+    """Fast-kernel training epilogues (dense bf16 rows): mode 1 y = x w^T + bias, y2 =
+    dropout(act(y)); mode 2 y = dropout(x w^T) * act'(z).  False (nothing launched) when the
+    fast kernel does not take the shape; the caller then runs gemm + act_fwd / act_bwd."""
+    _need_cuda(x, w, y, bias, z, y2)
+    _req(x.dtype == w.dtype == y.dtype == torch.bfloat16, "gemm_train_epi bf16 operands")
+    _req(all(t.is_contiguous() for t in (x, w, y) + tuple(t for t in (z, y2) if t is not None)))
+    _req(x.numel() >= M * K and w.numel() >= N * K and y.numel() >= M * N, "gemm_train_epi operand sizes")
+    _req(z is None or (z.dtype == torch.bfloat16 and z.numel() >= M * N), "gemm_train_epi z")
+    _req(y2 is None or (y2.dtype == torch.bfloat16 and y2.numel() >= M * N), "gemm_train_epi y2")
+    _req(bias is None or (bias.dtype == torch.float32 and bias.numel() >= N), "gemm_train_epi bias fp32")
+    rc = lib().sdp_gemm_train_epi(int(mode), x.data_ptr(), K, w.data_ptr(), K, _ptr(bias), _ptr(z), N,
+                                  y.data_ptr(), N, _ptr(y2), N, M, N, K, int(act), float(p),
+                                  int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(y))
+    if rc == HIP_ERROR_NOT_SUPPORTED:
+        return False
+    _check(rc, "gemm_train_epi")
+    return True
 
 
 def gemm_flex(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: int, ta: bool = False,

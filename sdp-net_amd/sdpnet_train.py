@@ -54,6 +54,9 @@ from sdpnet_engine import act_code, as_dtype, compute_dtype, f32, num_reg_rows
 Rows = sp.Rows
 
 _FP32_STREAM = os.environ.get("SDPNET_TRAIN_FP32_STREAM", "1") != "0"
+# GEMM + activation fusion (sdp_gemm_train_epi): bit-identical but measured slower on the XL step
+# (856 vs 890 img/s: the exact-erf GELU runs in the tile epilogue while the MFMAs idle), so off
+_FUSED_EPI = os.environ.get("SDPNET_TRAIN_FUSED_EPI", "0") != "0"
 
 
 def set_fp32_stream(on: bool) -> None:
@@ -127,6 +130,38 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         return dx
     sp.gemm_flex(dy, w, dx, M, K, N, ta=False, tb=False)
     return dx
+
+
+def _linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], dt, act: int, p: float = 0.0,
+                seed: int = 0):
+    """(z, h): z = x . w^T + b (kept for the backward), h = dropout_p(act(z)) -- one fast-kernel
+    launch with a two-output epilogue when it takes the shape (bit-identical to gemm + act_fwd)."""
+    M, K = x.shape
+    N = w.shape[0]
+    z = _empty((M, N), dt, x.device)
+    h = _empty((M, N), dt, x.device)
+    if _FUSED_EPI and dt == torch.bfloat16 and sp.gemm_train_epi(1, x, w, z, M, N, K, bias=b, y2=h, act=act, p=p,
+                                                                seed=seed):
+        return z, h
+    sp.gemm(_dense(x), w, _dense(z), M, N, K, bias=b)
+    sp.act_fwd(z, h, M, N, act, p, seed)
+    return z, h
+
+
+def _dgrad_act(dy: torch.Tensor, w: torch.Tensor, z: torch.Tensor, act: int, p: float = 0.0, seed: int = 0):
+    """dz = dropout_p(dy . w) * act'(z): the input gradient through a Linear and the activation
+    (+ dropout) before it, the activation backward fused into the fast kernel's epilogue when it
+    takes the shape (bit-identical to _dgrad + act_bwd)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    if _FUSED_EPI and sp.gemm_variant(dy.dtype, M, K, N) == 1:
+        dz = _empty((M, K), dy.dtype, dy.device)
+        if sp.gemm_train_epi(2, dy, sp.transpose(w), dz, M, K, N, z=z, act=act, p=p, seed=seed):
+            return dz
+    dh = _dgrad(dy, w)
+    dz = _empty((M, K), dy.dtype, dy.device)
+    sp.act_bwd(z, dh, dz, M, K, act, p, seed)
+    return dz
 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
@@ -253,9 +288,7 @@ class _MixerFn(torch.autograd.Function):
         sp.rowscale_add(_dense(z1), imid, M, C, scale=dp2, sgrp=P, resid=img, act=act)   # act + drop path + residual
         # x = drop_path_1(PW_down(act(PW_up(LN2 x_)))) + x_
         a2, s2 = _ln_fwd(imid, M, C, W_["g2"], W_["b2"], m.layer_norm_2.eps, dt)
-        z2 = _linear(a2, W_["upw"], W_["upb"], dt)
-        h = _empty((M, 4 * C), dt, dev)
-        sp.act_fwd(z2, h, M, 4 * C, act)
+        z2, h = _linear_act(a2, W_["upw"], W_["upb"], dt, act)
         out = _with_regs(mid, B, R, N, C)
         if dp1 is None and tok.dtype == dt:  # residual add in the GEMM epilogue, straight into the token rows
             sp.gemm(_dense(h), W_["dnw"], Rows(out, C, P, N, R), M, C, 4 * C, bias=W_["dnb"], resid=imid)
@@ -279,11 +312,9 @@ class _MixerFn(torch.autograd.Function):
         iout = Rows(dout, C, P, N, R)
         # branch 1
         dz3 = _dense_copy(iout, M, C, dt, S["dp1"], P)
-        dh = _dgrad(dz3, W_["dnw"])
+        dz2 = _dgrad_act(dz3, W_["dnw"], S["z2"], act)
         has = S["has"]  # [g1, b1, dww, dwb, ccw, ccb, g2, b2, upw, upb, dnw, dnb]: bias grads only if the bias exists
         gdn, gdnb = _wgrad(dz3, S["h"]), (_colsum(dz3) if has[11] else None)
-        dz2 = _empty((M, 4 * C), dt, dev)
-        sp.act_bwd(S["z2"], dh, dz2, M, 4 * C, act)
         da2 = _dgrad(dz2, W_["upw"])
         gup, gupb = _wgrad(dz2, S["a2"]), (_colsum(dz2) if has[9] else None)
         dmid = _with_regs(dout, B, R, N, C)
@@ -419,10 +450,7 @@ class _EncoderFn(torch.autograd.Function):
         del zo
         # x = x + drop_path2(dropout(ff2(dropout(act(ff1(LN2 x))))))   (:306-309)
         a2, s2 = _ln_fwd(_dense(t2), T, C, W_["n2g"], W_["n2b"], e.norm2.eps, dt)
-        z1 = _linear(a2, W_["w1"], W_["b1"], dt)
-        F_ = z1.shape[1]
-        h = _empty((T, F_), dt, dev)
-        sp.act_fwd(z1, h, T, F_, act, p_ff, seeds[2])
+        z1, h = _linear_act(a2, W_["w1"], W_["b1"], dt, act, p_ff, seeds[2])
         z2 = _linear(h, W_["w2"], W_["b2"], dt)
         if p_ff > 0:
             sp.act_fwd(z2, z2, T, C, 0, p_ff, seeds[3])
@@ -446,12 +474,8 @@ class _EncoderFn(torch.autograd.Function):
         dev = dout.device
         # FFN branch
         dz2 = _branch_grad(dout, T, C, dt, S["dp2"], N, p_ff, seeds[3])
-        dh = _dgrad(dz2, W_["w2"])
+        dz1 = _dgrad_act(dz2, W_["w2"], S["z1"], act, p_ff, seeds[2])
         gw2, gb2 = _wgrad(dz2, S["h"]), _colsum(dz2)
-        F_ = dh.shape[1]
-        dz1 = _empty((T, F_), dt, dev)
-        sp.act_bwd(S["z1"], dh, dz1, T, F_, act, p_ff, seeds[2])
-        del dh
         da2 = _dgrad(dz1, W_["w1"])
         gw1, gb1 = _wgrad(dz1, S["a2"]), _colsum(dz1)
         dt2 = _empty((T, C), sdt, dev)

@@ -201,7 +201,8 @@ def test_softmax_dropout_mask_consistent():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
-@pytest.mark.parametrize("B,H,W,C,k", [(3, 14, 14, 128, 7), (2, 16, 16, 64, 3), (2, 7, 9, 96, 5)])
+@pytest.mark.parametrize("B,H,W,C,k", [(3, 14, 14, 128, 7), (2, 16, 16, 64, 3), (2, 7, 9, 96, 5), (3, 12, 24, 72, 7),
+                                     (130, 16, 16, 96, 7)])
 def test_dw_wgrad(dtype, B, H, W, C, k):
     a = rnd(B * H * W, C, seed=22, dtype=dtype)
     dy = rnd(B * H * W, C, seed=23, dtype=dtype)
@@ -345,3 +346,34 @@ def test_flash_train_attention_vs_torch(B, N, H, hd, p):
     for got, ref, what in ((g[0], q.grad, "dQ"), (g[1], k.grad, "dK")):
         err = float((got - ref).abs().max())
         assert err <= 2e-2 * max(gs, float(ref.abs().max())), f"{what}: {err:.3e} (scale {gs:.3e})"
+
+
+@pytest.mark.parametrize("act", ["gelu", "relu", "kelu"])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+@pytest.mark.parametrize("M,N,K", [(512, 3072, 768), (300, 256, 128), (1000, 1024, 256)])
+def test_gemm_train_epilogues_bit_identical_to_separate_kernels(act, p, M, N, K):
+    """sdp_gemm_train_epi: mode 1 (z and dropout(act(z)) from one launch) and mode 2
+    (dropout(dy . w^T) * act'(z)) equal the fast GEMM followed by sdp_act_fwd / sdp_act_bwd bit
+    for bit (same masks), ragged M included."""
+    code = sp.ACT_CODES[act]
+    x, w = rnd(M, K, seed=1, dtype=BF), rnd(N, K, seed=2, dtype=BF, scale=0.05)
+    b = rnd(N, seed=3, scale=0.1)
+    z, h = torch.empty(M, N, dtype=BF, device=DEV), torch.empty(M, N, dtype=BF, device=DEV)
+    assert sp.gemm_train_epi(1, x, w, z, M, N, K, bias=b, y2=h, act=code, p=p, seed=77)
+    z_ref, h_ref = torch.empty_like(z), torch.empty_like(h)
+    sp.gemm(sp.dense(x), w, sp.dense(z_ref), M, N, K, bias=b)
+    sp.act_fwd(z_ref, h_ref, M, N, code, p, 77)
+    assert torch.equal(z, z_ref) and torch.equal(h, h_ref)
+    # mode 2: dy [M, K2] . wt^T with wt [N, K2] -> [M, N], times act'(z)
+    K2 = 256
+    dy, wt = rnd(M, K2, seed=4, dtype=BF), rnd(N, K2, seed=5, dtype=BF, scale=0.05)
+    dz = torch.empty(M, N, dtype=BF, device=DEV)
+    assert sp.gemm_train_epi(2, dy, wt, dz, M, N, K2, z=z, act=code, p=p, seed=78)
+    dh = torch.empty(M, N, dtype=BF, device=DEV)
+    sp.gemm(sp.dense(dy), wt, sp.dense(dh), M, N, K2)
+    dz_ref = torch.empty_like(dz)
+    sp.act_bwd(z, dh, dz_ref, M, N, code, p, 78)
+    assert torch.equal(dz, dz_ref)
+    # shapes the fast kernel does not take are refused without a launch
+    assert not sp.gemm_train_epi(1, x[:100].contiguous(), w, z[:100].contiguous(), 100, N, K, bias=b,
+                                 y2=h[:100].contiguous(), act=code)
