@@ -207,6 +207,9 @@ int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_ma
  * (each where it applies, else the next lower one).
  * Other values leave the selection unchanged.  Returns the previous selection. */
 int sdp_attention_set_kernel(int k);
+/* Workgroups per CU of the persistent fa4 kernel (0 = as many as LDS and registers allow, at
+ * most 4); returns the previous setting. */
+int sdp_attn_set_per_cu(int n);
 
 /*
  * im2col of the patch conv: image [B,3,Hi,Wi] -> rows [B*(Hi/p)*(Wi/p), Kpad],

@@ -1017,7 +1017,14 @@ __global__ __launch_bounds__(256, 2) void attn_fa4_bf16(const bf16_t* __restrict
   }
 }
 
-static int g_attn_grid = 0;  // persistent grid override (0 = two workgroups per CU)
+static int g_attn_per_cu = 0;  // fa4 workgroups per CU (0 = as many as LDS and registers allow)
+
+// Set the fa4 workgroups per CU (0 = occupancy-derived); returns the old value.
+extern "C" int sdp_attn_set_per_cu(int n) {
+  const int old = g_attn_per_cu;
+  if (n >= 0 && n <= 8) g_attn_per_cu = n;
+  return old;
+}
 
 static size_t attn_fa4_bytes(int N, int hd) { return (size_t)2 * ((N + 15) / 16 * 16) * hd * 2 + 16 * (size_t)hd; }
 
@@ -1043,8 +1050,16 @@ static int launch_attn_fa4(const void* QKV, int64_t ldq, void* O, int64_t ldo, i
   int dev = 0, ncu = 256;
   (void)hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  const int per_cu = bytes <= 80 * 1024 ? 2 : 1;
-  int grid = g_attn_grid > 0 ? g_attn_grid : per_cu * ncu;
+  // persistent grid: as many workgroups per CU as LDS and registers allow (N = 200, hd = 64:
+  // 54 KiB and 160 VGPRs -> 3), so each SIMD interleaves up to three waves' MFMA / softmax phases
+  int per_cu = g_attn_per_cu;
+  if (per_cu <= 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, bytes) != hipSuccess || nb <= 0)
+      nb = bytes <= 80 * 1024 ? 2 : 1;
+    per_cu = nb < 4 ? nb : 4;
+  }
+  int grid = per_cu * ncu;
   grid = grid / 8 * 8;
   if (grid < 8) grid = 8;
   if (grid > B * H) grid = B * H;

@@ -83,6 +83,7 @@ _SIGS = {
                           _vp], _i32),
     "sdp_act_rowscale_add": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _i32, _i32,
                           _vp], _i32),
+    "sdp_attn_set_per_cu": ([_i32], _i32),
     "sdp_gemm_train_epi": ([_i32, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32,
                             _i32, _f32, _u64, _vp], _i32),
     "sdp_rowscale_add_mixed": ([_i32, _i32, _i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64,
@@ -154,7 +155,7 @@ def lib():
         kern = os.environ.get("SDPNET_GEMM_GROUP_M")  # tile raster of the 8-phase GEMM (-1 auto, 1 row-major)
         if kern:
             L.sdp_gemm_set_group_m(int(kern))
-        kern = os.environ.get("SDPNET_GEMM_SCHEDULE")  # 0 data-parallel tiles, 1 stream-K (default)
+        kern = os.environ.get("SDPNET_GEMM_SCHEDULE")  # 0 data-parallel tiles (default), 1 stream-K
         if kern:
             L.sdp_gemm_set_schedule(int(kern))
         kern = os.environ.get("SDPNET_DW_KERNEL")  # A/B switch for the depthwise conv
@@ -163,6 +164,9 @@ def lib():
         kern = os.environ.get("SDPNET_ATTN_KERNEL")  # A/B switch for the bf16 flash attention
         if kern:
             L.sdp_attention_set_kernel(int(kern))
+        kern = os.environ.get("SDPNET_ATTN_PER_CU")  # fa4 workgroups per CU (0 = occupancy-derived)
+        if kern:
+            L.sdp_attn_set_per_cu(int(kern))
         _lib = L
     return _lib
 

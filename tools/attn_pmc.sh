@@ -11,3 +11,16 @@ for ctr in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   timeout -s KILL 120 rocprofv3 --pmc $ctr -d gpurun_out/apmc$i -o run --output-format csv -- $KB > gpurun_out/apmc$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/apmc$i.log; exit 1; }
 done
 echo done
+python - <<'PY'
+import csv, glob, collections
+for d in sorted(glob.glob("gpurun_out/apmc[0-9]")):
+    f = glob.glob(d + "/**/*counter_collection.csv", recursive=True)
+    if not f:
+        continue
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(f[0])):
+        if "fa4" in r["Kernel_Name"]:
+            acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, v in sorted(acc.items()):
+        print(f"{k:26s} {sum(v) / len(v):.4g}")
+PY
