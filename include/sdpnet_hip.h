@@ -406,6 +406,13 @@ int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, int64_t a_gst
  * dlogits = grad_scale / B * (softmax - ((1 - eps) onehot + eps / K)) (may be NULL). */
 int sdp_ce_loss(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K, float eps,
                 float grad_scale, void* dlogits, int64_t ldd, float* loss, void* stream);
+/* The same loss on probability targets (fp32 rows [B][ldt], the CutMix / MixUp targets of
+ * dataset_generator.py:105-110 fed to nn.CrossEntropyLoss): t' = (1 - eps) t + eps / K,
+ * loss = mean_i -sum_k t'_ik log p_ik, dlogits = grad_scale / B * (p sum_k t' - t').  A hard
+ * label outside [0, K) (ignore_index is not implemented) makes its row's loss and gradient NaN
+ * instead of reading out of bounds. */
+int sdp_ce_loss_soft(int dtype, const void* logits, int64_t ldl, const float* targets, int64_t ldt, int B, int K,
+                     float eps, float grad_scale, void* dlogits, int64_t ldd, float* loss, void* stream);
 
 /* Multi-tensor optimizer step over fp32 tensors (device arrays of pointers / sizes and a
  * block table of sdp_mt_block_bytes()-sized {int tensor; int64 start} entries, 4096

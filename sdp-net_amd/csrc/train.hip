@@ -1555,13 +1555,20 @@ extern "C" int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, in
 
 // ---------------------------------------------------------------------------
 // Label-smoothed cross entropy (nn.CrossEntropyLoss(label_smoothing=eps), mean over rows):
-//   loss_i = -(1 - eps) log p_{y_i} - eps / K * sum_k log p_k
-//   dlogits_i = grad_scale / B * (softmax_i - ((1 - eps) onehot(y_i) + eps / K))
-// loss_sum += sum_i loss_i / B (atomic, fp32).  One wave per row.
+//   hard labels:  loss_i = -(1 - eps) log p_{y_i} - eps / K * sum_k log p_k
+//                 dlogits_i = grad_scale / B * (softmax_i - ((1 - eps) onehot(y_i) + eps / K))
+//   soft targets (probability rows t_i, the CutMix / MixUp targets of dataset_generator.py:105-110):
+//                 t'_i = (1 - eps) t_i + eps / K,  loss_i = -sum_k t'_ik log p_ik,
+//                 dlogits_i = grad_scale / B * (softmax_i * sum_k t'_ik - t'_i)
+// loss_sum += sum_i loss_i / B (atomic, fp32).  One wave per row.  A hard label outside [0, K)
+// (ignore_index -100 included, which this loss does not implement) is never dereferenced: the
+// row's loss and gradient become NaN, so the bad batch shows in the loss instead of reading
+// out of bounds (torch raises there).
 // ---------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(256) void ce_k(const T* __restrict__ L, int64_t ldl, const int64_t* __restrict__ y, int B,
-                                            int K, float eps, float grad_scale, T* __restrict__ D, int64_t ldd,
+template <typename T, bool SOFT>
+__global__ __launch_bounds__(256) void ce_k(const T* __restrict__ L, int64_t ldl, const int64_t* __restrict__ y,
+                                            const float* __restrict__ tg, int64_t ldt, int B, int K, float eps,
+                                            float grad_scale, T* __restrict__ D, int64_t ldd,
                                             float* __restrict__ loss) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1579,36 +1586,69 @@ __global__ __launch_bounds__(256) void ce_k(const T* __restrict__ L, int64_t ldl
   for (int c = lane; c < K; c += 64) se += expf(to_f<T>(lp[c]) - mx);
   se = wave_sum(se);
   const float lse = mx + logf(se);
-  const int64_t lab = y[r];
-  const float ly = to_f<T>(lp[lab]);
-  if (lane == 0) {
-    const float li = (1.0f - eps) * (lse - ly) + eps * (lse - sl / (float)K);
-    atomicAdd(loss, li / (float)B);
+  int64_t lab = 0;
+  float li, tsum = 1.0f;
+  if constexpr (SOFT) {
+    // -sum t'_k (l_k - lse) = lse * sum t' - sum t' l
+    const float* tp = tg + r * ldt;
+    float st = 0.f, stl = 0.f;
+    for (int c = lane; c < K; c += 64) {
+      const float t = fmaf(1.0f - eps, tp[c], eps / (float)K);
+      st += t;
+      stl = fmaf(t, to_f<T>(lp[c]), stl);
+    }
+    st = wave_sum(st);
+    stl = wave_sum(stl);
+    tsum = st;
+    li = lse * st - stl;
+  } else {
+    lab = y[r];
+    const bool ok = lab >= 0 && lab < K;
+    const float ly = ok ? to_f<T>(lp[lab]) : NAN;
+    li = (1.0f - eps) * (lse - ly) + eps * (lse - sl / (float)K);
   }
+  if (lane == 0) atomicAdd(loss, li / (float)B);
   if (!D) return;
   const float sc = grad_scale / (float)B, inv = 1.0f / se;
+  const float bad = (!SOFT && !(lab >= 0 && lab < K)) ? NAN : 0.0f;
   for (int c = lane; c < K; c += 64) {
     const float pr = expf(to_f<T>(lp[c]) - mx) * inv;
-    const float tgt = (c == lab ? (1.0f - eps) : 0.0f) + eps / (float)K;
-    D[r * ldd + c] = from_f<T>(sc * (pr - tgt));
+    float tgt;
+    if constexpr (SOFT) tgt = fmaf(1.0f - eps, tg[r * ldt + c], eps / (float)K);
+    else tgt = (c == lab ? (1.0f - eps) : 0.0f) + eps / (float)K;
+    D[r * ldd + c] = from_f<T>(sc * (pr * tsum - tgt) + bad);
   }
 }
 
-extern "C" int sdp_ce_loss(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K, float eps,
-                           float grad_scale, void* dlogits, int64_t ldd, float* loss, void* stream) {
-  if (!logits || !labels || !loss || B < 0 || K <= 0) return (int)hipErrorInvalidValue;
+template <bool SOFT>
+static int ce_launch(int dtype, const void* logits, int64_t ldl, const int64_t* labels, const float* targets,
+                     int64_t ldt, int B, int K, float eps, float grad_scale, void* dlogits, int64_t ldd, float* loss,
+                     void* stream) {
+  if (!logits || !loss || B < 0 || K <= 0) return (int)hipErrorInvalidValue;
+  if (SOFT ? !targets : !labels) return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((B + 3) / 4);
   if (dtype == 1)
-    hipLaunchKernelGGL(ce_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)logits, ldl, labels, B, K, eps, grad_scale,
-                       (bf16_t*)dlogits, ldd, loss);
+    hipLaunchKernelGGL((ce_k<bf16_t, SOFT>), grid, dim3(256), 0, s, (const bf16_t*)logits, ldl, labels, targets, ldt,
+                       B, K, eps, grad_scale, (bf16_t*)dlogits, ldd, loss);
   else if (dtype == 0)
-    hipLaunchKernelGGL(ce_k<float>, grid, dim3(256), 0, s, (const float*)logits, ldl, labels, B, K, eps, grad_scale,
-                       (float*)dlogits, ldd, loss);
+    hipLaunchKernelGGL((ce_k<float, SOFT>), grid, dim3(256), 0, s, (const float*)logits, ldl, labels, targets, ldt, B,
+                       K, eps, grad_scale, (float*)dlogits, ldd, loss);
   else
     return (int)hipErrorInvalidValue;
   return SDP_CHECK_LAUNCH();
+}
+
+extern "C" int sdp_ce_loss(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K, float eps,
+                           float grad_scale, void* dlogits, int64_t ldd, float* loss, void* stream) {
+  return ce_launch<false>(dtype, logits, ldl, labels, nullptr, 0, B, K, eps, grad_scale, dlogits, ldd, loss, stream);
+}
+
+extern "C" int sdp_ce_loss_soft(int dtype, const void* logits, int64_t ldl, const float* targets, int64_t ldt, int B,
+                                int K, float eps, float grad_scale, void* dlogits, int64_t ldd, float* loss,
+                                void* stream) {
+  return ce_launch<true>(dtype, logits, ldl, nullptr, targets, ldt, B, K, eps, grad_scale, dlogits, ldd, loss, stream);
 }
 
 // ---------------------------------------------------------------------------

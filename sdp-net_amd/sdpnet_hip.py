@@ -102,6 +102,7 @@ _SIGS = {
     "sdp_dw_wgrad_chunks": ([_i32], _i32),
     "sdp_dw_wgrad": ([_i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _i32, _i32, _i32, _i32, _i32, _vp, _vp], _i32),
     "sdp_ce_loss": ([_i32, _vp, _i64, _vp, _i32, _i32, _f32, _f32, _vp, _i64, _vp, _vp], _i32),
+    "sdp_ce_loss_soft": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _f32, _f32, _vp, _i64, _vp, _vp], _i32),
     "sdp_mt_block_bytes": ([], _i32),
     "sdp_grad_sumsq": ([_vp, _vp, _vp, _i32, _vp, _vp], _i32),
     "sdp_adamw": ([_vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _f32, _f32, _f32, _f32, _f32, _i32, _f32, _f32, _vp], _i32),
@@ -709,6 +710,19 @@ def ce_loss(logits: torch.Tensor, labels: torch.Tensor, eps: float, grad_scale: 
                            B, K, float(eps), float(grad_scale), _ptr(dlogits),
                            dlogits.stride(0) if dlogits is not None else 0, loss.data_ptr(), _stream(loss))
     _check(rc, "ce_loss")
+
+
+def ce_loss_soft(logits: torch.Tensor, targets: torch.Tensor, eps: float, grad_scale: float,
+                 dlogits: Optional[torch.Tensor], loss: torch.Tensor):
+    """Cross entropy on probability targets [B, K] fp32 (nn.CrossEntropyLoss with soft targets)."""
+    _need_cuda(logits, targets, dlogits, loss)
+    _req(targets.dtype == torch.float32 and loss.dtype == torch.float32 and targets.shape == logits.shape
+         and targets.stride(1) == 1, "ce_loss_soft: fp32 [B, K] targets")
+    B, K = logits.shape
+    rc = lib().sdp_ce_loss_soft(dcode(logits.dtype), logits.data_ptr(), logits.stride(0), targets.data_ptr(),
+                                targets.stride(0), B, K, float(eps), float(grad_scale), _ptr(dlogits),
+                                dlogits.stride(0) if dlogits is not None else 0, loss.data_ptr(), _stream(loss))
+    _check(rc, "ce_loss_soft")
 
 
 def transpose(x: torch.Tensor) -> torch.Tensor:

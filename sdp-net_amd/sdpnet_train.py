@@ -1105,7 +1105,10 @@ class _CEFn(torch.autograd.Function):
     def forward(ctx, logits, labels, eps):
         loss = torch.zeros(1, dtype=torch.float32, device=logits.device)
         d = torch.empty_like(logits)
-        sp.ce_loss(logits.contiguous(), labels, eps, 1.0, d, loss)
+        if labels.is_floating_point():  # probability targets (CutMix / MixUp, dataset_generator.py:105-110)
+            sp.ce_loss_soft(logits.contiguous(), labels.float().contiguous(), eps, 1.0, d, loss)
+        else:
+            sp.ce_loss(logits.contiguous(), labels, eps, 1.0, d, loss)
         ctx.save_for_backward(d)
         return loss[0]
 
@@ -1122,7 +1125,9 @@ class _CEFn(torch.autograd.Function):
 
 def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, label_smoothing: float = 0.0) -> torch.Tensor:
     """nn.CrossEntropyLoss(label_smoothing=...)(logits, labels) (mean over the batch) as one
-    HIP kernel (training_tools.py:76, :88)."""
+    HIP kernel (training_tools.py:76, :88).  ``labels`` are int64 class indices or float
+    probability rows [B, K] (the CutMix / MixUp targets, dataset_generator.py:105-110).  A class
+    index outside [0, K) gives a NaN loss (torch raises; ignore_index is not implemented)."""
     return _CEFn.apply(logits, labels, float(label_smoothing))
 
 

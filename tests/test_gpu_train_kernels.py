@@ -231,6 +231,47 @@ def test_ce_loss(dtype, eps):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("eps", [0.0, 0.1])
+def test_ce_loss_soft_targets(dtype, eps):
+    # CutMix / MixUp probability targets (dataset_generator.py:105-110) into nn.CrossEntropyLoss
+    B, K = 37, 1000
+    logits = rnd(B, K, seed=27, dtype=dtype, scale=3)
+    g = torch.Generator().manual_seed(1)
+    a = torch.randint(0, K, (B,), generator=g)
+    b = torch.randint(0, K, (B,), generator=g)
+    lam = torch.rand(B, 1, generator=g)
+    tgt = (lam * F.one_hot(a, K) + (1 - lam) * F.one_hot(b, K)).float().to(DEV)
+    d = torch.empty_like(logits)
+    loss = torch.zeros(1, device=DEV)
+    sp.ce_loss_soft(logits, tgt, eps, 8.0, d, loss)
+    lr = logits.float().clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, tgt, label_smoothing=eps)
+    (gr,) = torch.autograd.grad(ref * 8.0, lr)
+    close(loss, ref.detach().view(1), 1e-5, "soft ce loss")
+    close(d, gr, 1e-5 if dtype == torch.float32 else 2e-2, "soft ce dlogits")
+    # through the autograd entry point
+    import sdpnet_train as st
+    lr2 = logits.float().clone().requires_grad_(True)
+    l2 = st.cross_entropy(lr2, tgt, label_smoothing=eps)
+    l2.backward()
+    close(l2.detach().view(1), ref.detach().view(1), 1e-5, "cross_entropy(soft)")
+    close(lr2.grad, gr / 8.0, 1e-5, "cross_entropy(soft) grad")
+
+
+def test_ce_loss_label_out_of_range_is_nan_not_oob():
+    B, K = 8, 100
+    logits = rnd(B, K, seed=28)
+    labels = torch.tensor([0, 5, -100, 99, 100, 3, 7, 1], device=DEV)
+    d = torch.empty_like(logits)
+    loss = torch.zeros(1, device=DEV)
+    sp.ce_loss(logits, labels, 0.0, 1.0, d, loss)
+    torch.cuda.synchronize()
+    assert torch.isnan(loss).all()
+    bad = torch.isnan(d).all(dim=1).cpu()
+    assert bad.tolist() == [False, False, True, False, True, False, False, False]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
 @pytest.mark.parametrize("R,C", [(768, 3072), (100, 37), (1, 64)])
 def test_transpose(dtype, R, C):
     x = rnd(R, C, seed=25, dtype=dtype)
