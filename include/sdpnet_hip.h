@@ -471,6 +471,22 @@ int sdp_grad_sumsq_parts(float* const* grads, const int64_t* sizes, const void* 
                          float* partials, float* state, void* stream);
 int sdp_sum_partials(const float* partials, int n, float* state, void* stream);
 
+/* Weight gradient on the 8-phase MFMA main loop (training backward of every Linear / 1x1 conv,
+ * the adjoint of layers.py:79-91, :242-249, :282-284, :308): C + s * split_stride = sum over
+ * the token rows of split s of A[k][i] * B[k][j] (fp32), A = dY [ktok][lda], B = X [ktok][ldb]
+ * bf16 token-major.  Split s covers K-tiles [s * kchunk_tiles, (s + 1) * kchunk_tiles) of 64
+ * tokens; the caller reduces the slabs.  A last K-tile past ktok reads `zrow` (>= max(ni, nj)
+ * zero bf16, 16-B aligned; may be NULL when ktok % 64 == 0) for the missing rows.  ni % 256 ==
+ * 0, nj % 256 == 0, 16-B aligned operands (hipErrorNotSupported otherwise: use sdp_gemm_flex). */
+int sdp_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc,
+                   int64_t split_stride, int ni, int nj, int ktok, int kchunk_tiles, const void* zrow,
+                   void* stream);
+
+/* Experimental: a HIP stream restricted to part `part` of `nparts` CU subsets (contiguous CU
+ * index ranges, or every nparts-th CU with interleave != 0), for the sub-batch streams of the
+ * fused forward (SDPNET_CU_SPLIT).  *out receives the hipStream_t. */
+int sdp_stream_create_cu_mask(int part, int nparts, int interleave, void** out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -406,3 +406,28 @@ extern "C" int sdp_fold_ln_weight(const float* W, const float* gamma, const floa
     return (int)hipErrorInvalidValue;
   return SDP_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------
+// Sub-batch stream restricted to a subset of the CUs (hipExtStreamCreateWithCUMask), for the
+// concurrent sub-batch schedule of the fused forward: part p of nparts gets the CUs whose
+// index i satisfies (interleave ? i % nparts : i * nparts / ncu) == p.  Experimental (A/B).
+// ---------------------------------------------------------------------------
+#include <hip/hip_ext.h>
+extern "C" int sdp_stream_create_cu_mask(int part, int nparts, int interleave, void** out) {
+  if (!out || nparts <= 0 || part < 0 || part >= nparts) return (int)hipErrorInvalidValue;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  uint32_t mask[32] = {0};
+  const int nw = (ncu + 31) / 32;
+  if (nw > 32) return (int)hipErrorInvalidValue;
+  for (int i = 0; i < ncu; ++i) {
+    const int p = interleave ? i % nparts : (int)((int64_t)i * nparts / ncu);
+    if (p == part) mask[i >> 5] |= 1u << (i & 31);
+  }
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)nw, mask);
+  if (e != hipSuccess) return (int)e;
+  *out = (void*)s;
+  return 0;
+}

@@ -43,6 +43,8 @@ _SIGS = {
     "sdp_gemm_workspace_bytes": ([], _i64),
     "sdp_gemm_set_workspace": ([_vp, _vp, _i64], _i32),
     "sdp_gemm_set_schedule": ([_i32], _i32),
+    "sdp_stream_create_cu_mask": ([_i32, _i32, _i32, _vp], _i32),
+    "sdp_gemm_wgrad": ([_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp], _i32),
     "sdp_gemm_sk_applies": ([_i32, _i32, _i32], _i32),
     "sdp_gemm_sk_status": ([_vp, _vp], _i32),
     "sdp_layernorm": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _f32, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
@@ -581,6 +583,41 @@ def gemm_flex(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int,
                              B.data_ptr() + b_off * es, ldb, sb[0], sb[1], C.data_ptr() + c_off * eo, ldc, sc[0],
                              sc[1], M, N, K, Z, zdiv, splits, split_stride, float(alpha), int(bool(accum)), _stream(C))
     _check(rc, "gemm_flex")
+
+
+_ZERO_ROWS = {}
+
+
+def _zero_row(device, n: int) -> torch.Tensor:
+    """A cached zero bf16 row of >= n elements (the rows gemm_wgrad reads past the last token)."""
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    z = _ZERO_ROWS.get(key)
+    if z is None or z.numel() < n:
+        z = torch.zeros(max(n, 4096), dtype=torch.bfloat16, device=device)
+        _ZERO_ROWS[key] = z
+    return z
+
+
+def gemm_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, ktok: int, kchunk_tiles: int,
+               split_stride: int = 0):
+    """out[s] (fp32 [N, K] slabs) = dy[rows of split s]^T x[rows of split s] on the 8-phase MFMA
+    kernel (sdp_gemm_wgrad); dy [>= ktok, N], x [>= ktok, K] bf16 with unit column stride."""
+    _need_cuda(dy, x, out)
+    _req(dy.dtype == x.dtype == torch.bfloat16 and out.dtype == torch.float32, "gemm_wgrad dtypes")
+    _req(dy.stride(1) == 1 and x.stride(1) == 1 and out.stride(-1) == 1, "gemm_wgrad unit column strides")
+    N, K = dy.shape[1], x.shape[1]
+    _req(dy.shape[0] >= ktok and x.shape[0] >= ktok and ktok > 0, "gemm_wgrad token rows")
+    nkt = (ktok + 63) // 64
+    zrow = _zero_row(dy.device, max(N, K)) if ktok % 64 else None
+    splits = (nkt + kchunk_tiles - 1) // kchunk_tiles
+    ldc = out.stride(-2)
+    _req(out.shape[-2] >= N and out.shape[-1] >= K, "gemm_wgrad output shape")
+    last = (splits - 1) * split_stride + (N - 1) * ldc + K
+    avail = out.untyped_storage().nbytes() // 4 - out.storage_offset()
+    _req(last <= avail and (splits == 1 or split_stride >= N * ldc), "gemm_wgrad output out of bounds")
+    rc = lib().sdp_gemm_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(), ldc,
+                              split_stride, N, K, ktok, kchunk_tiles, _ptr(zrow), _stream(out))
+    _check(rc, "gemm_wgrad")
 
 
 def seg_colsum(X: torch.Tensor, out: torch.Tensor, G: int, length: int, gstride: int, estride: int, C: int,

@@ -164,8 +164,42 @@ def _dgrad_act(dy: torch.Tensor, w: torch.Tensor, z: torch.Tensor, act: int, p: 
     return dz
 
 
+_WGRAD_8PH = os.environ.get("SDPNET_WGRAD_8PH", "1") != "0"
+
+
+def _wgrad_8ph_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    M, N = dy.shape
+    K = x.shape[1]
+    return (_WGRAD_8PH and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and N % 256 == 0
+            and K % 256 == 0 and M >= 256 and dy.stride(1) == 1 and x.stride(1) == 1 and dy.stride(0) % 8 == 0
+            and x.stride(0) % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
+
+
+def _wgrad_8ph(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW [N, K] fp32 = dy^T x on the 8-phase MFMA kernel (csrc/wgrad.hip): the token rows are
+    split into at most one workgroup per CU's worth of fp32 slabs, reduced in a fixed order by
+    sdp_seg_colsum (bit-reproducible)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    nkt = -(-M // 64)
+    tiles = (N // 256) * (K // 256)
+    target = max(1, min(nkt, 256 // tiles))
+    kchunk = -(-nkt // target)
+    splits = -(-nkt // kchunk)
+    dw = _empty((N, K), torch.float32, dy.device)
+    if splits == 1:
+        sp.gemm_wgrad(dy, x, dw, M, kchunk)
+    else:
+        slabs = _empty((splits, N, K), torch.float32, dy.device)
+        sp.gemm_wgrad(dy, x, slabs, M, kchunk, split_stride=N * K)
+        sp.seg_colsum(slabs.view(splits, N * K), dw.view(1, N * K), 1, splits, 0, 1, N * K)
+    return dw
+
+
 def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """dW [N, K] fp32 = dy^T x, reduction over the M token rows split across workgroups."""
+    if _wgrad_8ph_ok(dy, x):
+        return _wgrad_8ph(dy, x)
     M, N = dy.shape
     K = x.shape[1]
     tiles = ((N + 127) // 128) * ((K + 127) // 128)

@@ -214,6 +214,46 @@ def test_dw_wgrad(dtype, B, H, W, C, k):
     close(got, gw.view(C, k * k), 1e-4 if dtype == torch.float32 else 2e-2, "dw wgrad")
 
 
+@pytest.mark.parametrize("N,K,M,kchunk", [(256, 256, 64, 1), (256, 512, 640, 3), (768, 768, 30720, 18),
+                                          (512, 256, 4096, 64), (2304, 768, 1024, 4), (256, 256, 37, 1),
+                                          (768, 512, 31200, 55), (256, 768, 700, 4)])
+def test_gemm_wgrad_8ph(N, K, M, kchunk):
+    # dW = dY^T X on the 8-phase kernel (csrc/wgrad.hip) vs fp32 torch; each split's slab alone
+    # too; M % 64 != 0: the last K-tile reads the zero row past the last token
+    dy = rnd(M, N, seed=31, dtype=BF, scale=0.5)
+    x = rnd(M, K, seed=32, dtype=BF)
+    nkt = -(-M // 64)
+    splits = -(-nkt // kchunk)
+    slabs = torch.full((splits, N, K), float("nan"), device=DEV)
+    sp.gemm_wgrad(dy, x, slabs, M, kchunk, split_stride=N * K)
+    for s in range(splits):
+        lo, hi = s * kchunk * 64, min(M, (s + 1) * kchunk * 64)
+        ref = dy[lo:hi].float().t() @ x[lo:hi].float()
+        close(slabs[s], ref, 1e-5, f"wgrad slab {s}")
+    close(slabs.sum(0), dy.float().t() @ x.float(), 1e-5, "wgrad sum")
+
+
+def test_gemm_wgrad_8ph_strided_and_training_dispatch():
+    import sdpnet_train as st
+    # strided token rows (ld > N), a 40-token partial last K-tile, bit-reproducible
+    M, N, K = 4136, 512, 768
+    base_dy = rnd(M, N + 64, seed=33, dtype=BF, scale=0.5)
+    base_x = rnd(M, K + 8, seed=34, dtype=BF)
+    dy, x = base_dy[:, 32:32 + N], base_x[:, :K]
+    assert st._wgrad_8ph_ok(dy, x)
+    a = st._wgrad(dy, x)
+    b = st._wgrad(dy, x)
+    assert torch.equal(a, b)
+    close(a, dy.float().t() @ x.float(), 1e-5, "wgrad strided + tail")
+    old = st._WGRAD_8PH
+    try:
+        st._WGRAD_8PH = False
+        c = st._wgrad(dy.contiguous(), x.contiguous())
+    finally:
+        st._WGRAD_8PH = old
+    close(a, c, 1e-5, "wgrad 8ph vs gemm_flex")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
 @pytest.mark.parametrize("eps", [0.0, 0.1])
 def test_ce_loss(dtype, eps):
