@@ -482,6 +482,14 @@ int sdp_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t ldb, float
                    int64_t split_stride, int ni, int nj, int ktok, int kchunk_tiles, const void* zrow,
                    void* stream);
 
+/* Per-step weight preparation of the bf16 training step in one launch: entries is a device
+ * array of sdp_mt_cast_transpose_entry_bytes()-sized records {const float* src; uint16_t* dst;
+ * uint16_t* dstT; int64 ldd; int64 ldt; int R; int C} (fp32 [R][C] row-major in; bf16 copy
+ * dst[r * ldd + c] and transposed copy dstT[c * ldt + r] out, either may be NULL); tiles is a
+ * device array of int4 {entry, r0, c0, 0}, one 64 x 64 tile per workgroup. */
+int sdp_mt_cast_transpose_entry_bytes(void);
+int sdp_mt_cast_transpose(const void* entries, const void* tiles, int ntiles, void* stream);
+
 /* Experimental: a HIP stream restricted to part `part` of `nparts` CU subsets (contiguous CU
  * index ranges, or every nparts-th CU with interleave != 0), for the sub-batch streams of the
  * fused forward (SDPNET_CU_SPLIT).  *out receives the hipStream_t. */

@@ -236,3 +236,89 @@ extern "C" int sdp_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t
                      ktok, (const bf16_t*)zrow);
   return SDP_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------
+// Per-step weight preparation of the training forward / backward in one launch: every entry
+// reads an fp32 weight [R][C] (row stride C) once and writes its bf16 copy dst[r * ldd + c]
+// (the GEMM operand of the forward) and / or its transposed bf16 copy dstT[c * ldt + r] (the
+// operand of the input-gradient GEMM dX = dY W); either output may be NULL.  64 x 64 tiles,
+// transposed through LDS.  Replaces one cast and one transpose launch per weight and step.
+// ---------------------------------------------------------------------------
+struct MtCastT {
+  const float* src;
+  uint16_t* dst;
+  uint16_t* dstT;
+  int64_t ldd, ldt;
+  int R, C;
+};
+
+extern "C" int sdp_mt_cast_transpose_entry_bytes(void) { return (int)sizeof(MtCastT); }
+
+__global__ __launch_bounds__(256) void mt_cast_transpose_k(const MtCastT* __restrict__ ent,
+                                                           const int4* __restrict__ tiles) {
+  __shared__ uint16_t tl[64][72];
+  const int4 t = tiles[blockIdx.x];
+  const MtCastT e = ent[t.x];
+  const int r0 = t.y, c0 = t.z, tid = threadIdx.x;
+  const int cc = (tid & 15) * 4;
+  const bool vec = (e.C & 3) == 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rr = (tid >> 4) + 16 * i;
+    const int r = r0 + rr, c = c0 + cc;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r < e.R) {
+      const float* p = e.src + (int64_t)r * e.C + c;
+      if (vec && c + 3 < e.C) {
+        const float4 q = *(const float4*)p;
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (c + k < e.C) v[k] = p[k];
+      }
+    }
+    uint16_t b[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      b[k] = f2bf(v[k]);
+      tl[rr][cc + k] = b[k];
+    }
+    if (e.dst && r < e.R) {
+      uint16_t* q = e.dst + (int64_t)r * e.ldd + c;
+      if (c + 3 < e.C && ((uintptr_t)q & 7) == 0) {
+        *(uint2*)q = make_uint2((uint32_t)b[0] | ((uint32_t)b[1] << 16), (uint32_t)b[2] | ((uint32_t)b[3] << 16));
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (c + k < e.C) q[k] = b[k];
+      }
+    }
+  }
+  if (!e.dstT) return;
+  __syncthreads();
+  // transposed: lane -> column c0 + tc, rows r0 + tr .. tr + 15 (32 contiguous bytes)
+  const int tc = tid >> 2, tr = (tid & 3) * 16;
+  const int c = c0 + tc;
+  if (c >= e.C) return;
+  uint16_t* q = e.dstT + (int64_t)c * e.ldt + r0 + tr;
+  uint32_t w[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k] = (uint32_t)tl[tr + 2 * k][tc] | ((uint32_t)tl[tr + 2 * k + 1][tc] << 16);
+  if (r0 + tr + 15 < e.R && ((uintptr_t)q & 15) == 0) {
+    *(uint4*)q = make_uint4(w[0], w[1], w[2], w[3]);
+    *(uint4*)(q + 8) = make_uint4(w[4], w[5], w[6], w[7]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (r0 + tr + k < e.R) q[k] = tl[tr + k][tc];
+  }
+}
+
+extern "C" int sdp_mt_cast_transpose(const void* entries, const void* tiles, int ntiles, void* stream) {
+  if (!entries || !tiles || ntiles < 0) return (int)hipErrorInvalidValue;
+  if (ntiles == 0) return 0;
+  hipLaunchKernelGGL(mt_cast_transpose_k, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, (const MtCastT*)entries,
+                     (const int4*)tiles);
+  return SDP_CHECK_LAUNCH();
+}

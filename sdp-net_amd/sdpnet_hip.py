@@ -44,6 +44,8 @@ _SIGS = {
     "sdp_gemm_set_workspace": ([_vp, _vp, _i64], _i32),
     "sdp_gemm_set_schedule": ([_i32], _i32),
     "sdp_stream_create_cu_mask": ([_i32, _i32, _i32, _vp], _i32),
+    "sdp_mt_cast_transpose_entry_bytes": ([], _i32),
+    "sdp_mt_cast_transpose": ([_vp, _vp, _i32, _vp], _i32),
     "sdp_gemm_wgrad": ([_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp], _i32),
     "sdp_gemm_sk_applies": ([_i32, _i32, _i32], _i32),
     "sdp_gemm_sk_status": ([_vp, _vp], _i32),
@@ -583,6 +585,34 @@ def gemm_flex(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int,
                              B.data_ptr() + b_off * es, ldb, sb[0], sb[1], C.data_ptr() + c_off * eo, ldc, sc[0],
                              sc[1], M, N, K, Z, zdiv, splits, split_stride, float(alpha), int(bool(accum)), _stream(C))
     _check(rc, "gemm_flex")
+
+
+def mt_cast_transpose(jobs):
+    """jobs: [(src fp32 [R, C] contiguous, dst bf16 view or None, dstT bf16 view or None)]:
+    dst[r, c] = bf16(src[r, c]) and dstT[c, r] = bf16(src[r, c]) in one launch (dst / dstT may be
+    row-strided views; unit column stride)."""
+    import struct
+    if not jobs:
+        return
+    dev = jobs[0][0].device
+    eb = lib().sdp_mt_cast_transpose_entry_bytes()
+    raw, tiles = bytearray(), []
+    for i, (src, dst, dt_) in enumerate(jobs):
+        _need_cuda(src, dst, dt_)
+        _req(src.dtype == torch.float32 and src.dim() == 2 and src.is_contiguous(), "mt_cast_transpose src")
+        R, C = src.shape
+        for t, shp in ((dst, (R, C)), (dt_, (C, R))):
+            _req(t is None or (t.dtype == torch.bfloat16 and tuple(t.shape) == shp and t.stride(1) == 1),
+                 "mt_cast_transpose outputs")
+        ent = struct.pack("<QQQqqii", src.data_ptr(), 0 if dst is None else dst.data_ptr(),
+                          0 if dt_ is None else dt_.data_ptr(), 0 if dst is None else dst.stride(0),
+                          0 if dt_ is None else dt_.stride(0), R, C)
+        raw += ent + bytes(eb - len(ent))
+        tiles += [(i, r0, c0, 0) for r0 in range(0, R, 64) for c0 in range(0, C, 64)]
+    ent = torch.frombuffer(raw, dtype=torch.uint8).to(dev)
+    tl = torch.tensor(tiles, dtype=torch.int32, device=dev)
+    _check(lib().sdp_mt_cast_transpose(ent.data_ptr(), tl.data_ptr(), len(tiles), _stream(jobs[0][0])),
+           "mt_cast_transpose")
 
 
 _ZERO_ROWS = {}

@@ -117,15 +117,15 @@ def _linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out_dt)
     return z
 
 
-def _dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+def _dgrad(dy: torch.Tensor, w: torch.Tensor, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dx = dy . w.  Shapes the 256x256 MFMA kernel takes (bf16, N % 64 == 0, M >= 128) run on it
-    with a transposed weight copy (HIP transpose, small next to the GEMM); others on gemm_flex,
-    which reads w transposed from LDS."""
+    with a transposed weight copy (``wt`` from the step's weight preparation, else a HIP
+    transpose); others on gemm_flex, which reads w transposed from LDS."""
     M, N = dy.shape
     K = w.shape[1]
     dx = _empty((M, K), dy.dtype, dy.device)
     if sp.gemm_variant(dy.dtype, M, K, N) == 1:
-        wt = sp.transpose(w)
+        wt = wt if wt is not None else sp.transpose(w)
         sp.gemm(_dense(dy), wt, _dense(dx), M, K, N)
         return dx
     sp.gemm_flex(dy, w, dx, M, K, N, ta=False, tb=False)
@@ -148,7 +148,8 @@ def _linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], dt,
     return z, h
 
 
-def _dgrad_act(dy: torch.Tensor, w: torch.Tensor, z: torch.Tensor, act: int, p: float = 0.0, seed: int = 0):
+def _dgrad_act(dy: torch.Tensor, w: torch.Tensor, z: torch.Tensor, act: int, p: float = 0.0, seed: int = 0,
+               wt: Optional[torch.Tensor] = None):
     """dz = dropout_p(dy . w) * act'(z): the input gradient through a Linear and the activation
     (+ dropout) before it, the activation backward fused into the fast kernel's epilogue when it
     takes the shape (bit-identical to _dgrad + act_bwd)."""
@@ -156,12 +157,98 @@ def _dgrad_act(dy: torch.Tensor, w: torch.Tensor, z: torch.Tensor, act: int, p: 
     K = w.shape[1]
     if _FUSED_EPI and sp.gemm_variant(dy.dtype, M, K, N) == 1:
         dz = _empty((M, K), dy.dtype, dy.device)
-        if sp.gemm_train_epi(2, dy, sp.transpose(w), dz, M, K, N, z=z, act=act, p=p, seed=seed):
+        if sp.gemm_train_epi(2, dy, wt if wt is not None else sp.transpose(w), dz, M, K, N, z=z, act=act, p=p,
+                             seed=seed):
             return dz
-    dh = _dgrad(dy, w)
+    dh = _dgrad(dy, w, wt)
     dz = _empty((M, K), dy.dtype, dy.device)
     sp.act_bwd(z, dh, dz, M, K, act, p, seed)
     return dz
+
+
+# ---------------------------------------------------------------------------
+# Per-step weight preparation: the bf16 GEMM operands of every ConvMixer / EncoderLayer weight
+# (forward) and their transposes (input-gradient GEMMs) from the fp32 parameters, in ONE
+# sdp_mt_cast_transpose launch at the start of a bf16 training forward, into buffers kept on
+# the model.  Only valid inside that forward (_WPREP is cleared after it), so a sub-module
+# trained on its own or an fp32 forward never sees them.
+# ---------------------------------------------------------------------------
+_WPREP: Optional[dict] = None
+_WPREP_ON = os.environ.get("SDPNET_WEIGHT_PREP", "1") != "0"
+
+
+def _weight_jobs(model):
+    """(key, [(param, row offset in the stacked weight)], rows, cols) of every prepared weight."""
+    jobs = []
+    encs = [blk.t_block for blk in model.blocks] + [model.final_block.t_block]
+    for blk in model.blocks:
+        for mx in blk.conv_blocks:
+            for conv in (mx.conv2d[1], mx.conv1d[0], mx.conv1d[2]):
+                w = conv.weight
+                jobs.append((id(w), [(w, 0)], w.shape[0], w.shape[1]))
+    for e in encs:
+        C = e.embedding_dim
+        jobs.append((("qkv", id(e.q_proj.weight)), [(e.q_proj.weight, 0), (e.k_proj.weight, C), (e.v_proj.weight, 2 * C)],
+                     3 * C, C))
+        for lin in (e.o_proj, e.ff_linear1, e.ff_linear2):
+            w = lin.weight
+            jobs.append((id(w), [(w, 0)], w.shape[0], w.shape[1]))
+    return jobs
+
+
+def _prep_weights(model, dt) -> Optional[dict]:
+    """Fill the step's bf16 weight operands (and transposes) in one launch; returns
+    {key: (w [R, C] bf16, w^T [C, R] bf16)} (key = id(param), or ("qkv", id(q weight)))."""
+    if not _WPREP_ON or dt != torch.bfloat16:
+        return None
+    dev = model.conv_init.conv.weight.device
+    if dev.type != "cuda":
+        return None
+    jobs = _weight_jobs(model)
+    sig = tuple((k, r, c, tuple((p.data_ptr(), off) for p, off in ps)) for k, ps, r, c in jobs)
+    st = model.__dict__.get("_sdp_wprep")
+    if st is None or st["dev"] != dev or st["shapes"] != tuple((k, r, c) for k, _, r, c in jobs):
+        import struct
+        bufs, tiles = {}, []
+        for k, ps, r, c in jobs:
+            bufs[k] = (_empty((r, c), torch.bfloat16, dev), _empty((c, r), torch.bfloat16, dev))
+        ei = 0
+        for k, ps, r, c in jobs:
+            for p, off in ps:
+                pr, pc = p.shape[0], p.numel() // p.shape[0]
+                for r0 in range(0, pr, 64):
+                    for c0 in range(0, pc, 64):
+                        tiles.append((ei, r0, c0, 0))
+                ei += 1
+        st = dict(dev=dev, shapes=tuple((k, r, c) for k, _, r, c in jobs), bufs=bufs, sig=None,
+                  tiles=torch.tensor(tiles, dtype=torch.int32, device=dev), ntiles=len(tiles), entries=None,
+                  pack=struct)
+        model.__dict__["_sdp_wprep"] = st
+    if st["sig"] != sig:  # parameter storage moved (or first call): rebuild the entry table
+        struct = st["pack"]
+        eb = sp.lib().sdp_mt_cast_transpose_entry_bytes()
+        raw = bytearray()
+        for k, ps, r, c in jobs:
+            w, wt = st["bufs"][k]
+            for p, off in ps:
+                if p.dtype != torch.float32 or not p.is_contiguous():
+                    return None
+                pr, pc = p.shape[0], p.numel() // p.shape[0]
+                ent = struct.pack("<QQQqqii", p.data_ptr(), w.data_ptr() + 2 * off * c, wt.data_ptr() + 2 * off,
+                                  c, r, pr, pc)
+                raw += ent + bytes(eb - len(ent))
+        st["entries"] = torch.frombuffer(raw, dtype=torch.uint8).to(dev)
+        st["sig"] = sig
+    sp._check(sp.lib().sdp_mt_cast_transpose(st["entries"].data_ptr(), st["tiles"].data_ptr(), st["ntiles"],
+                                             torch.cuda.current_stream(dev).cuda_stream), "mt_cast_transpose")
+    return st["bufs"]
+
+
+def _wprep(key, dt):
+    """The prepared (w, w^T) of a weight inside a bf16 training forward, else None."""
+    if _WPREP is None or dt != torch.bfloat16:
+        return None
+    return _WPREP.get(key)
 
 
 _WGRAD_8PH = os.environ.get("SDPNET_WGRAD_8PH", "1") != "0"
@@ -306,10 +393,12 @@ class _MixerFn(torch.autograd.Function):
         dev = tok.device
         act = act_code(m.activation)
         img = Rows(tok, C, P, N, R)
+        pcc, pup, pdn = _wprep(id(ccw), dt), _wprep(id(upw), dt), _wprep(id(dnw), dt)
         W_ = dict(g1=f32(g1), b1=f32(b1), dww=f32(dww.reshape(C, k * k)), dwb=f32(dwb),
-                  ccw=as_dtype(ccw.reshape(C, C), dt), ccb=f32(ccb), g2=f32(g2), b2=f32(b2),
-                  upw=as_dtype(upw.reshape(4 * C, C), dt), upb=f32(upb),
-                  dnw=as_dtype(dnw.reshape(C, 4 * C), dt), dnb=f32(dnb))
+                  ccw=pcc[0] if pcc else as_dtype(ccw.reshape(C, C), dt), ccb=f32(ccb), g2=f32(g2), b2=f32(b2),
+                  upw=pup[0] if pup else as_dtype(upw.reshape(4 * C, C), dt), upb=f32(upb),
+                  dnw=pdn[0] if pdn else as_dtype(dnw.reshape(C, 4 * C), dt), dnb=f32(dnb),
+                  ccw_t=pcc[1] if pcc else None, upw_t=pup[1] if pup else None, dnw_t=pdn[1] if pdn else None)
         dp2 = _drop_path_scale(_drop_p(m.drop_path_2), B, dev)
         dp1 = _drop_path_scale(_drop_p(m.drop_path_1), B, dev)
         # x_ = drop_path_2(act(PW(DW(LN1 x)))) + x
@@ -346,10 +435,10 @@ class _MixerFn(torch.autograd.Function):
         iout = Rows(dout, C, P, N, R)
         # branch 1
         dz3 = _dense_copy(iout, M, C, dt, S["dp1"], P)
-        dz2 = _dgrad_act(dz3, W_["dnw"], S["z2"], act)
+        dz2 = _dgrad_act(dz3, W_["dnw"], S["z2"], act, wt=W_["dnw_t"])
         has = S["has"]  # [g1, b1, dww, dwb, ccw, ccb, g2, b2, upw, upb, dnw, dnb]: bias grads only if the bias exists
         gdn, gdnb = _wgrad(dz3, S["h"]), (_colsum(dz3) if has[11] else None)
-        da2 = _dgrad(dz2, W_["upw"])
+        da2 = _dgrad(dz2, W_["upw"], W_["upw_t"])
         gup, gupb = _wgrad(dz2, S["a2"]), (_colsum(dz2) if has[9] else None)
         dmid = _with_regs(dout, B, R, N, C)
         imid = Rows(dmid, C, P, N, R)
@@ -358,7 +447,7 @@ class _MixerFn(torch.autograd.Function):
         dh1 = _dense_copy(imid, M, C, dt, S["dp2"], P)
         dz1 = _empty((M, C), dt, dev)
         sp.act_bwd(S["z1"], dh1, dz1, M, C, act)
-        dd = _dgrad(dz1, W_["ccw"])
+        dd = _dgrad(dz1, W_["ccw"], W_["ccw_t"])
         gcc, gccb = _wgrad(dz1, S["d"]), (_colsum(dz1) if has[5] else None)
         da1 = _empty((M, C), dt, dev)
         wflip = W_["dww"].view(C, k, k).flip(1, 2).reshape(C, k * k).contiguous()
@@ -437,9 +526,12 @@ class _EncoderFn(torch.autograd.Function):
         p_ff = float(e.dropout.p)
         p_att = float(e.att_dropout) if e.fast_att else p_ff  # manual path drops with self.dropout (:297)
         qn = qg is not None
-        wqkv32 = torch.cat([f32(wq), f32(wk), f32(wv)], 0)
-        W_ = dict(n1g=f32(n1g), n1b=f32(n1b), wqkv=as_dtype(wqkv32, dt), wo=as_dtype(wo, dt), n2g=f32(n2g),
-                  n2b=f32(n2b), w1=as_dtype(w1, dt), b1=f32(b1), w2=as_dtype(w2, dt), b2=f32(b2))
+        pq, po, p1, p2 = _wprep(("qkv", id(wq)), dt), _wprep(id(wo), dt), _wprep(id(w1), dt), _wprep(id(w2), dt)
+        wqkv = pq[0] if pq else as_dtype(torch.cat([f32(wq), f32(wk), f32(wv)], 0), dt)
+        W_ = dict(n1g=f32(n1g), n1b=f32(n1b), wqkv=wqkv, wo=po[0] if po else as_dtype(wo, dt), n2g=f32(n2g),
+                  n2b=f32(n2b), w1=p1[0] if p1 else as_dtype(w1, dt), b1=f32(b1), w2=p2[0] if p2 else as_dtype(w2, dt),
+                  b2=f32(b2), wqkv_t=pq[1] if pq else None, wo_t=po[1] if po else None, w1_t=p1[1] if p1 else None,
+                  w2_t=p2[1] if p2 else None)
         if qn:
             W_.update(qg=f32(qg), qb=f32(qb), kg=f32(kg), kb=f32(kb))
         seeds = [rng.next() for _ in range(4)]
@@ -508,15 +600,15 @@ class _EncoderFn(torch.autograd.Function):
         dev = dout.device
         # FFN branch
         dz2 = _branch_grad(dout, T, C, dt, S["dp2"], N, p_ff, seeds[3])
-        dz1 = _dgrad_act(dz2, W_["w2"], S["z1"], act, p_ff, seeds[2])
+        dz1 = _dgrad_act(dz2, W_["w2"], S["z1"], act, p_ff, seeds[2], wt=W_["w2_t"])
         gw2, gb2 = _wgrad(dz2, S["h"]), _colsum(dz2)
-        da2 = _dgrad(dz1, W_["w1"])
+        da2 = _dgrad(dz1, W_["w1"], W_["w1_t"])
         gw1, gb1 = _wgrad(dz1, S["a2"]), _colsum(dz1)
         dt2 = _empty((T, C), sdt, dev)
         gn2g, gn2b = sp.ln_bwd(_dense(S["t2"]), S["s2"], W_["n2g"], _dense(da2), _dense(dt2), T, C, add=_dense(dout))
         # attention branch
         dzo = _branch_grad(dt2, T, C, dt, S["dp1"], N, p_ff, seeds[1])
-        do = _dgrad(dzo, W_["wo"])
+        do = _dgrad(dzo, W_["wo"], W_["wo_t"])
         gwo = _wgrad(dzo, S["o"])
         qkvn, Pm, Pd = S["qkvn"], S["P"], S["Pd"]
         scale = 1.0 / math.sqrt(hd)
@@ -541,7 +633,7 @@ class _EncoderFn(torch.autograd.Function):
                                  Rows(dqkv, hd, Hn, 3 * Hn, 0), T * Hn, hd)
             gkg, gkb = sp.ln_bwd(Rows(qkv, hd, Hn, 3 * Hn, Hn), S["sk"], W_["kg"], Rows(dqk, hd, Hn, 3 * Hn, Hn),
                                  Rows(dqkv, hd, Hn, 3 * Hn, Hn), T * Hn, hd)
-        da1 = _dgrad(dqkv, W_["wqkv"])
+        da1 = _dgrad(dqkv, W_["wqkv"], W_["wqkv_t"])
         gqkv = _wgrad(dqkv, S["a1"])
         dx = dt2
         gn1g, gn1b = sp.ln_bwd(_dense(S["tok"]), S["s1"], W_["n1g"], _dense(da1), _dense(dx), T, C, add=_dense(dx))
@@ -1006,6 +1098,15 @@ def train_pos_embedding(emb, x: torch.Tensor, num_registers: int):
 
 def train_forward(model, x: torch.Tensor, num_registers: int = 3, return_raw_outputs: bool = False):
     """MainModel.forward in training mode (model.py:129-149 with dropout / drop path active)."""
+    global _WPREP
+    _WPREP = _prep_weights(model, compute_dtype(x, model))
+    try:
+        return _train_forward(model, x, num_registers, return_raw_outputs)
+    finally:
+        _WPREP = None
+
+
+def _train_forward(model, x: torch.Tensor, num_registers: int, return_raw_outputs: bool):
     dt = compute_dtype(x, model)
     B, _, Hi, Wi = x.shape
     p = model.conv_init.patch_size
@@ -1061,6 +1162,15 @@ def tape_forward(model, x: torch.Tensor, num_registers: int, dt):
     kept on a tape (no autograd graph), for the opaque torch.compile custom op
     (sdpnet_ops.train_forward).  Same kernels, same order, same RNG draws as train_forward,
     so a compiled step is bit-identical to an eager one."""
+    global _WPREP
+    _WPREP = _prep_weights(model, dt)
+    try:
+        return _tape_forward(model, x, num_registers, dt)
+    finally:
+        _WPREP = None
+
+
+def _tape_forward(model, x: torch.Tensor, num_registers: int, dt):
     B, _, Hi, Wi = x.shape
     p = model.conv_init.patch_size
     Hp, Wp = Hi // p, Wi // p

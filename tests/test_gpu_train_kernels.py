@@ -311,6 +311,31 @@ def test_ce_loss_label_out_of_range_is_nan_not_oob():
     assert bad.tolist() == [False, False, True, False, True, False, False, False]
 
 
+def test_mt_cast_transpose():
+    # one launch, ragged shapes, a stacked destination (the fused q/k/v weight) and NULL outputs
+    shapes = [(768, 768), (100, 70), (768, 588), (3, 130), (64, 64)]
+    srcs = [rnd(r, c, seed=40 + i) for i, (r, c) in enumerate(shapes)]
+    jobs, outs = [], []
+    for i, x in enumerate(srcs):
+        d = torch.zeros(x.shape, dtype=BF, device=DEV) if i != 3 else None
+        t = torch.zeros(x.shape[::-1], dtype=BF, device=DEV) if i != 4 else None
+        jobs.append((x, d, t))
+        outs.append((d, t))
+    stacked = torch.zeros(3 * 256, 256, dtype=BF, device=DEV)
+    stacked_t = torch.zeros(256, 3 * 256, dtype=BF, device=DEV)
+    parts = [rnd(256, 256, seed=50 + j) for j in range(3)]
+    for j, x in enumerate(parts):
+        jobs.append((x, stacked[j * 256:(j + 1) * 256], stacked_t[:, j * 256:(j + 1) * 256]))
+    sp.mt_cast_transpose(jobs)
+    for x, (d, t) in zip(srcs, outs):
+        if d is not None:
+            assert torch.equal(d, x.to(BF))
+        if t is not None:
+            assert torch.equal(t, x.to(BF).t())
+    ref = torch.cat(parts, 0).to(BF)
+    assert torch.equal(stacked, ref) and torch.equal(stacked_t, ref.t())
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
 @pytest.mark.parametrize("R,C", [(768, 3072), (100, 37), (1, 64)])
 def test_transpose(dtype, R, C):

@@ -502,6 +502,48 @@ def test_xl_full_size_training_step_is_deterministic():
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.gpu
+def test_batched_weight_prep_is_bit_identical_over_two_steps():
+    """The per-step bf16 weight operands (and their transposes for the input-gradient GEMMs)
+    built in one sdp_mt_cast_transpose launch give the same bits as the per-weight cast /
+    transpose path, over two AdamW steps (the second forward must see the updated weights)."""
+    import model as ours
+    import sdpnet_train
+    cfg = dict(XL_TRAIN_CFG, num_blocks=2, ffn_dropout=0.2, attn_dropout=0.2)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(4, 3, 224, 224, generator=g).to(DEV)
+    y = torch.randint(0, 1000, (4,), generator=g).to(DEV)
+    res = {}
+    old = sdpnet_train._WPREP_ON
+    try:
+        for on in (True, False):
+            sdpnet_train._WPREP_ON = on
+            torch.manual_seed(231424314)
+            m = ours.MainModel.from_dict(**cfg).to(DEV).train()
+            opt = sdpnet_train.AdamW(m.parameters(), lr=0.01, weight_decay=0.05)
+            grads = []
+            for step in range(2):
+                torch.manual_seed(100 + step)
+                m.zero_grad(set_to_none=True)
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = sdpnet_train.cross_entropy(m(x), y, 0.1)
+                loss.backward()
+                grads.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]).cpu())
+                opt.step(grad_scale=1.0, max_norm=5.0)
+            torch.cuda.synchronize()
+            res[on] = grads
+            assert on == ("_sdp_wprep" in m.__dict__)
+    finally:
+        sdpnet_train._WPREP_ON = old
+    for a, b in zip(res[True], res[False]):
+        assert torch.equal(a, b)
+
+
+def test_mt_cast_transpose_entry_layout():
+    import sdpnet_hip as sp
+    assert sp.lib().sdp_mt_cast_transpose_entry_bytes() == 48
+
+
 class _OracleModule(torch.nn.Module):
     """The oracle forward (reference math, stock torch CPU ops) as a module whose parameters
     DDP can hook (CPU gloo test of the data-parallel gradient average)."""
