@@ -482,6 +482,16 @@ int sdp_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t ldb, float
                    int64_t split_stride, int ni, int nj, int ktok, int kchunk_tiles, const void* zrow,
                    void* stream);
 
+/* Y = dropout(X) * scale[m / sgrp] (+ R) (mode 1) or Y = dropout(round(X * scale)) (mode 2), the
+ * counter-hash mask of sdp_act_fwd (index m * N + n): the dropout of EncoderLayer's output
+ * projections fused into the drop-path / residual pass (layers.py:301-309) and, mode 2, into the
+ * cast of the stream gradient into that branch.  X in x_dtype, R / Y in y_dtype; 16-B aligned
+ * rows, N % 8 == 0 (hipErrorNotSupported otherwise). */
+int sdp_rowscale_add_dropout(int x_dtype, int y_dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride,
+                             int x_off, const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp,
+                             int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride,
+                             int y_off, int M, int N, float p, uint64_t seed, int mode, void* stream);
+
 /* Per-step weight preparation of the bf16 training step in one launch: entries is a device
  * array of sdp_mt_cast_transpose_entry_bytes()-sized records {const float* src; uint16_t* dst;
  * uint16_t* dstT; int64 ldd; int64 ldt; int R; int C} (fp32 [R][C] row-major in; bf16 copy

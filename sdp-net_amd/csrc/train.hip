@@ -487,9 +487,10 @@ template <typename TX, typename TY>
 __global__ __launch_bounds__(256) void rowscale_v8(const TX* __restrict__ X, int64_t ldx, RowMap xm,
                                                    const float* __restrict__ sc, int sgrp, const TY* __restrict__ R,
                                                    int64_t ldr, RowMap rm, TY* __restrict__ Y, int64_t ldy, RowMap ym,
-                                                   int M, int N, int act) {
+                                                   int M, int N, int act, float p, uint64_t seed, int dmode) {
   const int n8 = N >> 3;
   const int64_t total = (int64_t)M * n8;
+  const float inv = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     const int64_t m = e / n8;
     const int n = (int)(e - m * n8) * 8;
@@ -498,6 +499,11 @@ __global__ __launch_bounds__(256) void rowscale_v8(const TX* __restrict__ X, int
     if (act != ACT_NONE) {  // = sdp_act_fwd's stored output (rounded to TX) without the round trip
 #pragma unroll
       for (int q = 0; q < 8; ++q) x.v[q] = to_f<TX>(from_f<TX>(apply_act(act, x.v[q])));
+    }
+    if (dmode == 1) {  // dropout on the branch (= sdp_act_fwd / sdp_act_bwd with no activation, rounded to TX)
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        x.v[q] = to_f<TX>(from_f<TX>(uniform01(seed, (uint64_t)m * N + n + q) >= p ? x.v[q] * inv : 0.f));
     }
     const float s_ = sc ? sc[m / sgrp] : 1.0f;
     V8<TY> y;
@@ -508,6 +514,13 @@ __global__ __launch_bounds__(256) void rowscale_v8(const TX* __restrict__ X, int
     } else {
 #pragma unroll
       for (int q = 0; q < 8; ++q) y.v[q] = x.v[q] * s_;
+    }
+    if (dmode == 2) {  // dropout on the rounded output (a stream gradient cast into a dropout branch)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float r = to_f<TY>(from_f<TY>(y.v[q]));
+        y.v[q] = uniform01(seed, (uint64_t)m * N + n + q) >= p ? r * inv : 0.f;
+      }
     }
     y.store(Y + ym(m) * ldy + n);
   }
@@ -639,8 +652,10 @@ __global__ __launch_bounds__(256) void rowscale_k(const T* __restrict__ X, int64
 static int rowscale_impl(int xdt, int ydt, int act, const void* X, int64_t ldx, int x_grp, int64_t x_gstride,
                          int x_off, const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp,
                          int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off,
-                         int M, int N, void* stream) {
+                         int M, int N, void* stream, float p = 0.f, uint64_t seed = 0, int dmode = 0) {
   if (!X || !Y || M < 0 || N < 0 || (scale && sgrp <= 0) || act < 0 || act > ACT_KELU) return (int)hipErrorInvalidValue;
+  if (p < 0.f || p >= 1.f || dmode < 0 || dmode > 2) return (int)hipErrorInvalidValue;
+  if (p == 0.f) dmode = 0;
   if ((int64_t)M * N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), rm = mk_tmap(r_grp, r_gstride, r_off),
@@ -652,11 +667,12 @@ static int rowscale_impl(int xdt, int ydt, int act, const void* X, int64_t ldx, 
       using TX = typename decltype(tx)::type;
       using TY = typename decltype(ty)::type;
       hipLaunchKernelGGL((rowscale_v8<TX, TY>), dim3(gv), dim3(256), 0, s, (const TX*)X, ldx, xm, scale, sgrp,
-                         (const TY*)R, ldr, rm, (TY*)Y, ldy, ym, M, N, act);
+                         (const TY*)R, ldr, rm, (TY*)Y, ldy, ym, M, N, act, p, seed, dmode);
       return SDP_CHECK_LAUNCH();
     });
   }
   if (xdt != ydt) return (int)hipErrorInvalidValue;  // mixed dtypes: 16-B aligned rows, N % 8 == 0 only
+  if (dmode) return (int)hipErrorNotSupported;       // fused dropout: the vector path only
   const int g = ew_grid((int64_t)M * N);
   if (xdt == 1)
     hipLaunchKernelGGL(rowscale_k<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)X, ldx, xm, scale, sgrp,
@@ -695,6 +711,22 @@ extern "C" int sdp_rowscale_add_mixed(int x_dtype, int y_dtype, int act, const v
                                       int y_grp, int64_t y_gstride, int y_off, int M, int N, void* stream) {
   return rowscale_impl(x_dtype, y_dtype, act, X, ldx, x_grp, x_gstride, x_off, scale, sgrp, R, ldr, r_grp, r_gstride,
                        r_off, Y, ldy, y_grp, y_gstride, y_off, M, N, stream);
+}
+
+// The same with a dropout mask (the counter hash of sdp_act_fwd / sdp_act_bwd, index m * N + n
+// over the logical rows): mode 1 drops the branch X before the scale and the residual add,
+// y = dropout(X) * scale + R (EncoderLayer's x + drop_path(dropout(proj(.))), layers.py:301-309);
+// mode 2 drops the rounded output, y = dropout(round(X * scale)) (its gradient cast into the
+// branch).  Bit-identical to sdp_act_fwd / sdp_act_bwd followed by sdp_rowscale_add[_mixed] and
+// the reverse; 16-B aligned rows and N % 8 == 0 only (hipErrorNotSupported otherwise).
+extern "C" int sdp_rowscale_add_dropout(int x_dtype, int y_dtype, const void* X, int64_t ldx, int x_grp,
+                                        int64_t x_gstride, int x_off, const float* scale, int sgrp, const void* R,
+                                        int64_t ldr, int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy,
+                                        int y_grp, int64_t y_gstride, int y_off, int M, int N, float p, uint64_t seed,
+                                        int mode, void* stream) {
+  if (mode != 1 && mode != 2) return (int)hipErrorInvalidValue;
+  return rowscale_impl(x_dtype, y_dtype, ACT_NONE, X, ldx, x_grp, x_gstride, x_off, scale, sgrp, R, ldr, r_grp,
+                       r_gstride, r_off, Y, ldy, y_grp, y_gstride, y_off, M, N, stream, p, seed, mode);
 }
 
 // ---------------------------------------------------------------------------

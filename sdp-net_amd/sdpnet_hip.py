@@ -25,6 +25,7 @@ F32, BF16 = 0, 1
 ACT_CODES = {"none": 0, "gelu": 1, "relu": 2, "tanh": 3, "sigmoid": 4, "leaky_relu": 5, "selu": 6, "kelu": 7}
 
 _i32, _i64, _f32, _vp, _u64 = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint64
+_HIP_NOT_SUPPORTED = 801  # hipErrorNotSupported
 _ROWMAP = [_i32, _i64, _i32]
 
 # Signatures, in the order of include/sdpnet_hip.h.
@@ -92,6 +93,8 @@ _SIGS = {
                             _i32, _f32, _u64, _vp], _i32),
     "sdp_rowscale_add_mixed": ([_i32, _i32, _i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64,
                                 *_ROWMAP, _i32, _i32, _vp], _i32),
+    "sdp_rowscale_add_dropout": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64,
+                                  *_ROWMAP, _i32, _i32, _f32, _u64, _i32, _vp], _i32),
     "sdp_ln_fwd_mixed": ([_i32, _i32, _vp, _i64, *_ROWMAP, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp],
                          _i32),
     "sdp_ln_bwd_mixed": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _vp,
@@ -682,12 +685,33 @@ def act_bwd(Z: torch.Tensor, DY: torch.Tensor, DZ: torch.Tensor, M: int, N: int,
 
 
 def rowscale_add(x: Rows, y: Rows, M: int, N: int, scale: Optional[torch.Tensor] = None, sgrp: int = 1,
-                 resid: Optional[Rows] = None, act: int = 0):
+                 resid: Optional[Rows] = None, act: int = 0, p: float = 0.0, seed: int = 0, dmode: int = 0):
     """y = act(x) * scale[m / sgrp] (+ resid) over row maps (act 0: sdp_rowscale_add).  x may
-    differ in dtype from y (resid has y's dtype): sdp_rowscale_add_mixed."""
+    differ in dtype from y (resid has y's dtype): sdp_rowscale_add_mixed.  p > 0 with dmode 1 /
+    2: dropout (counter hash, index m * N + n) on x / on the rounded output
+    (sdp_rowscale_add_dropout; act must be 0)."""
     _need_cuda(x.t, y.t, scale)
     _req(scale is None or scale.dtype == torch.float32, "rowscale scale fp32")
     _req(resid is None or resid.t.dtype == y.t.dtype, "rowscale resid dtype = y dtype")
+    if p > 0 and dmode:
+        _req(act == 0 and dmode in (1, 2), "rowscale dropout: no activation, mode 1 or 2")
+        rc = lib().sdp_rowscale_add_dropout(dcode(x.t.dtype), dcode(y.t.dtype), *x.args(), _ptr(scale), sgrp,
+                                            *_rows_args(resid), *y.args(), M, N, float(p),
+                                            int(seed) & 0xFFFFFFFFFFFFFFFF, int(dmode), _stream(y.t))
+        if rc != _HIP_NOT_SUPPORTED:
+            _check(rc, "rowscale_add_dropout")
+            return
+        # unaligned rows / N % 8 != 0: the same arithmetic as two passes (dense operands only)
+        _req(x.t.is_contiguous() and x.t.shape[-1] == N and y.t.is_contiguous() and y.t.shape[-1] == N,
+             "rowscale dropout fallback: dense rows")
+        if dmode == 1:
+            tmp = torch.empty(M, N, dtype=x.t.dtype, device=x.t.device)
+            act_fwd(x.t, tmp, M, N, 0, p, seed)
+            rowscale_add(Rows(tmp, N), y, M, N, scale=scale, sgrp=sgrp, resid=resid)
+        else:
+            rowscale_add(x, y, M, N, scale=scale, sgrp=sgrp, resid=resid)
+            act_bwd(y.t, y.t, y.t, M, N, 0, p, seed)
+        return
     if x.t.dtype != y.t.dtype:
         rc = lib().sdp_rowscale_add_mixed(dcode(x.t.dtype), dcode(y.t.dtype), int(act), *x.args(), _ptr(scale), sgrp,
                                           *_rows_args(resid), *y.args(), M, N, _stream(y.t))

@@ -252,6 +252,8 @@ def _wprep(key, dt):
 
 
 _WGRAD_8PH = os.environ.get("SDPNET_WGRAD_8PH", "1") != "0"
+# dropout of the encoder's output projections fused into the drop-path / residual pass (A/B knob)
+_DMODE = 1 if os.environ.get("SDPNET_FUSED_DROPOUT", "1") != "0" else 0
 
 
 def _wgrad_8ph_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
@@ -332,19 +334,22 @@ def _branch_grad(d: torch.Tensor, T: int, C: int, dt, dp: Optional[torch.Tensor]
     An fp32 stream gradient is rounded to the bf16 branch first (with the drop-path scale),
     then the dropout mask is applied in place."""
     if d.dtype != dt:
-        out = _dense_copy(_dense(d), T, C, dt, dp, grp)
-        if p > 0:
-            sp.act_bwd(out, out, out, T, C, 0, p, seed)
+        out = _empty((T, C), dt, d.device)
+        # one pass: cast (with the drop-path scale), then the dropout mask on the rounded value
+        if _DMODE:
+            sp.rowscale_add(_dense(d), _dense(out), T, C, scale=dp, sgrp=grp, p=p, seed=seed, dmode=2)
+        else:
+            sp.rowscale_add(_dense(d), _dense(out), T, C, scale=dp, sgrp=grp)
+            if p > 0:
+                sp.act_bwd(out, out, out, T, C, 0, p, seed)
         return out
     if p <= 0 and dp is None:
         return d
     out = _empty((T, C), dt, d.device)
-    if p > 0:
+    if not _DMODE and p > 0:
         sp.act_bwd(d, d, out, T, C, 0, p, seed)
-        if dp is not None:
-            sp.rowscale_add(_dense(out), _dense(out), T, C, scale=dp, sgrp=grp)
-    else:
-        sp.rowscale_add(_dense(d), _dense(out), T, C, scale=dp, sgrp=grp)
+        d = out
+    sp.rowscale_add(_dense(d), _dense(out), T, C, scale=dp, sgrp=grp, p=p, seed=seed, dmode=_DMODE)
     return out
 
 
@@ -569,19 +574,21 @@ class _EncoderFn(torch.autograd.Function):
 
         # x = x + drop_path1(dropout(o_proj(o)))                       (:300-303)
         zo = _linear(o, W_["wo"], None, dt)
-        if p_ff > 0:
-            sp.act_fwd(zo, zo, T, C, 0, p_ff, seeds[1])
         t2 = _empty((T, C), tok.dtype, dev)                               # stream dtype
-        sp.rowscale_add(_dense(zo), _dense(t2), T, C, scale=dp1, sgrp=N, resid=_dense(tok))
+        if not _DMODE and p_ff > 0:
+            sp.act_fwd(zo, zo, T, C, 0, p_ff, seeds[1])
+        sp.rowscale_add(_dense(zo), _dense(t2), T, C, scale=dp1, sgrp=N, resid=_dense(tok), p=p_ff, seed=seeds[1],
+                        dmode=_DMODE)                                     # dropout + drop path + residual
         del zo
         # x = x + drop_path2(dropout(ff2(dropout(act(ff1(LN2 x))))))   (:306-309)
         a2, s2 = _ln_fwd(_dense(t2), T, C, W_["n2g"], W_["n2b"], e.norm2.eps, dt)
         z1, h = _linear_act(a2, W_["w1"], W_["b1"], dt, act, p_ff, seeds[2])
         z2 = _linear(h, W_["w2"], W_["b2"], dt)
-        if p_ff > 0:
-            sp.act_fwd(z2, z2, T, C, 0, p_ff, seeds[3])
         out = _empty((T, C), tok.dtype, dev)
-        sp.rowscale_add(_dense(z2), _dense(out), T, C, scale=dp2, sgrp=N, resid=_dense(t2))
+        if not _DMODE and p_ff > 0:
+            sp.act_fwd(z2, z2, T, C, 0, p_ff, seeds[3])
+        sp.rowscale_add(_dense(z2), _dense(out), T, C, scale=dp2, sgrp=N, resid=_dense(t2), p=p_ff, seed=seeds[3],
+                        dmode=_DMODE)
         ctx.st = dict(tok=tok, a1=a1, s1=s1, qkv=qkv, qkvn=qkvn, sq=sq, sk=sk, P=Pm, Pd=Pd, lse=lse, o=o, t2=t2, a2=a2, s2=s2,
                       z1=z1, h=h, W=W_, seeds=seeds, dp1=dp1, dp2=dp2, geo=(B, N, C, Hn, hd, Np), act=act, dt=dt,
                       p_ff=p_ff, p_att=p_att, qn=qn)

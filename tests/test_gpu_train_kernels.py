@@ -311,6 +311,34 @@ def test_ce_loss_label_out_of_range_is_nan_not_oob():
     assert bad.tolist() == [False, False, True, False, True, False, False, False]
 
 
+@pytest.mark.parametrize("xdt,ydt", [(BF, torch.float32), (BF, BF), (torch.float32, BF)])
+@pytest.mark.parametrize("with_scale", [False, True])
+def test_rowscale_dropout_fused_is_bit_identical(xdt, ydt, with_scale):
+    # EncoderLayer's x + drop_path(dropout(proj)) (mode 1) and its gradient cast into the branch
+    # (mode 2) in one pass == act_fwd / act_bwd (dropout only) + rowscale_add, bit for bit
+    M, N, grp, p, seed = 780, 768, 260, 0.2, 12345
+    x = rnd(M, N, seed=60, dtype=xdt)
+    r = rnd(M, N, seed=61, dtype=ydt)
+    sc = (torch.rand(M // grp, generator=torch.Generator().manual_seed(2)) + 0.5).to(DEV) if with_scale else None
+    if xdt == BF:  # mode 1: branch x (bf16) into the stream (ydt) with the residual
+        got = torch.empty(M, N, dtype=ydt, device=DEV)
+        sp.rowscale_add(sp.dense(x), sp.dense(got), M, N, scale=sc, sgrp=grp, resid=sp.dense(r), p=p, seed=seed,
+                        dmode=1)
+        tmp = torch.empty_like(x)
+        sp.act_fwd(x, tmp, M, N, 0, p, seed)
+        ref = torch.empty(M, N, dtype=ydt, device=DEV)
+        sp.rowscale_add(sp.dense(tmp), sp.dense(ref), M, N, scale=sc, sgrp=grp, resid=sp.dense(r))
+        assert torch.equal(got, ref)
+        assert 0.15 < float((tmp == 0).float().mean()) < 0.25
+    # mode 2: x cast into a bf16 branch, then the dropout mask on the rounded value
+    got = torch.empty(M, N, dtype=ydt, device=DEV)
+    sp.rowscale_add(sp.dense(x), sp.dense(got), M, N, scale=sc, sgrp=grp, p=p, seed=seed, dmode=2)
+    ref = torch.empty(M, N, dtype=ydt, device=DEV)
+    sp.rowscale_add(sp.dense(x), sp.dense(ref), M, N, scale=sc, sgrp=grp)
+    sp.act_bwd(ref, ref, ref, M, N, 0, p, seed)
+    assert torch.equal(got, ref)
+
+
 def test_mt_cast_transpose():
     # one launch, ragged shapes, a stacked destination (the fused q/k/v weight) and NULL outputs
     shapes = [(768, 768), (100, 70), (768, 588), (3, 130), (64, 64)]
