@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--bench-log")
     ap.add_argument("--out", default=os.path.join(REPO, "profiles"))
+    ap.add_argument("--cmd", default="bench.py --steps 3 --warmup 1 --no-graph --streams 1 --no-cpu-baseline "
+                                     "--prof-steps 1", help="the profiled bench.py arguments (for the summary text)")
+    ap.add_argument("--graph", action="store_true", help="the profiled command replays the 2-stream HIP graph")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
 
@@ -93,11 +96,16 @@ def main():
 
     L = [f"# {args.round}: rocprofv3 kernel summary of bench.py (SdP-Net-M, bs 256, bf16, 1 GPU)", ""]
     L.append("Command (kernel trace): `rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv "
-             "-- python bench.py --steps 3 --warmup 1 --no-graph --streams 1 --no-cpu-baseline --prof-steps 1`  ")
+             f"-- python {args.cmd}`  ")
     L.append("PMC passes: the same command under `rocprofv3 --pmc FETCH_SIZE` and, separately, `--pmc WRITE_SIZE`.  ")
-    L.append("Un-graphed, single stream: 5 forwards (1 warmup + 3 timed + 1 event-timed pass), identical launch mix. "
-             "Raw rocprof summary: "
-             f"`{args.round}_kernel_stats.csv`.")
+    if args.graph:
+        L.append("The benchmarked configuration: HIP-graph replay with 2 sub-batch streams (every GEMM launch is a "
+                 "128-image half batch; the profiler serialises dispatches for the PMC passes), warmup + timed + "
+                 "event-timed forwards, identical launch mix. Raw rocprof summary: "
+                 f"`{args.round}_kernel_stats.csv`.")
+    else:
+        L.append("Un-graphed, single stream: 5 forwards (1 warmup + 3 timed + 1 event-timed pass), identical launch "
+                 f"mix. Raw rocprof summary: `{args.round}_kernel_stats.csv`.")
     L.append("")
     L.append("| kernel (all instantiations) | calls | total ms | % | avg µs | HBM MB / call (PMC) |")
     L.append("|---|---|---|---|---|---|")
@@ -145,7 +153,7 @@ def main():
             L.append(f"| {k} | {v['launches']} | {v['avg_us']} | {v['tflops']} | {v['kernel']} |")
         L.append("")
         L.append(f"bench line of the profiled run: value {bench['value']} img/s, {bench['ms_per_step']} ms/step "
-                 "(un-graphed, 1 stream, under the profiler — not the headline number).")
+                 "(under the profiler — not the headline number).")
     if trace:
         L.append("")
         L.append(f"Per-dispatch trace kept on the box only (`{os.path.basename(trace)}`); the stats CSV is committed.")
