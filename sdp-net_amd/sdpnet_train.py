@@ -285,6 +285,46 @@ def _wgrad_8ph(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return dw
 
 
+# Weight-gradient work of a layer's backward (dW GEMMs, bias column sums, the depthwise weight
+# gradient) is off the critical dX chain: it runs on a side stream, so its workgroups fill the
+# partial tile rounds of the dX GEMMs and the memory-bound passes, and the main stream waits for it
+# before the layer's backward returns (autograd / DDP hooks only ever see finished gradients).
+_WSTREAM = os.environ.get("SDPNET_WGRAD_STREAM", "1") != "0"
+_SIDE_STREAMS = {}
+
+
+class _Side:
+    def __init__(self, dev):
+        self.on = _WSTREAM and dev.type == "cuda"
+        if self.on:
+            self.main = torch.cuda.current_stream(dev)
+            key = (dev.index, self.main.cuda_stream)
+            if key not in _SIDE_STREAMS:
+                _SIDE_STREAMS[key] = torch.cuda.Stream(device=dev)
+            self.side = _SIDE_STREAMS[key]
+
+    def run(self, fn, *inputs):
+        """fn() on the side stream after everything queued on the main stream so far; its input
+        tensors are kept from reuse until the side stream has read them, its outputs until the
+        main stream's work on them is done."""
+        if not self.on:
+            return fn()
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            out = fn()
+        for t in inputs:
+            if t is not None:
+                t.record_stream(self.side)
+        for o in (out if isinstance(out, tuple) else (out,)):
+            if o is not None:
+                o.record_stream(self.main)
+        return out
+
+    def join(self):
+        if self.on:
+            self.main.wait_stream(self.side)
+
+
 def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """dW [N, K] fp32 = dy^T x, reduction over the M token rows split across workgroups."""
     if _wgrad_8ph_ok(dy, x):
@@ -442,9 +482,11 @@ class _MixerFn(torch.autograd.Function):
         dz3 = _dense_copy(iout, M, C, dt, S["dp1"], P)
         dz2 = _dgrad_act(dz3, W_["dnw"], S["z2"], act, wt=W_["dnw_t"])
         has = S["has"]  # [g1, b1, dww, dwb, ccw, ccb, g2, b2, upw, upb, dnw, dnb]: bias grads only if the bias exists
-        gdn, gdnb = _wgrad(dz3, S["h"]), (_colsum(dz3) if has[11] else None)
+        side = _Side(dev)
+        h_, a2_, d_, a1_ = S["h"], S["a2"], S["d"], S["a1"]
+        gdn, gdnb = side.run(lambda: (_wgrad(dz3, h_), _colsum(dz3) if has[11] else None), dz3, h_)
         da2 = _dgrad(dz2, W_["upw"], W_["upw_t"])
-        gup, gupb = _wgrad(dz2, S["a2"]), (_colsum(dz2) if has[9] else None)
+        gup, gupb = side.run(lambda: (_wgrad(dz2, a2_), _colsum(dz2) if has[9] else None), dz2, a2_)
         dmid = _with_regs(dout, B, R, N, C)
         imid = Rows(dmid, C, P, N, R)
         gg2, gb2 = sp.ln_bwd(Rows(S["mid"], C, P, N, R), S["s2"], W_["g2"], _dense(da2), imid, M, C, add=iout)
@@ -453,16 +495,17 @@ class _MixerFn(torch.autograd.Function):
         dz1 = _empty((M, C), dt, dev)
         sp.act_bwd(S["z1"], dh1, dz1, M, C, act)
         dd = _dgrad(dz1, W_["ccw"], W_["ccw_t"])
-        gcc, gccb = _wgrad(dz1, S["d"]), (_colsum(dz1) if has[5] else None)
+        gcc, gccb = side.run(lambda: (_wgrad(dz1, d_), _colsum(dz1) if has[5] else None), dz1, d_)
         da1 = _empty((M, C), dt, dev)
         wflip = W_["dww"].view(C, k, k).flip(1, 2).reshape(C, k * k).contiguous()
         sp.dwconv(_dense(dd), wflip, None, _dense(da1), B, H, W, C, k)
-        gdw = sp.dw_wgrad(_dense(S["a1"]), _dense(dd), B, H, W, C, k)
-        gdwb = _colsum(dd) if has[3] else None
+        gdw, gdwb = side.run(lambda: (sp.dw_wgrad(_dense(a1_), _dense(dd), B, H, W, C, k),
+                                      _colsum(dd) if has[3] else None), a1_, dd)
         dx = dmid  # residual; LN1's input gradient is added in place on the image rows
         idx = Rows(dx, C, P, N, R)
         gg1, gb1 = sp.ln_bwd(Rows(S["tok"], C, P, N, R), S["s1"], W_["g1"], _dense(da1), idx, M, C, add=idx)
         grads = [gg1, gb1, gdw, gdwb, gcc, gccb, gg2, gb2, gup, gupb, gdn, gdnb]
+        side.join()
         ctx.st = None
         return (dx, None, None, None, *[g.view(shp) if h else None for g, shp, h in zip(grads, ctx.shapes, S["has"])])
 
@@ -608,15 +651,17 @@ class _EncoderFn(torch.autograd.Function):
         # FFN branch
         dz2 = _branch_grad(dout, T, C, dt, S["dp2"], N, p_ff, seeds[3])
         dz1 = _dgrad_act(dz2, W_["w2"], S["z1"], act, p_ff, seeds[2], wt=W_["w2_t"])
-        gw2, gb2 = _wgrad(dz2, S["h"]), _colsum(dz2)
+        side = _Side(dev)
+        h_, a2_, o_, a1_ = S["h"], S["a2"], S["o"], S["a1"]
+        gw2, gb2 = side.run(lambda: (_wgrad(dz2, h_), _colsum(dz2)), dz2, h_)
         da2 = _dgrad(dz1, W_["w1"], W_["w1_t"])
-        gw1, gb1 = _wgrad(dz1, S["a2"]), _colsum(dz1)
+        gw1, gb1 = side.run(lambda: (_wgrad(dz1, a2_), _colsum(dz1)), dz1, a2_)
         dt2 = _empty((T, C), sdt, dev)
         gn2g, gn2b = sp.ln_bwd(_dense(S["t2"]), S["s2"], W_["n2g"], _dense(da2), _dense(dt2), T, C, add=_dense(dout))
         # attention branch
         dzo = _branch_grad(dt2, T, C, dt, S["dp1"], N, p_ff, seeds[1])
         do = _dgrad(dzo, W_["wo"], W_["wo_t"])
-        gwo = _wgrad(dzo, S["o"])
+        gwo = side.run(lambda: _wgrad(dzo, o_), dzo, o_)
         qkvn, Pm, Pd = S["qkvn"], S["P"], S["Pd"]
         scale = 1.0 / math.sqrt(hd)
         # dQ / dK land in dqk, dV in dqkv (the same buffer unless the q/k head LayerNorm follows)
@@ -641,11 +686,14 @@ class _EncoderFn(torch.autograd.Function):
             gkg, gkb = sp.ln_bwd(Rows(qkv, hd, Hn, 3 * Hn, Hn), S["sk"], W_["kg"], Rows(dqk, hd, Hn, 3 * Hn, Hn),
                                  Rows(dqkv, hd, Hn, 3 * Hn, Hn), T * Hn, hd)
         da1 = _dgrad(dqkv, W_["wqkv"], W_["wqkv_t"])
-        gqkv = _wgrad(dqkv, S["a1"])
-        dx = dt2
-        gn1g, gn1b = sp.ln_bwd(_dense(S["tok"]), S["s1"], W_["n1g"], _dense(da1), _dense(dx), T, C, add=_dense(dx))
+        gqkv = side.run(lambda: _wgrad(dqkv, a1_), dqkv, a1_)
+        # dzo may BE dt2 (no dropout / drop path): with the side stream still reading it, the LN
+        # backward adds into a fresh buffer instead of updating dt2 in place
+        dx = _empty((T, C), sdt, dev) if side.on else dt2
+        gn1g, gn1b = sp.ln_bwd(_dense(S["tok"]), S["s1"], W_["n1g"], _dense(da1), _dense(dx), T, C, add=_dense(dt2))
         grads = [gn1g, gn1b, gqkv[:C], gqkv[C:2 * C], gqkv[2 * C:], gqg, gqb, gkg, gkb, gwo, gn2g, gn2b, gw1, gb1,
                  gw2, gb2]
+        side.join()
         has = ctx.has
         ctx.st = None
         return (dx, None, None, None, None, *[g if h else None for g, h in zip(grads, has)])

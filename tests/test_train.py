@@ -539,6 +539,41 @@ def test_batched_weight_prep_is_bit_identical_over_two_steps():
         assert torch.equal(a, b)
 
 
+@pytest.mark.gpu
+def test_side_stream_weight_gradients_are_bit_identical():
+    """The layers' weight gradients computed on the side stream (overlapping the dX chain) equal
+    the single-stream ones bit for bit, and the step after them sees finished gradients."""
+    import model as ours
+    import sdpnet_train
+    cfg = dict(XL_TRAIN_CFG, num_blocks=2, ffn_dropout=0.2, attn_dropout=0.2)
+    g = torch.Generator(device="cpu").manual_seed(6)
+    x = torch.randn(4, 3, 224, 224, generator=g).to(DEV)
+    y = torch.randint(0, 1000, (4,), generator=g).to(DEV)
+    res = {}
+    old = sdpnet_train._WSTREAM
+    try:
+        for on in (True, False):
+            sdpnet_train._WSTREAM = on
+            torch.manual_seed(231424314)
+            m = ours.MainModel.from_dict(**cfg).to(DEV).train()
+            opt = sdpnet_train.AdamW(m.parameters(), lr=0.01, weight_decay=0.05)
+            out = []
+            for step in range(2):
+                torch.manual_seed(200 + step)
+                m.zero_grad(set_to_none=True)
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = sdpnet_train.cross_entropy(m(x), y, 0.1)
+                loss.backward()
+                out.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]).cpu())
+                opt.step(grad_scale=1.0, max_norm=5.0)
+            out.append(torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu())
+            res[on] = out
+    finally:
+        sdpnet_train._WSTREAM = old
+    for a, b in zip(res[True], res[False]):
+        assert torch.equal(a, b)
+
+
 def test_mt_cast_transpose_entry_layout():
     import sdpnet_hip as sp
     assert sp.lib().sdp_mt_cast_transpose_entry_bytes() == 48
