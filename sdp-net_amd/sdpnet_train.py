@@ -43,6 +43,7 @@ from __future__ import annotations
 
 import math
 import os
+import struct
 from typing import List, Optional
 
 import torch
@@ -208,7 +209,6 @@ def _prep_weights(model, dt) -> Optional[dict]:
     sig = tuple((k, r, c, tuple((p.data_ptr(), off) for p, off in ps)) for k, ps, r, c in jobs)
     st = model.__dict__.get("_sdp_wprep")
     if st is None or st["dev"] != dev or st["shapes"] != tuple((k, r, c) for k, _, r, c in jobs):
-        import struct
         bufs, tiles = {}, []
         for k, ps, r, c in jobs:
             bufs[k] = (_empty((r, c), torch.bfloat16, dev), _empty((c, r), torch.bfloat16, dev))
@@ -221,11 +221,9 @@ def _prep_weights(model, dt) -> Optional[dict]:
                         tiles.append((ei, r0, c0, 0))
                 ei += 1
         st = dict(dev=dev, shapes=tuple((k, r, c) for k, _, r, c in jobs), bufs=bufs, sig=None,
-                  tiles=torch.tensor(tiles, dtype=torch.int32, device=dev), ntiles=len(tiles), entries=None,
-                  pack=struct)
+                  tiles=torch.tensor(tiles, dtype=torch.int32, device=dev), ntiles=len(tiles), entries=None)
         model.__dict__["_sdp_wprep"] = st
     if st["sig"] != sig:  # parameter storage moved (or first call): rebuild the entry table
-        struct = st["pack"]
         eb = sp.lib().sdp_mt_cast_transpose_entry_bytes()
         raw = bytearray()
         for k, ps, r, c in jobs:
@@ -1392,7 +1390,6 @@ class AdamW(torch.optim.Optimizer):
         return sig
 
     def _build(self, dev):
-        import struct
         bb = sp.lib().sdp_mt_block_bytes()
         self._tables = []
         groups = [[p for p in group["params"] if p.grad is not None] for group in self.param_groups]
