@@ -1467,12 +1467,25 @@ extern "C" int sdp_softmax_bwd(int dtype, const void* P, int64_t ldp, const void
 // planes of one image staged in LDS as fp32 [pixel][64].  Reduce the chunk slabs with
 // sdp_seg_colsum.
 // ---------------------------------------------------------------------------
-// Thread (channel cl, tap row ty): for every output row h (in 16-column segments) it loads the
-// 16-wide DY row and the (16 + KS - 1)-wide zero-padded A row hh = h + ty - KS/2 into registers
-// once and does the KS x 16 FMAs of that row pair from registers.  Both planes are staged in
+// Thread (channel pair cp = lane % 32, tap row ty = wave, output rows h = lane / 32 mod 2): for each
+// of its rows (in 16-column segments) it loads the 16-wide DY row and the (16 + KS - 1)-wide
+// zero-padded A row hh = h + ty - KS/2 of both channels into registers once (one 32-bit LDS read
+// per pixel for bf16) and does the KS x 16 two-channel FMAs (v_pk_fma_f32) of that row pair from
+// registers; the two half-waves' row sums are added at the end (lane ^ 32).  Both planes are staged in
 // the input dtype (bf16: 2 x HW x 128 B = 64 KiB at 16 x 16, so two workgroups share a CU and one
 // stages while the other computes), with all of a thread's staging loads of an image issued
 // before its LDS stores.
+// Two adjacent channels of one staged pixel as fp32 (bf16: one 32-bit LDS read).
+template <typename T>
+__device__ __forceinline__ f32x2 ld_pair(const T* p) {
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t v = *(const uint32_t*)p;
+    return f32x2{__uint_as_float(v << 16), __uint_as_float(v & 0xFFFF0000u)};
+  } else {
+    return *(const f32x2*)p;
+  }
+}
+
 template <typename T, int KS>
 __global__ __launch_bounds__(64 * KS) void dw_wgrad_k(const T* __restrict__ A, int64_t lda, RowMap am,
                                                       const T* __restrict__ DY, int64_t lddy, RowMap dym, int B, int H,
@@ -1483,10 +1496,10 @@ __global__ __launch_bounds__(64 * KS) void dw_wgrad_k(const T* __restrict__ A, i
   T* ap = (T*)dw_sm;   // [HW][64]
   T* dp = ap + HW * 64;  // [HW][64]
   const int c0 = blockIdx.x * 64, chunk = blockIdx.y;
-  const int cl = threadIdx.x & 63, ty = threadIdx.x / 64;
-  float acc[KS];
+  const int cp = threadIdx.x & 31, hpar = (threadIdx.x >> 5) & 1, ty = threadIdx.x / 64;
+  f32x2 acc[KS];
 #pragma unroll
-  for (int i = 0; i < KS; ++i) acc[i] = 0.f;
+  for (int i = 0; i < KS; ++i) acc[i] = f32x2{0.f, 0.f};
   const int b0 = chunk * ipb, b1 = min(B, b0 + ipb);
   const bool v8 = (sizeof(T) == 2) && (c0 + 64 <= C) && (lda % 8 == 0) && (lddy % 8 == 0) &&
                   (((uintptr_t)A & 15) == 0) && (((uintptr_t)DY & 15) == 0);
@@ -1521,28 +1534,39 @@ __global__ __launch_bounds__(64 * KS) void dw_wgrad_k(const T* __restrict__ A, i
       }
     }
     __syncthreads();
-    for (int h = 0; h < H; ++h) {
+    for (int h = hpar; h < H; h += 2) {
       const int hh = h + ty - P;
       if (hh < 0 || hh >= H) continue;
       for (int w0 = 0; w0 < W; w0 += MW) {
-        float ar[MW + KS - 1], dr[MW];
+        f32x2 ar[MW + KS - 1], dr[MW];
 #pragma unroll
         for (int q = 0; q < MW + KS - 1; ++q) {
           const int ww = w0 + q - P;
-          ar[q] = (ww >= 0 && ww < W) ? to_f<T>(ap[(hh * W + ww) * 64 + cl]) : 0.f;
+          ar[q] = (ww >= 0 && ww < W) ? ld_pair<T>(ap + (hh * W + ww) * 64 + 2 * cp) : f32x2{0.f, 0.f};
         }
 #pragma unroll
-        for (int q = 0; q < MW; ++q) dr[q] = w0 + q < W ? to_f<T>(dp[(h * W + w0 + q) * 64 + cl]) : 0.f;
+        for (int q = 0; q < MW; ++q)
+          dr[q] = w0 + q < W ? ld_pair<T>(dp + (h * W + w0 + q) * 64 + 2 * cp) : f32x2{0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < MW; ++q)
 #pragma unroll
-          for (int tx = 0; tx < KS; ++tx) acc[tx] = fmaf(dr[q], ar[q + tx], acc[tx]);
+          for (int tx = 0; tx < KS; ++tx) acc[tx] = __builtin_elementwise_fma(dr[q], ar[q + tx], acc[tx]);
       }
     }
   }
-  if (c0 + cl >= C) return;
 #pragma unroll
-  for (int tx = 0; tx < KS; ++tx) part[((int64_t)chunk * C + c0 + cl) * (KS * KS) + ty * KS + tx] = acc[tx];
+  for (int tx = 0; tx < KS; ++tx) {
+    acc[tx].x += __shfl_xor(acc[tx].x, 32);
+    acc[tx].y += __shfl_xor(acc[tx].y, 32);
+  }
+  const int c = c0 + 2 * cp;
+  if (hpar || c >= C) return;
+  float* o = part + ((int64_t)chunk * C + c) * (KS * KS) + ty * KS;
+#pragma unroll
+  for (int tx = 0; tx < KS; ++tx) o[tx] = acc[tx].x;
+  if (c + 1 >= C) return;
+#pragma unroll
+  for (int tx = 0; tx < KS; ++tx) o[KS * KS + tx] = acc[tx].y;
 }
 
 extern "C" int sdp_dw_wgrad_chunks(int B) { return B < 64 ? (B > 0 ? B : 1) : 64; }
