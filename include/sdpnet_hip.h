@@ -394,7 +394,7 @@ int sdp_softmax_bwd(int dtype, const void* P, int64_t ldp, const void* DPd, int6
 
 /* Depthwise-conv weight gradient (layers.py:73-78): part[chunk][c][t] = sum over the chunk's
  * images of DY[b, h, w, c] * A[b, h + ty - k/2, w + tx - k/2, c] (zero padded), NHWC rows,
- * chunk < sdp_dw_wgrad_chunks(B); H * W <= 640 (bf16) / 320 (fp32), any W, odd k <= 9.  The input gradient is
+ * chunk < sdp_dw_wgrad_chunks(B); H * W <= 640 (both planes staged as fp32), any W, odd k <= 9.  The input gradient is
  * sdp_dwconv with the kernel flipped. */
 int sdp_dw_wgrad_chunks(int B);
 int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, int64_t a_gstride, int a_off, const void* DY,

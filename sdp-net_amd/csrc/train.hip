@@ -1463,78 +1463,70 @@ extern "C" int sdp_softmax_bwd(int dtype, const void* P, int64_t ldp, const void
 // ---------------------------------------------------------------------------
 // Depthwise-conv weight gradient (layers.py:73-78 backward):
 //   part[chunk][c][t] = sum over the chunk's images and pixels of DY[b,h,w,c] * A[b,h+ty-P,w+tx-P,c]
-// (zero padding), NHWC rows through row maps.  Block: 64 channels x (image chunk); both
-// planes of one image staged in LDS as fp32 [pixel][64].  Reduce the chunk slabs with
-// sdp_seg_colsum.
+// (zero padding), NHWC rows through row maps.  Block: 32 channels x (image chunk); both planes of
+// one image staged in LDS as fp32 [pixel][32] (converted once at staging: every staged value is
+// read by KS threads).  Reduce the chunk slabs with sdp_seg_colsum.
 // ---------------------------------------------------------------------------
-// Thread (channel pair cp = lane % 32, tap row ty = wave, output rows h = lane / 32 mod 2): for each
-// of its rows (in 16-column segments) it loads the 16-wide DY row and the (16 + KS - 1)-wide
-// zero-padded A row hh = h + ty - KS/2 of both channels into registers once (one 32-bit LDS read
-// per pixel for bf16) and does the KS x 16 two-channel FMAs (v_pk_fma_f32) of that row pair from
-// registers; the two half-waves' row sums are added at the end (lane ^ 32).  Both planes are staged in
-// the input dtype (bf16: 2 x HW x 128 B = 64 KiB at 16 x 16, so two workgroups share a CU and one
-// stages while the other computes), with all of a thread's staging loads of an image issued
-// before its LDS stores.
-// Two adjacent channels of one staged pixel as fp32 (bf16: one 32-bit LDS read).
-template <typename T>
-__device__ __forceinline__ f32x2 ld_pair(const T* p) {
-  if constexpr (sizeof(T) == 2) {
-    const uint32_t v = *(const uint32_t*)p;
-    return f32x2{__uint_as_float(v << 16), __uint_as_float(v & 0xFFFF0000u)};
-  } else {
-    return *(const f32x2*)p;
-  }
-}
-
+// Thread (channel pair cp = lane % 16, tap row ty = wave, output rows h = lane / 16 mod 4): for
+// each of its rows (in 16-column segments) it loads the 16-wide DY row and the (16 + KS - 1)-wide
+// zero-padded A row hh = h + ty - KS/2 of both channels into registers once (one 64-bit LDS read
+// per pixel) and does the KS x 16 two-channel FMAs (v_pk_fma_f32) of that row pair from
+// registers; the four row groups' sums are added at the end (lane ^ 16, lane ^ 32).  The planes
+// take 2 x HW x 128 B = 64 KiB at 16 x 16, so two workgroups share a CU and one stages while the
+// other computes; all of a thread's staging loads of an image are issued before its LDS stores.
 template <typename T, int KS>
 __global__ __launch_bounds__(64 * KS) void dw_wgrad_k(const T* __restrict__ A, int64_t lda, RowMap am,
                                                       const T* __restrict__ DY, int64_t lddy, RowMap dym, int B, int H,
                                                       int W, int C, int ipb, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) char dw_sm[];
-  constexpr int P = KS / 2, MW = 16, NT = 64 * KS, U = 4;
+  constexpr int P = KS / 2, MW = 16, NT = 64 * KS, U = 4, CB = 32, NCP = CB / 2, NRG = 64 / NCP, CH = CB / 8;
   const int HW = H * W;
-  T* ap = (T*)dw_sm;   // [HW][64]
-  T* dp = ap + HW * 64;  // [HW][64]
-  const int c0 = blockIdx.x * 64, chunk = blockIdx.y;
-  const int cp = threadIdx.x & 31, hpar = (threadIdx.x >> 5) & 1, ty = threadIdx.x / 64;
+  float* ap = (float*)dw_sm;  // [HW][32]
+  float* dp = ap + HW * CB;   // [HW][32]
+  const int c0 = blockIdx.x * CB, chunk = blockIdx.y;
+  const int cp = threadIdx.x % NCP, rg = (threadIdx.x & 63) / NCP, ty = threadIdx.x / 64;
   f32x2 acc[KS];
 #pragma unroll
   for (int i = 0; i < KS; ++i) acc[i] = f32x2{0.f, 0.f};
   const int b0 = chunk * ipb, b1 = min(B, b0 + ipb);
-  const bool v8 = (sizeof(T) == 2) && (c0 + 64 <= C) && (lda % 8 == 0) && (lddy % 8 == 0) &&
+  const bool v8 = (sizeof(T) == 2) && (c0 + CB <= C) && (lda % 8 == 0) && (lddy % 8 == 0) &&
                   (((uintptr_t)A & 15) == 0) && (((uintptr_t)DY & 15) == 0);
   for (int b = b0; b < b1; ++b) {
     __syncthreads();
-    if (v8) {  // 16-B loads: 8 chunks of 8 channels per pixel, U chunk pairs in flight per thread
-      const int n = HW * 8;
+    if (v8) {  // 16-B loads: CH chunks of 8 channels per pixel, U chunk pairs in flight per thread
+      const int n = HW * CH;
       for (int e0 = threadIdx.x; e0 < n; e0 += NT * U) {
         bf16x8 va[U], vd[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int e = min(e0 + u * NT, n - 1);
-          const int64_t m = (int64_t)b * HW + (e >> 3);
-          va[u] = *(const bf16x8*)(A + am(m) * lda + c0 + (e & 7) * 8);
-          vd[u] = *(const bf16x8*)(DY + dym(m) * lddy + c0 + (e & 7) * 8);
+          const int64_t m = (int64_t)b * HW + e / CH;
+          va[u] = *(const bf16x8*)(A + am(m) * lda + c0 + (e % CH) * 8);
+          vd[u] = *(const bf16x8*)(DY + dym(m) * lddy + c0 + (e % CH) * 8);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int e = e0 + u * NT;
           if (e < n) {
-            *(bf16x8*)(ap + (e >> 3) * 64 + (e & 7) * 8) = va[u];
-            *(bf16x8*)(dp + (e >> 3) * 64 + (e & 7) * 8) = vd[u];
+            f32x4* pa = (f32x4*)(ap + (e / CH) * CB + (e % CH) * 8);
+            f32x4* pd = (f32x4*)(dp + (e / CH) * CB + (e % CH) * 8);
+            pa[0] = f32x4{bf2f((bf16_t)va[u][0]), bf2f((bf16_t)va[u][1]), bf2f((bf16_t)va[u][2]), bf2f((bf16_t)va[u][3])};
+            pa[1] = f32x4{bf2f((bf16_t)va[u][4]), bf2f((bf16_t)va[u][5]), bf2f((bf16_t)va[u][6]), bf2f((bf16_t)va[u][7])};
+            pd[0] = f32x4{bf2f((bf16_t)vd[u][0]), bf2f((bf16_t)vd[u][1]), bf2f((bf16_t)vd[u][2]), bf2f((bf16_t)vd[u][3])};
+            pd[1] = f32x4{bf2f((bf16_t)vd[u][4]), bf2f((bf16_t)vd[u][5]), bf2f((bf16_t)vd[u][6]), bf2f((bf16_t)vd[u][7])};
           }
         }
       }
     } else {
-      for (int e = threadIdx.x; e < HW * 64; e += NT) {
-        const int px = e >> 6, c = c0 + (e & 63);
+      for (int e = threadIdx.x; e < HW * CB; e += NT) {
+        const int px = e / CB, c = c0 + (e % CB);
         const int64_t m = (int64_t)b * HW + px;
-        ap[e] = c < C ? A[am(m) * lda + c] : from_f<T>(0.f);
-        dp[e] = c < C ? DY[dym(m) * lddy + c] : from_f<T>(0.f);
+        ap[e] = c < C ? to_f<T>(A[am(m) * lda + c]) : 0.f;
+        dp[e] = c < C ? to_f<T>(DY[dym(m) * lddy + c]) : 0.f;
       }
     }
     __syncthreads();
-    for (int h = hpar; h < H; h += 2) {
+    for (int h = rg; h < H; h += NRG) {
       const int hh = h + ty - P;
       if (hh < 0 || hh >= H) continue;
       for (int w0 = 0; w0 < W; w0 += MW) {
@@ -1542,11 +1534,11 @@ __global__ __launch_bounds__(64 * KS) void dw_wgrad_k(const T* __restrict__ A, i
 #pragma unroll
         for (int q = 0; q < MW + KS - 1; ++q) {
           const int ww = w0 + q - P;
-          ar[q] = (ww >= 0 && ww < W) ? ld_pair<T>(ap + (hh * W + ww) * 64 + 2 * cp) : f32x2{0.f, 0.f};
+          ar[q] = (ww >= 0 && ww < W) ? *(const f32x2*)(ap + (hh * W + ww) * CB + 2 * cp) : f32x2{0.f, 0.f};
         }
 #pragma unroll
         for (int q = 0; q < MW; ++q)
-          dr[q] = w0 + q < W ? ld_pair<T>(dp + (h * W + w0 + q) * 64 + 2 * cp) : f32x2{0.f, 0.f};
+          dr[q] = w0 + q < W ? *(const f32x2*)(dp + (h * W + w0 + q) * CB + 2 * cp) : f32x2{0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < MW; ++q)
 #pragma unroll
@@ -1556,11 +1548,14 @@ __global__ __launch_bounds__(64 * KS) void dw_wgrad_k(const T* __restrict__ A, i
   }
 #pragma unroll
   for (int tx = 0; tx < KS; ++tx) {
-    acc[tx].x += __shfl_xor(acc[tx].x, 32);
-    acc[tx].y += __shfl_xor(acc[tx].y, 32);
+#pragma unroll
+    for (int sh = NCP; sh < 64; sh *= 2) {
+      acc[tx].x += __shfl_xor(acc[tx].x, sh);
+      acc[tx].y += __shfl_xor(acc[tx].y, sh);
+    }
   }
   const int c = c0 + 2 * cp;
-  if (hpar || c >= C) return;
+  if (rg || c >= C) return;
   float* o = part + ((int64_t)chunk * C + c) * (KS * KS) + ty * KS;
 #pragma unroll
   for (int tx = 0; tx < KS; ++tx) o[tx] = acc[tx].x;
@@ -1577,12 +1572,12 @@ extern "C" int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, in
   if (!A || !DY || !part || B < 0 || H <= 0 || W <= 0 || C <= 0 || (k != 3 && k != 5 && k != 7 && k != 9))
     return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
-  const size_t lds = (size_t)H * W * 64 * 2 * (dtype == 1 ? 2 : 4);
+  const size_t lds = (size_t)H * W * 32 * 2 * 4;  // both planes, fp32 [HW][32]
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   if ((a_grp > 0 && a_grp % (H * W)) || (dy_grp > 0 && dy_grp % (H * W))) return (int)hipErrorInvalidValue;
   const RowMap am = mk_tmap(a_grp, a_gstride, a_off), dym = mk_tmap(dy_grp, dy_gstride, dy_off);
   const int nch = sdp_dw_wgrad_chunks(B), ipb = (B + nch - 1) / nch;
-  dim3 grid((C + 63) / 64, nch);
+  dim3 grid((C + 31) / 32, nch);
   hipStream_t s = (hipStream_t)stream;
 #define SDP_DWG(TT, KK)                                                                                              \
   do {                                                                                                               \

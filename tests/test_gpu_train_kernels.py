@@ -202,7 +202,7 @@ def test_softmax_dropout_mask_consistent():
 
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
 @pytest.mark.parametrize("B,H,W,C,k", [(3, 14, 14, 128, 7), (2, 16, 16, 64, 3), (2, 7, 9, 96, 5), (3, 12, 24, 72, 7),
-                                     (130, 16, 16, 96, 7)])
+                                     (130, 16, 16, 96, 7), (2, 20, 24, 40, 7)])
 def test_dw_wgrad(dtype, B, H, W, C, k):
     a = rnd(B * H * W, C, seed=22, dtype=dtype)
     dy = rnd(B * H * W, C, seed=23, dtype=dtype)
