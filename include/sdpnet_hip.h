@@ -95,6 +95,24 @@ int sdp_gemm_set_fast_kernel(int k);
  * stores, 0 = default.  Returns the previous value. */
 int sdp_gemm_set_store_policy(int nt);
 
+/* Epilogue specialisation of the whole-line fast-GEMM epilogue: 1 (default) = the model's
+ * flag combinations (LN fold + bias; residual + LN partials [+ bias]) with no / GELU
+ * activation run an instantiation with the flags fixed at compile time (packed residual add,
+ * dot2 partial sums); 0 = the run-time-flag epilogue for every call.  Outputs are
+ * bit-identical; the emitted LN partials agree to fp32 rounding.  Returns the previous value. */
+int sdp_gemm_set_epi_spec(int on);
+
+/* Launch timeline of the bf16 fast GEMM (measurement only; bench.py's roofline inside a replayed
+ * HIP graph, where events cannot be recorded).  sdp_gemm_set_timeline(buf, slots): while buf
+ * (device memory, 2 x u64 per slot, caller-initialised to {UINT64_MAX, 0}) is set, fast-GEMM
+ * launch i (host launch order) atomically folds its first workgroup's start and its last
+ * workgroup's end (after that workgroup's stores drained) into slot i, in s_memrealtime ticks
+ * (100 MHz); launches beyond `slots` are not timed.  buf = NULL stops; returns the number of
+ * slots the previous timeline took.  sdp_gemm_timeline_count() = slots taken so far.  Replaces
+ * nothing in the reference. */
+int sdp_gemm_set_timeline(void* buf, int slots);
+int sdp_gemm_timeline_count(void);
+
 /* Tile raster of the 8-phase GEMM: M-blocks per group (consecutive blocks walk a group of
  * gm M-blocks before the next N-tile).  1 = row-major, -1 = auto (8 when N spans >= 12
  * tiles, else 1).  Results do not depend on it.  Returns the previous value. */
@@ -401,16 +419,20 @@ int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, int64_t a_gst
                  int64_t lddy, int dy_grp, int64_t dy_gstride, int dy_off, int B, int H, int W, int C, int k,
                  float* part, void* stream);
 
-/* Label-smoothed cross entropy, mean over B (nn.CrossEntropyLoss(label_smoothing),
- * training_tools.py:76, :88): *loss += mean loss (fp32, atomic);
- * dlogits = grad_scale / B * (softmax - ((1 - eps) onehot + eps / K)) (may be NULL). */
+/* Label-smoothed cross entropy, mean over the rows whose label is not ignore_index
+ * (nn.CrossEntropyLoss(label_smoothing), training_tools.py:76, :88, with torch's default
+ * ignore_index = -100): *loss += mean loss (fp32, atomic); dlogits = grad_scale / n * (softmax -
+ * ((1 - eps) onehot + eps / K)) for the n counted rows, 0 for ignored rows (may be NULL); all rows
+ * ignored gives a NaN loss (torch: 0 / 0).  sdp_ce_loss_ignore takes any ignore_index. */
 int sdp_ce_loss(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K, float eps,
                 float grad_scale, void* dlogits, int64_t ldd, float* loss, void* stream);
+int sdp_ce_loss_ignore(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K, float eps,
+                       float grad_scale, int64_t ignore_index, void* dlogits, int64_t ldd, float* loss, void* stream);
 /* The same loss on probability targets (fp32 rows [B][ldt], the CutMix / MixUp targets of
  * dataset_generator.py:105-110 fed to nn.CrossEntropyLoss): t' = (1 - eps) t + eps / K,
  * loss = mean_i -sum_k t'_ik log p_ik, dlogits = grad_scale / B * (p sum_k t' - t').  A hard
- * label outside [0, K) (ignore_index is not implemented) makes its row's loss and gradient NaN
- * instead of reading out of bounds. */
+ * label outside [0, K) other than ignore_index makes its row's loss and gradient NaN instead of
+ * reading out of bounds. */
 int sdp_ce_loss_soft(int dtype, const void* logits, int64_t ldl, const float* targets, int64_t ldt, int B, int K,
                      float eps, float grad_scale, void* dlogits, int64_t ldd, float* loss, void* stream);
 

@@ -495,8 +495,14 @@ extern "C" int sdp_attn_train_bwd(int dtype, const void* qkv, int64_t ldq, const
                                   const void* dO, int64_t lddo, const float* lse, float* delta, void* dq,
                                   int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv, int B, int N, int H,
                                   int hd, float scale, float p, uint64_t seed, void* stream) {
+  // the same leading-dimension checks as the forward, plus the row widths of dq / dk / dv and the
+  // base alignments the kernels' vector accesses need (bf16x8 loads of qkv / o / dO, 8-B stores)
+  const int64_t hw = (int64_t)H * hd;
+  auto al = [](const void* q, uintptr_t a) { return ((uintptr_t)q % a) == 0; };
   if (!sdp_attn_train_applies(dtype, N, hd) || !qkv || !o || !dO || !lse || !delta || !dq || !dk || !dv || B < 0 ||
-      H <= 0 || p < 0.f || p >= 1.f || ldq % 8 || ldo % 8 || lddo % 8 || lddq % 4 || lddk % 4 || lddv % 4)
+      H <= 0 || p < 0.f || p >= 1.f || ldq % 8 || ldo % 8 || lddo % 8 || lddq % 4 || lddk % 4 || lddv % 4 ||
+      ldq < 3 * hw || ldo < hw || lddo < hw || lddq < hw || lddk < hw || lddv < hw || !al(qkv, 16) || !al(o, 16) ||
+      !al(dO, 16) || !al(dq, 8) || !al(dk, 8) || !al(dv, 8))
     return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
   uint32_t thresh;

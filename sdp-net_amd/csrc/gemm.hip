@@ -56,6 +56,11 @@ struct Epi {
   // sdp_act_fwd / sdp_act_bwd (mask index m * N + n):
   //   EPI 5: out = z (pre-activation), out2[m * ld2 + n] = dropout(act2(z))
   //   EPI 6: out = dropout(acc) * act2'(resid)       (resid = the stored pre-activation z)
+  // launch timeline (bench.py's roofline inside graph replay): {min start, max end} in
+  // s_memrealtime ticks (100 MHz), or null
+  unsigned long long* tline = nullptr;
+  // byte extents of out / resid / part (tile_epilogue_fl's buffer descriptors; < 2 GiB)
+  uint32_t out_bytes = 0, res_bytes = 0, part_bytes = 0;
   T* out2 = nullptr;
   int64_t ld2 = 0;
   int act2 = 0;
@@ -521,6 +526,203 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
   }
 }
 
+// Whole-line epilogue of the model's GEMMs with the epilogue flags fixed at compile time
+// (FL: EF_BIAS | EF_LN | EF_RESID | EF_PART; same staging and drain order as
+// tile_epilogue_rows<ACT, 4, true>).  Differences, all in instruction count: no run-time flag
+// branches; output / residual / partial accesses are buffer instructions with 32-bit byte
+// offsets walked incrementally per row (the host guarantees every operand's extent < 2 GiB,
+// Epi::*_bytes) and rows past M or columns past N get an offset beyond the descriptor's range,
+// so the hardware drops those stores instead of a branch per row; the residual add works on
+// packed bf16 pairs; the row partials come from v_dot2c_f32_bf16 sums of the stored bf16
+// values (sum and sum of squares, one pass: M2 = sumsq - sum * mean, clamped at 0) reduced
+// over the row's 8 lanes with DPP adds.  Stored outputs are bit-identical to
+// tile_epilogue_rows; the partials agree to fp32 rounding.
+enum { EF_BIAS = 1, EF_LN = 2, EF_RESID = 4, EF_PART = 8 };
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2n;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+typedef __attribute__((ext_vector_type(2))) int i32x2v;
+typedef __attribute__((ext_vector_type(4))) int i32x4v;
+constexpr uint32_t OFF_DROP = 0x80000000u;  // >= every descriptor range used below
+
+SDP_DEV float dpp_sum8(float v) {  // sum over the 8-lane group (lane & ~7), result in every lane
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  return v;
+}
+
+SDP_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, bf16x2n{(__bf16)lo, (__bf16)hi});
+}
+
+// o := bf16(o + r) elementwise (8 bf16), in packed fp32 pairs
+SDP_DEV u32x4 add_bf16x8(u32x4 ou, u32x4 ru) {
+  u32x4 res;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 a = {__uint_as_float(ou[i] << 16), __uint_as_float(ou[i] & 0xffff0000u)};
+    const f32x2 b = {__uint_as_float(ru[i] << 16), __uint_as_float(ru[i] & 0xffff0000u)};
+    const f32x2 sm = a + b;
+    res[i] = pack_bf16x2(sm.x, sm.y);
+  }
+  return res;
+}
+
+// byte offset of a lane's rows m, m + 8, m + 16, ... through a RowMap (see RowWalk), 32-bit
+struct RowOff {
+  uint32_t off, step, wrap;
+  int r, grp;
+  SDP_DEV RowOff(const RowMap& rm, int m, uint32_t ldb) : grp(rm.grp) {
+    const int g = (int)((unsigned)m / (unsigned)rm.grp);
+    r = m - g * rm.grp;
+    off = (uint32_t)(((int64_t)g * rm.gstride + rm.off + r) * (int64_t)ldb);
+    step = 8u * ldb;
+    wrap = (uint32_t)((rm.gstride - (int64_t)rm.grp) * (int64_t)ldb);
+  }
+  SDP_DEV void step8() {  // the host guarantees grp >= 8 (at most one carry per step): branch-free
+    r += 8;
+    off += step;
+    const bool c = r >= grp;
+    r = c ? r - grp : r;
+    off = c ? off + wrap : off;
+  }
+};
+
+template <int ACT, int FL>
+SDP_DEV void tile_epilogue_fl(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0, int n0, int M, int N, int wm,
+                              int wn, int lane, int fr, int fq, char* stg) {
+  constexpr bool HB = FL & EF_BIAS, HL = FL & EF_LN, HR = FL & EF_RESID, HP = FL & EF_PART;
+  const int cbase = n0 + wn * 64 + pair_col0(fq);
+  f32x4 bv[2][2], sv[2][2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c0 = min(cbase + 32 * p, N - 8);
+    if constexpr (HB || HL) {
+      if (epi.bias) {
+        bv[p][0] = *(const f32x4*)(epi.bias + c0);
+        bv[p][1] = *(const f32x4*)(epi.bias + c0 + 4);
+      } else {
+        bv[p][0] = bv[p][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    if constexpr (HL) {
+      sv[p][0] = *(const f32x4*)(epi.lnsum + c0);
+      sv[p][1] = *(const f32x4*)(epi.lnsum + c0 + 4);
+    }
+  }
+  const int rlo = lane >> 3, ch = lane & 7;
+  const int col = n0 + wn * 64 + ch * 8;
+  const bool col_ok = col < N;
+  const int wchunk0 = ((fq & 1) << 1) | (fq >> 1);
+  const int mb = m0 + wm * 128 + rlo;
+  auto stage = [&](int j) {
+    char* sl = stg + j * 2048;
+    f32x2 lr2 = {1.f, 1.f}, lm2 = {0.f, 0.f};
+    if constexpr (HL) {
+      const int mrow = min(m0 + wm * 128 + j * 16 + fr, M - 1);
+      const float2 st = *(const float2*)(epi.lnst + 2 * (int64_t)mrow);
+      lr2 = f32x2{st.y, st.y};
+      lm2 = f32x2{-st.y * st.x, -st.y * st.x};
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                   __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[4 + r] = __uint_as_float(sw[1]);
+      }
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        f32x2 x2 = {v[e], v[e + 1]};
+        if constexpr (HL) {
+          const f32x2 b2 = {bv[p][e >> 2][e & 3], bv[p][e >> 2][(e & 3) + 1]};
+          const f32x2 s2 = {sv[p][e >> 2][e & 3], sv[p][e >> 2][(e & 3) + 1]};
+          x2 = x2 * lr2 + (s2 * lm2 + b2);
+        } else if constexpr (HB) {
+          x2 = x2 + f32x2{bv[p][e >> 2][e & 3], bv[p][e >> 2][(e & 3) + 1]};
+        }
+        if constexpr (ACT == ACT_GELU) {
+          x2 = gelu_fast2(x2);
+        } else if constexpr (ACT != ACT_NONE) {
+          x2.x = epi_act<ACT>(epi.act, x2.x);
+          x2.y = epi_act<ACT>(epi.act, x2.y);
+        }
+        o[e >> 1] = pack_bf16x2(x2.x, x2.y);
+      }
+      *(u32x4*)(sl + fr * 128 + (((4 * p + wchunk0) ^ (fr & 7)) << 4)) = o;
+    }
+  };
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(epi.out, 0, (int)epi.out_bytes, 0x00020000);
+  RowOff ow(epi.cmap, mb, (uint32_t)epi.ldc * 2u);
+  const uint32_t colb = (uint32_t)col * 2u;
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t prs;
+  [[maybe_unused]] uint32_t pcolb = 0;
+  RowOff pw(epi.cmap, mb, (uint32_t)(N >> 6) * 8u);  // bytes per physical row of partials
+  if constexpr (HP) {
+    prs = __builtin_amdgcn_make_buffer_rsrc(epi.part, 0, (int)epi.part_bytes, 0x00020000);
+    pcolb = (uint32_t)((n0 + wn * 64) >> 6) * 8u;
+  }
+  auto drain = [&](int j, const u32x4(&rr)[2]) {
+    const char* sl = stg + j * 2048;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = rlo + 8 * q;
+      u32x4 o = *(const u32x4*)(sl + r * 128 + ((ch ^ (r & 7)) << 4));
+      const int m = mb + j * 16 + 8 * q;
+      if constexpr (HR) o = add_bf16x8(o, rr[q]);
+      const bool ok = m < M && col_ok;
+      const uint32_t rowoff = ow.off;
+      ow.step8();
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4v, o), ors, ok ? rowoff + colb : OFF_DROP, 0, 0);
+      if constexpr (HP) {
+        const bf16x2n one = {(__bf16)1.0f, (__bf16)1.0f};
+        float sm = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          // opaque copy: hipcc (ROCm 7.2) miscompiles bit_cast<bf16x2>(u32 vector element) feeding
+          // v_dot2c_f32_bf16 (every i reads element 0); a register the compiler cannot see through
+          // keeps the element
+          uint32_t u = o[i];
+          asm volatile("" : "+v"(u));
+          const bf16x2n x = __builtin_bit_cast(bf16x2n, u);
+          sm = __builtin_amdgcn_fdot2_f32_bf16(x, one, sm, false);
+          s2 = __builtin_amdgcn_fdot2_f32_bf16(x, x, s2, false);
+        }
+        sm = dpp_sum8(sm);
+        s2 = dpp_sum8(s2);
+        const float mean = sm * (1.0f / 64.0f);
+        const float m2 = fmaxf(fmaf(-sm, mean, s2), 0.0f);
+        // the partials are addressed by the output's physical row (walk pw, nch * 8 B per row)
+        const uint32_t poff = pw.off;
+        pw.step8();
+        if (ch == 0)
+          __builtin_amdgcn_raw_buffer_store_b64(i32x2v{__float_as_int(mean), __float_as_int(m2)}, prs,
+                                                ok ? poff + pcolb : OFF_DROP, 0, 0);
+      }
+    }
+  };
+  u32x4 rres[8][2];
+  if constexpr (HR) {
+    const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc((void*)epi.resid, 0, (int)epi.res_bytes, 0x00020000);
+    RowOff rw(epi.rmap, mb, (uint32_t)epi.ldr * 2u);
+    static_for<0, 8>([&](auto j) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int m = mb + j * 16 + 8 * q;
+        const uint32_t ro = rw.off;
+        rw.step8();
+        rres[j][q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, (m < M && col_ok) ? ro + colb : OFF_DROP, 0, 0));
+      }
+    });
+  }
+  static_for<0, 8>([&](auto j) { stage(j); });
+  static_for<0, 8>([&](auto j) { drain(j, rres[j]); });
+}
+
 // EPI: 0 = 8-B stores, 1 = permlane-paired 16-B stores, 2 = no stores (timing probe only)
 // ---------------------------------------------------------------------------
 // 8-phase ping-pong kernel: 256x256x64 tiles, 8 waves (2 along M x 4 along N,
@@ -567,8 +769,10 @@ constexpr int BUF8 = 2 * TILE_BYTES;
 // instead of arriving together once per tile round, and the last partial round of
 // the data-parallel grid disappears.
 // Flags return to 0 at the end of every launch (the consumer clears the word it
-// consumed), which keeps graph replays valid; a wait gives up after ~2^22 polls and
-// records it in *status (never expected; checked by the tests).
+// consumed), which keeps graph replays valid.  A wait gives up after ~2^22 polls (the
+// producer range is not resident, e.g. the chip is shared with another stream's kernels):
+// the consumer marks the flag abandoned (2), counts it in *status and recomputes the tile
+// from k = 0 -- same accumulation order, same bits; the producer, finding 2, resets it to 0.
 // ---------------------------------------------------------------------------
 struct SkArgs {
   float* part;        // G slots x 64 Ki floats (one 256x256 fp32 tile each)
@@ -605,6 +809,7 @@ typedef __attribute__((ext_vector_type(4))) int i32x4;
 // Diagnostic build only (tools/gemm_stamps.py, a separate library): wall-clock stamps of
 // workgroup events, 64 per workgroup; stamp = event code << 56 | s_memrealtime (100 MHz).
 __device__ unsigned long long g_gemm_stamps[8192 * 64];
+__device__ int g_gemm_dephase;  // experiment: first-round workgroup b waits ((b >> 3) & 3) * this many 10-ns ticks
 #define SDP_STAMP(code)                                                                            \
   do {                                                                                             \
     if (tid == 0 && nstamp < 64)                                                                   \
@@ -620,7 +825,8 @@ template <int ACT, int EPI, bool SK>
 __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
                                                          const bf16_t* __restrict__ W, int64_t ldw, Epi<bf16_t> epi,
                                                          int M, int N, int K, int tiles_m, int tiles_n, SkArgs sk) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF8];
+  // 2 K-tile buffers (+16 B: the stream-K tail's resume decision, broadcast to every wave)
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF8 + 16];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -630,6 +836,14 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   int nstamp = 0;
 #endif
   SDP_STAMP(0);
+  if (epi.tline && tid == 0) atomicMin(epi.tline, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#ifdef SDP_GEMM_STAMPS
+  if (g_gemm_dephase > 0 && b < 256) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long w = (unsigned long long)(((b >> 3) & 3) * g_gemm_dephase);
+    while (__builtin_amdgcn_s_memrealtime() - t0 < w) __builtin_amdgcn_s_sleep(8);
+  }
+#endif
 
   // ---- segment plan: (tile, first k-tile, k-tiles, mode) per segment
   enum { SEG_FULL = 0, SEG_HEAD = 1, SEG_TAIL = 2 };
@@ -693,6 +907,42 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   tile_coords(tile, tiles_m, tiles_n, epi.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
+  // stream-K tail: continue the head's accumulation (range p-1 computed it first, so this rarely
+  // waits).  A wait that gives up (producer not resident: the grid shares the chip with other
+  // streams' kernels) marks the flag abandoned (0 -> 2) and recomputes the head's k-range itself:
+  // the same k = 0..nk-1 order into one accumulator, so the output stays bit-identical.
+  bool resume = false;
+  const int prev = p - 8;  // range j - 1 of the same XCD
+  if (SK && mode == SEG_TAIL) {
+    SDP_STAMP(2);
+    if (wave == 0) {
+      unsigned spins = 0;
+      unsigned f = 0;
+      while ((f = __hip_atomic_load(sk.flags + prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 22)) break;
+      }
+      if (f == 0u && lane == 0) {
+        unsigned expect = 0u;
+        if (__hip_atomic_compare_exchange_strong(sk.flags + prev, &expect, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          __hip_atomic_fetch_add(sk.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          f = expect;  // published after all
+      }
+      if (lane == 0) *(volatile unsigned*)(smem + 2 * BUF8) = (f == 1u) ? 1u : 0u;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    resume = *(volatile unsigned*)(smem + 2 * BUF8) != 0u;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slot loads below the poll
+    SDP_STAMP(3);
+    if (!resume) {  // abandoned: this segment computes the whole tile
+      kb = 0;
+      kn = nk;
+    }
+  }
+
   // The wave's 8 DMA pieces per K-tile (8 rows x 128 B each): [0,1] S1-X,
   // [2,3] S1-W, [4,5] S2-W, [6,7] S3-X.  Source pointers advance by BK per tile.
   const bf16_t* src[8];
@@ -732,23 +982,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   auto S3 = [&](int kt) { dma(6, kt); dma(7, kt); };
 
   f32x4 acc[4][8];
-  if (SK && mode == SEG_TAIL) {
-    // continue the head's accumulation (range p-1 computed it first, so this rarely waits)
-    const int prev = p - 8;  // range j - 1 of the same XCD
-    SDP_STAMP(2);
-    if (wave == 0) {
-      unsigned spins = 0;
-      while (__hip_atomic_load(sk.flags + prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 22)) {
-          if (lane == 0) __hip_atomic_fetch_add(sk.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the poll
-    SDP_STAMP(3);
+  if (SK && resume) {
     const __amdgpu_buffer_rsrc_t rs = sk_rsrc(sk.part + (int64_t)prev * SK_SLOT_FLOATS);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -847,7 +1081,12 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
                                                ((wave * 32 + i * 8 + j) * 64 + lane) * 16, 0, 16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (tid == 0) __hip_atomic_store(sk.flags + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {  // 0 -> 1; a consumer that gave up left 2: reset for the next launch
+      unsigned expect = 0u;
+      if (!__hip_atomic_compare_exchange_strong(sk.flags + p, &expect, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT))
+        __hip_atomic_store(sk.flags + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     SDP_STAMP(6);
     continue;
   }
@@ -855,6 +1094,8 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     // per wave: both K buffers, free once the balancing barrier above has passed); the host
     // routes resid_pre-with-activation and unaligned calls to EPI 1
     tile_epilogue_rows<ACT, 4, true>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + wave * 16384);
+  } else if constexpr (EPI >= 16) {  // whole-line epilogue with compile-time flags (EPI - 16)
+    tile_epilogue_fl<ACT, EPI - 16>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + wave * 16384);
   } else if constexpr (EPI == 5 || EPI == 6) {  // training epilogues (same staging)
     tile_epilogue_rows<ACT, 4, true, EPI - 4>(epi, acc, m0, n0, M, N, wm, wn, lane, fr, fq, smem + wave * 16384);
   } else {
@@ -862,6 +1103,10 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   }
   SDP_STAMP(6);
   }  // segments
+  if (epi.tline) {  // end of this workgroup: its stores have left (timeline runs only)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) atomicMax(epi.tline + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
 }
 
 #undef SDP_VMCNT
@@ -995,6 +1240,38 @@ extern "C" int sdp_gemm_set_exact_gelu(int on) {
   return old;
 }
 
+// Launch timeline (bench.py): while a buffer is set, fast-GEMM launch i gets slot i of it
+// ({start, end} u64 pair) until `slots` run out; launches past that are not timed.
+static unsigned long long* g_tl_buf = nullptr;
+static int g_tl_slots = 0, g_tl_next = 0;
+static std::mutex g_tl_mu;
+extern "C" int sdp_gemm_set_timeline(void* buf, int slots) {
+  std::lock_guard<std::mutex> lk(g_tl_mu);
+  const int used = g_tl_next;
+  g_tl_buf = (unsigned long long*)buf;
+  g_tl_slots = buf ? slots : 0;
+  g_tl_next = 0;
+  return used;
+}
+extern "C" int sdp_gemm_timeline_count(void) {
+  std::lock_guard<std::mutex> lk(g_tl_mu);
+  return g_tl_next;
+}
+static unsigned long long* tl_take() {
+  std::lock_guard<std::mutex> lk(g_tl_mu);
+  if (!g_tl_buf || g_tl_next >= g_tl_slots) return nullptr;
+  return g_tl_buf + 2 * (g_tl_next++);
+}
+
+// 1 (default): the model's epilogue flag combinations take tile_epilogue_fl; 0: the run-time
+// flag epilogue for every call (A/B switch, SDPNET_GEMM_EPI_SPEC=0)
+static int g_epi_spec = 1;
+extern "C" int sdp_gemm_set_epi_spec(int on) {
+  int old = g_epi_spec;
+  g_epi_spec = on ? 1 : 0;
+  return old;
+}
+
 static int g_nt_store = 0;
 extern "C" int sdp_gemm_set_store_policy(int nt) {
   int old = g_nt_store;
@@ -1072,6 +1349,9 @@ extern "C" int sdp_gemm_sk_status(void* stream, unsigned* out) {
 }
 
 #ifdef SDP_GEMM_STAMPS
+extern "C" int sdp_gemm_set_dephase(int ticks) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(fast::g_gemm_dephase), &ticks, sizeof(int));
+}
 extern "C" int sdp_gemm_stamps(void* dst, int64_t bytes, int clear) {
   hipError_t rc = hipDeviceSynchronize();
   if (rc == hipSuccess && dst) rc = hipMemcpyFromSymbol(dst, HIP_SYMBOL(fast::g_gemm_stamps), std::min<int64_t>(bytes, sizeof(fast::g_gemm_stamps)));
@@ -1199,6 +1479,7 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
                          (ldw % 8 == 0) && ((uintptr_t)W % 16 == 0);
     if (!g_force_generic && aligned && sdp_gemm_variant(dtype, M, N, K) == 1) {
       const int tm = (M + fast::BM - 1) / fast::BM, tn = (N + fast::BN - 1) / fast::BN;
+      e.tline = g_tl_buf ? tl_take() : nullptr;
       // the whole-line epilogue needs 16-B aligned output / residual rows and N % 8 == 0,
       // and implements resid_pre only without an activation
       const bool rows_ok = (N % 8 == 0) && (ldy % 8 == 0) && ((uintptr_t)Y % 16 == 0) &&
@@ -1228,7 +1509,39 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
   } while (0)
       // exact-erf GELU goes through the runtime-activation epilogue (apply_act)
       const int ak = (act == ACT_GELU && g_exact_gelu) ? -1 : act;
-      if (fk == 14) {
+      // the model's epilogue combinations get compile-time flags (tile_epilogue_fl)
+      const int fl = (bias ? fast::EF_BIAS : 0) | (ln_stats ? fast::EF_LN : 0) | (R ? fast::EF_RESID : 0) |
+                     (e.part ? fast::EF_PART : 0);
+      // byte extents of the operands the specialised epilogue addresses with 32-bit offsets
+      auto extent = [M](const RowMap& rm, int64_t row_bytes) -> int64_t {
+        const int64_t last = (int64_t)((M - 1) / rm.grp) * rm.gstride + rm.off + (M - 1) % rm.grp;
+        int64_t mx = last;
+        if ((M - 1) / rm.grp > 0) mx = std::max(mx, (int64_t)((M - 1) / rm.grp - 1) * rm.gstride + rm.off + rm.grp - 1);
+        return (mx + 1) * row_bytes;
+      };
+      const int64_t ob = extent(ym, ldy * 2), rb = R ? extent(rm, ldr * 2) : 0, pb = e.part ? extent(ym, (N / 64) * 8) : 0;
+      const bool small = ob < (1ll << 31) && rb < (1ll << 31) && pb < (1ll << 31) && ym.grp >= 8 && rm.grp >= 8;
+      e.out_bytes = (uint32_t)ob;
+      e.res_bytes = (uint32_t)rb;
+      e.part_bytes = (uint32_t)pb;
+      const bool spec = g_epi_spec && !ws && fk == 14 && small && !e.nt_store && (ak == ACT_NONE || ak == ACT_GELU) &&
+                        (fl == (fast::EF_BIAS | fast::EF_LN) || fl == (fast::EF_RESID | fast::EF_PART) ||
+                         fl == (fast::EF_BIAS | fast::EF_RESID | fast::EF_PART));
+      if (spec) {
+#define SDP_8PH_DP(A, E)                                                                                   \
+  hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,        \
+                     (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk)
+#define SDP_8PH_FL(A)                                                           \
+  do {                                                                          \
+    if (fl == (fast::EF_BIAS | fast::EF_LN)) SDP_8PH_DP(A, 16 + 3);             \
+    else if (fl == (fast::EF_RESID | fast::EF_PART)) SDP_8PH_DP(A, 16 + 12);    \
+    else SDP_8PH_DP(A, 16 + 13);                                                \
+  } while (0)
+        if (ak == ACT_NONE) SDP_8PH_FL(ACT_NONE);
+        else SDP_8PH_FL(ACT_GELU);
+#undef SDP_8PH_FL
+#undef SDP_8PH_DP
+      } else if (fk == 14) {
         if (ak == ACT_NONE) SDP_8PH(ACT_NONE, 4);
         else if (ak == ACT_GELU) SDP_8PH(ACT_GELU, 4);
         else if (ak == ACT_TANH) SDP_8PH(ACT_TANH, 4);

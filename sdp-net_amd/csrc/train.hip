@@ -1611,19 +1611,34 @@ extern "C" int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, in
 //   soft targets (probability rows t_i, the CutMix / MixUp targets of dataset_generator.py:105-110):
 //                 t'_i = (1 - eps) t_i + eps / K,  loss_i = -sum_k t'_ik log p_ik,
 //                 dlogits_i = grad_scale / B * (softmax_i * sum_k t'_ik - t'_i)
-// loss_sum += sum_i loss_i / B (atomic, fp32).  One wave per row.  A hard label outside [0, K)
-// (ignore_index -100 included, which this loss does not implement) is never dereferenced: the
-// row's loss and gradient become NaN, so the bad batch shows in the loss instead of reading
-// out of bounds (torch raises there).
+// loss_sum += sum_i loss_i / n (atomic, fp32), n = B for soft targets and the number of rows
+// whose label is not ignore_index for hard labels (nn.CrossEntropyLoss's default
+// ignore_index = -100, reduction 'mean': an ignored row adds nothing to the loss and gets a zero
+// gradient row; every row ignored gives a NaN loss, as torch's 0 / 0).  One wave per row; every
+// wave counts the ignored labels itself (B int64 reads).  Any other hard label outside [0, K) is
+// never dereferenced: the row's loss and gradient become NaN, so the bad batch shows in the loss
+// instead of reading out of bounds (torch raises there).
 // ---------------------------------------------------------------------------
 template <typename T, bool SOFT>
 __global__ __launch_bounds__(256) void ce_k(const T* __restrict__ L, int64_t ldl, const int64_t* __restrict__ y,
                                             const float* __restrict__ tg, int64_t ldt, int B, int K, float eps,
                                             float grad_scale, T* __restrict__ D, int64_t ldd,
-                                            float* __restrict__ loss) {
+                                            float* __restrict__ loss, int64_t ignore) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= B) return;
+  float nrows = (float)B;
+  if constexpr (!SOFT) {
+    float cnt = 0.f;
+    for (int i = lane; i < B; i += 64) cnt += (y[i] != ignore) ? 1.f : 0.f;
+    nrows = wave_sum(cnt);
+    if (y[r] == ignore) {  // no loss, zero gradient row
+      if (r == 0 && lane == 0 && nrows == 0.f) atomicAdd(loss, NAN);
+      if (D)
+        for (int c = lane; c < K; c += 64) D[r * ldd + c] = from_f<T>(0.f);
+      return;
+    }
+  }
   const T* lp = L + r * ldl;
   float mx = -INFINITY, sl = 0.f;
   for (int c = lane; c < K; c += 64) {
@@ -1658,9 +1673,9 @@ __global__ __launch_bounds__(256) void ce_k(const T* __restrict__ L, int64_t ldl
     const float ly = ok ? to_f<T>(lp[lab]) : NAN;
     li = (1.0f - eps) * (lse - ly) + eps * (lse - sl / (float)K);
   }
-  if (lane == 0) atomicAdd(loss, li / (float)B);
+  if (lane == 0) atomicAdd(loss, li / nrows);
   if (!D) return;
-  const float sc = grad_scale / (float)B, inv = 1.0f / se;
+  const float sc = grad_scale / nrows, inv = 1.0f / se;
   const float bad = (!SOFT && !(lab >= 0 && lab < K)) ? NAN : 0.0f;
   for (int c = lane; c < K; c += 64) {
     const float pr = expf(to_f<T>(lp[c]) - mx) * inv;
@@ -1674,7 +1689,7 @@ __global__ __launch_bounds__(256) void ce_k(const T* __restrict__ L, int64_t ldl
 template <bool SOFT>
 static int ce_launch(int dtype, const void* logits, int64_t ldl, const int64_t* labels, const float* targets,
                      int64_t ldt, int B, int K, float eps, float grad_scale, void* dlogits, int64_t ldd, float* loss,
-                     void* stream) {
+                     void* stream, int64_t ignore = -100) {
   if (!logits || !loss || B < 0 || K <= 0) return (int)hipErrorInvalidValue;
   if (SOFT ? !targets : !labels) return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
@@ -1682,10 +1697,10 @@ static int ce_launch(int dtype, const void* logits, int64_t ldl, const int64_t* 
   dim3 grid((B + 3) / 4);
   if (dtype == 1)
     hipLaunchKernelGGL((ce_k<bf16_t, SOFT>), grid, dim3(256), 0, s, (const bf16_t*)logits, ldl, labels, targets, ldt,
-                       B, K, eps, grad_scale, (bf16_t*)dlogits, ldd, loss);
+                       B, K, eps, grad_scale, (bf16_t*)dlogits, ldd, loss, ignore);
   else if (dtype == 0)
     hipLaunchKernelGGL((ce_k<float, SOFT>), grid, dim3(256), 0, s, (const float*)logits, ldl, labels, targets, ldt, B,
-                       K, eps, grad_scale, (float*)dlogits, ldd, loss);
+                       K, eps, grad_scale, (float*)dlogits, ldd, loss, ignore);
   else
     return (int)hipErrorInvalidValue;
   return SDP_CHECK_LAUNCH();
@@ -1694,6 +1709,13 @@ static int ce_launch(int dtype, const void* logits, int64_t ldl, const int64_t* 
 extern "C" int sdp_ce_loss(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K, float eps,
                            float grad_scale, void* dlogits, int64_t ldd, float* loss, void* stream) {
   return ce_launch<false>(dtype, logits, ldl, labels, nullptr, 0, B, K, eps, grad_scale, dlogits, ldd, loss, stream);
+}
+
+extern "C" int sdp_ce_loss_ignore(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K,
+                                  float eps, float grad_scale, int64_t ignore_index, void* dlogits, int64_t ldd,
+                                  float* loss, void* stream) {
+  return ce_launch<false>(dtype, logits, ldl, labels, nullptr, 0, B, K, eps, grad_scale, dlogits, ldd, loss, stream,
+                          ignore_index);
 }
 
 extern "C" int sdp_ce_loss_soft(int dtype, const void* logits, int64_t ldl, const float* targets, int64_t ldt, int B,

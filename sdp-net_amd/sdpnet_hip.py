@@ -39,6 +39,9 @@ _SIGS = {
     "sdp_gemm_force_generic": ([_i32], _i32),
     "sdp_gemm_set_fast_kernel": ([_i32], _i32),
     "sdp_gemm_set_store_policy": ([_i32], _i32),
+    "sdp_gemm_set_epi_spec": ([_i32], _i32),
+    "sdp_gemm_set_timeline": ([_vp, _i32], _i32),
+    "sdp_gemm_timeline_count": ([], _i32),
     "sdp_gemm_set_group_m": ([_i32], _i32),
     "sdp_gemm_set_exact_gelu": ([_i32], _i32),
     "sdp_gemm_workspace_bytes": ([], _i64),
@@ -109,6 +112,7 @@ _SIGS = {
     "sdp_dw_wgrad_chunks": ([_i32], _i32),
     "sdp_dw_wgrad": ([_i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _i32, _i32, _i32, _i32, _i32, _vp, _vp], _i32),
     "sdp_ce_loss": ([_i32, _vp, _i64, _vp, _i32, _i32, _f32, _f32, _vp, _i64, _vp, _vp], _i32),
+    "sdp_ce_loss_ignore": ([_i32, _vp, _i64, _vp, _i32, _i32, _f32, _f32, _i64, _vp, _i64, _vp, _vp], _i32),
     "sdp_ce_loss_soft": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _f32, _f32, _vp, _i64, _vp, _vp], _i32),
     "sdp_mt_block_bytes": ([], _i32),
     "sdp_grad_sumsq": ([_vp, _vp, _vp, _i32, _vp, _vp], _i32),
@@ -128,18 +132,28 @@ _SIGS = {
 
 _lib = None
 
-# Optional launch timer (bench.py roofline): callable(name, shape_key, flops, start_evt, end_evt)
-_TIMER = None
+# Fast-GEMM launch timeline (bench.py's roofline): while active, every launch that takes the
+# 8-phase kernel writes its {first workgroup start, last workgroup end} (s_memrealtime ticks,
+# 100 MHz) into one slot of a device buffer -- also inside a captured and replayed graph, where
+# HIP events cannot be recorded -- and the host side records (slot, M, N, K, flops, bytes).
+_TL = None
+TIMELINE_TICK_NS = 10.0
 
 
-def set_launch_timer(fn):
-    """Install fn(name, key, flops, algorithmic_bytes, ev_start, ev_end), called after
-    every GEMM launch with HIP events recorded around it on the launch stream
-    (bench.py's roofline).  Returns the previous timer."""
-    global _TIMER
-    old = _TIMER
-    _TIMER = fn
-    return old
+def gemm_timeline_begin(buf: torch.Tensor):
+    """Start recording fast-GEMM launches into buf (int64 device tensor, 2 entries per slot)."""
+    global _TL
+    _req(buf.is_cuda and buf.dtype == torch.int64 and buf.is_contiguous() and buf.numel() >= 2)
+    lib().sdp_gemm_set_timeline(buf.data_ptr(), buf.numel() // 2)
+    _TL = []
+
+
+def gemm_timeline_end():
+    """Stop recording; returns [(slot, M, N, K, flops, algorithmic_bytes)] in launch order."""
+    global _TL
+    lib().sdp_gemm_set_timeline(None, 0)
+    out, _TL = _TL, None
+    return out or []
 
 
 def lib():
@@ -160,6 +174,9 @@ def lib():
         kern = os.environ.get("SDPNET_GEMM_NT_STORE")  # streaming output stores in the GEMM epilogue
         if kern:
             L.sdp_gemm_set_store_policy(int(kern))
+        kern = os.environ.get("SDPNET_GEMM_EPI_SPEC")  # compile-time-flag GEMM epilogues (1 default)
+        if kern:
+            L.sdp_gemm_set_epi_spec(int(kern))
         kern = os.environ.get("SDPNET_GEMM_GROUP_M")  # tile raster of the 8-phase GEMM (-1 auto, 1 row-major)
         if kern:
             L.sdp_gemm_set_group_m(int(kern))
@@ -258,13 +275,9 @@ def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Option
         r = [None, 0, 0, 0, 0]
     if dt == BF16:
         _ensure_workspace(y.t, M, N, K)
-    timer = _TIMER
-    if timer is not None:
-        # inside a graph capture the events become external event-record nodes of the graph
-        ext = torch.cuda.is_current_stream_capturing()
-        e0 = torch.cuda.Event(enable_timing=True, external=ext)
-        e1 = torch.cuda.Event(enable_timing=True, external=ext)
-        e0.record()
+    tl = _TL
+    if tl is not None:
+        slot0 = lib().sdp_gemm_timeline_count()
     if ln is None and part is None:
         rc = lib().sdp_gemm(dt, *x.args(), w.data_ptr(), w.stride(0), _ptr(bias), *r, *y.args(), M, N, K, act,
                             int(bool(resid_pre)), _stream(y.t))
@@ -276,11 +289,10 @@ def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Option
                                int(bool(resid_pre)), _ptr(ln[0]) if ln else None, _ptr(ln[1]) if ln else None,
                                _ptr(part), _stream(y.t))
     _check(rc, "gemm")
-    if timer is not None:
-        e1.record()
+    if tl is not None and lib().sdp_gemm_timeline_count() > slot0:
         es = x.t.element_size()
         nbytes = es * (M * K + N * K + M * N * (2 if resid is not None else 1)) + (4 * N if bias is not None else 0)
-        timer("gemm", (M, N, K, lib().sdp_gemm_variant(dt, M, N, K)), 2.0 * M * N * K, nbytes, e0, e1)
+        tl.append((slot0, M, N, K, 2.0 * M * N * K, nbytes))
 
 
 # Stream-K workspaces, one per HIP stream that has run a GEMM (caller-owned memory the
@@ -295,14 +307,16 @@ def _ensure_workspace(t: torch.Tensor, M: int, N: int, K: int):
     if key in _WS or not lib().sdp_gemm_sk_applies(M, N, K) or torch.cuda.is_current_stream_capturing():
         return
     ws = torch.zeros(int(lib().sdp_gemm_workspace_bytes()), dtype=torch.uint8, device=t.device)
-    _check(lib().sdp_gemm_set_workspace(s.cuda_stream, ws.data_ptr(), ws.numel()), "gemm_set_workspace")
-    _WS[key] = ws
+    rc = lib().sdp_gemm_set_workspace(s.cuda_stream, ws.data_ptr(), ws.numel())
+    # every registration slot taken (more streams than the library tracks): this stream keeps
+    # the data-parallel schedule (remembered, so it is not retried per launch)
+    _WS[key] = ws if rc == 0 else None
 
 
 def gemm_sk_status(t: torch.Tensor) -> int:
     """Give-up count of the stream-K waits on the current stream's workspace (0 expected)."""
     key = (t.device.index, torch.cuda.current_stream(t.device).cuda_stream)
-    if key not in _WS:
+    if _WS.get(key) is None:
         return 0
     out = ctypes.c_uint(0)
     _check(lib().sdp_gemm_sk_status(key[1], ctypes.byref(out)), "gemm_sk_status")
@@ -627,7 +641,10 @@ def _zero_row(device, n: int) -> torch.Tensor:
     z = _ZERO_ROWS.get(key)
     if z is None or z.numel() < n:
         z = torch.zeros(max(n, 4096), dtype=torch.bfloat16, device=device)
-        _ZERO_ROWS[key] = z
+        # inside a graph capture the zeros are a memset node that only runs on replay: such a
+        # buffer is valid for that graph alone, so it is not cached for eager launches
+        if not torch.cuda.is_current_stream_capturing():
+            _ZERO_ROWS[key] = z
     return z
 
 
@@ -793,13 +810,16 @@ def dw_wgrad(a: Rows, dy: Rows, B: int, H: int, W: int, C: int, k: int) -> torch
 
 
 def ce_loss(logits: torch.Tensor, labels: torch.Tensor, eps: float, grad_scale: float,
-            dlogits: Optional[torch.Tensor], loss: torch.Tensor):
+            dlogits: Optional[torch.Tensor], loss: torch.Tensor, ignore_index: int = -100):
+    """Label-smoothed CE, mean over the rows whose label != ignore_index (those get zero dlogits)."""
     _need_cuda(logits, labels, dlogits, loss)
     _req(labels.dtype == torch.int64 and loss.dtype == torch.float32, "ce_loss dtypes")
     B, K = logits.shape
-    rc = lib().sdp_ce_loss(dcode(logits.dtype), logits.data_ptr(), logits.stride(0), labels.contiguous().data_ptr(),
-                           B, K, float(eps), float(grad_scale), _ptr(dlogits),
-                           dlogits.stride(0) if dlogits is not None else 0, loss.data_ptr(), _stream(loss))
+    _req(labels.numel() == B, "ce_loss: one label per row")
+    rc = lib().sdp_ce_loss_ignore(dcode(logits.dtype), logits.data_ptr(), logits.stride(0),
+                                  labels.contiguous().data_ptr(), B, K, float(eps), float(grad_scale),
+                                  int(ignore_index), _ptr(dlogits), dlogits.stride(0) if dlogits is not None else 0,
+                                  loss.data_ptr(), _stream(loss))
     _check(rc, "ce_loss")
 
 

@@ -1299,13 +1299,13 @@ def tape_backward(tape, dlogits: torch.Tensor, params: List[torch.Tensor]) -> Li
 # ---------------------------------------------------------------------------
 class _CEFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, labels, eps):
+    def forward(ctx, logits, labels, eps, ignore_index=-100):
         loss = torch.zeros(1, dtype=torch.float32, device=logits.device)
         d = torch.empty_like(logits)
         if labels.is_floating_point():  # probability targets (CutMix / MixUp, dataset_generator.py:105-110)
             sp.ce_loss_soft(logits.contiguous(), labels.float().contiguous(), eps, 1.0, d, loss)
         else:
-            sp.ce_loss(logits.contiguous(), labels, eps, 1.0, d, loss)
+            sp.ce_loss(logits.contiguous(), labels, eps, 1.0, d, loss, ignore_index)
         ctx.save_for_backward(d)
         return loss[0]
 
@@ -1317,15 +1317,18 @@ class _CEFn(torch.autograd.Function):
         M, K = d.shape
         sc = g.float().reshape(1).expand(M).contiguous()
         sp.rowscale_add(_dense(d), _dense(out), M, K, scale=sc, sgrp=1)
-        return out, None, None
+        return out, None, None, None
 
 
-def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, label_smoothing: float = 0.0) -> torch.Tensor:
-    """nn.CrossEntropyLoss(label_smoothing=...)(logits, labels) (mean over the batch) as one
-    HIP kernel (training_tools.py:76, :88).  ``labels`` are int64 class indices or float
-    probability rows [B, K] (the CutMix / MixUp targets, dataset_generator.py:105-110).  A class
-    index outside [0, K) gives a NaN loss (torch raises; ignore_index is not implemented)."""
-    return _CEFn.apply(logits, labels, float(label_smoothing))
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, label_smoothing: float = 0.0,
+                  ignore_index: int = -100) -> torch.Tensor:
+    """nn.CrossEntropyLoss(label_smoothing=..., ignore_index=...)(logits, labels) as one HIP
+    kernel (training_tools.py:76, :88).  ``labels`` are int64 class indices or float probability
+    rows [B, K] (the CutMix / MixUp targets, dataset_generator.py:105-110).  As torch's 'mean'
+    reduction: rows labelled ignore_index (default -100) are left out of the loss and of the
+    divisor and get zero gradient; all rows ignored gives NaN.  Any other class index outside
+    [0, K) gives a NaN loss (torch raises)."""
+    return _CEFn.apply(logits, labels, float(label_smoothing), int(ignore_index))
 
 
 class AdamW(torch.optim.Optimizer):

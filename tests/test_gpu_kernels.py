@@ -469,6 +469,53 @@ def test_gemm_emits_row_partials(kern, M, N, K):
 
 
 
+@pytest.mark.parametrize("act", [0, 1])
+@pytest.mark.parametrize("combo", ["ln_bias", "resid_part", "bias_resid_part"])
+@pytest.mark.parametrize("M,N,K", [(25088, 768, 768), (1003, 3072, 768), (70001, 768, 3072), (300, 2304, 768),
+                                   (513, 320, 128)])
+def test_gemm_specialised_epilogue_bit_identical(act, combo, M, N, K):
+    """The compile-time-flag epilogue (sdp_gemm_set_epi_spec(1), the default) stores exactly the
+    run-time-flag epilogue's outputs -- row-mapped token buffer, in-place residual, ragged M and
+    N -- and emits the same LN partials to fp32 rounding (one-pass dot2 sums vs two-pass)."""
+    B_, R = 2, 3
+    P = (M + B_ - 1) // B_
+    Mt = B_ * P
+    Nt = R + P
+    x = rnd(Mt, K, dtype=BF, seed=81)
+    w = rnd(N, K, dtype=BF, seed=82, scale=0.05)
+    b = rnd(N, seed=83) if combo != "resid_part" else None
+    tok0 = rnd(B_ * Nt, N, dtype=BF, seed=84)
+    nch = N // 64
+    ln = None
+    if combo == "ln_bias":
+        part_x = torch.empty(Mt, (K + 63) // 64, 2, device=DEV)
+        sp.row_partials(sp.dense(x), Mt, K, part_x)
+        st = torch.empty(Mt, 2, device=DEV)
+        sp.ln_stats(part_x, sp.dense(x), Mt, K, 1e-5, st)
+        g, be = rnd(K, seed=85) * 0.2 + 1, rnd(K, seed=86) * 0.2
+        w, colsum, b = sp.fold_ln_weight(w.float(), g, be, b, BF)
+        ln = (st, colsum)
+    outs = []
+    for spec in (0, 1):
+        old = sp.lib().sdp_gemm_set_epi_spec(spec)
+        try:
+            tok = tok0.clone()
+            img = sp.Rows(tok, N, P, Nt, R)
+            part = torch.full((B_ * Nt, nch, 2), float("nan"), device=DEV) if combo != "ln_bias" else None
+            resid = img if combo != "ln_bias" else None
+            sp.gemm(sp.dense(x), w, img, Mt, N, K, bias=b, resid=resid, act=act, ln=ln, part=part)
+            torch.cuda.synchronize()
+            outs.append((tok, part))
+        finally:
+            sp.lib().sdp_gemm_set_epi_spec(old)
+    assert torch.equal(outs[0][0], outs[1][0]), "specialised epilogue output differs"
+    if combo != "ln_bias":
+        p0, p1 = outs[0][1].view(B_, Nt, nch, 2), outs[1][1].view(B_, Nt, nch, 2)
+        assert torch.isnan(p1[:, :R]).all()  # register rows untouched
+        close(p1[:, R:, :, 0], p0[:, R:, :, 0], torch.float32, rel=1e-5, what="partial mean")
+        close(p1[:, R:, :, 1], p0[:, R:, :, 1], torch.float32, rel=1e-4, what="partial M2")
+
+
 # ------------------------------------------------- stream-K schedule of the 8-phase GEMM
 def _gemm_both_schedules(run):
     """run() -> output tensor; returns (data-parallel result, stream-K result)."""

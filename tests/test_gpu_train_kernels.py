@@ -301,7 +301,7 @@ def test_ce_loss_soft_targets(dtype, eps):
 def test_ce_loss_label_out_of_range_is_nan_not_oob():
     B, K = 8, 100
     logits = rnd(B, K, seed=28)
-    labels = torch.tensor([0, 5, -100, 99, 100, 3, 7, 1], device=DEV)
+    labels = torch.tensor([0, 5, -7, 99, 100, 3, 7, 1], device=DEV)
     d = torch.empty_like(logits)
     loss = torch.zeros(1, device=DEV)
     sp.ce_loss(logits, labels, 0.0, 1.0, d, loss)
@@ -309,6 +309,40 @@ def test_ce_loss_label_out_of_range_is_nan_not_oob():
     assert torch.isnan(loss).all()
     bad = torch.isnan(d).all(dim=1).cpu()
     assert bad.tolist() == [False, False, True, False, True, False, False, False]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("eps", [0.0, 0.1])
+@pytest.mark.parametrize("ignore", [-100, 3])
+def test_ce_loss_ignore_index(dtype, eps, ignore):
+    """nn.CrossEntropyLoss's ignore_index (default -100, training_tools.py:72): ignored rows leave
+    the loss and the mean's divisor and get zero gradient, against F.cross_entropy; every row
+    ignored gives NaN as torch does."""
+    import sdpnet_train as st
+    B, K = 37, 1000
+    logits = rnd(B, K, seed=29, dtype=dtype, scale=3)
+    labels = torch.randint(0, K, (B,), generator=torch.Generator().manual_seed(2))
+    labels[[0, 5, 6, 20, 36]] = ignore
+    labels = labels.to(DEV)
+    d = torch.empty_like(logits)
+    loss = torch.zeros(1, device=DEV)
+    sp.ce_loss(logits, labels, eps, 8.0, d, loss, ignore_index=ignore)
+    lr = logits.float().clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, labels, label_smoothing=eps, ignore_index=ignore)
+    (g,) = torch.autograd.grad(ref * 8.0, lr)
+    close(loss, ref.detach().view(1), 1e-5, "ce loss (ignore_index)")
+    close(d, g, 1e-5 if dtype == torch.float32 else 2e-2, "ce dlogits (ignore_index)")
+    assert (d[[0, 5, 6, 20, 36]] == 0).all()
+    lr2 = logits.float().clone().requires_grad_(True)
+    l2 = st.cross_entropy(lr2, labels, label_smoothing=eps, ignore_index=ignore)
+    l2.backward()
+    close(l2.detach().view(1), ref.detach().view(1), 1e-5, "cross_entropy(ignore_index)")
+    close(lr2.grad, g / 8.0, 1e-5, "cross_entropy(ignore_index) grad")
+    # every row ignored: torch's mean is 0 / 0
+    loss.zero_()
+    sp.ce_loss(logits, torch.full((B,), ignore, device=DEV), eps, 1.0, d, loss, ignore_index=ignore)
+    torch.cuda.synchronize()
+    assert torch.isnan(loss).all() and (d == 0).all()
 
 
 @pytest.mark.parametrize("xdt,ydt", [(BF, torch.float32), (BF, BF), (torch.float32, BF)])

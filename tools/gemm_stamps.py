@@ -89,7 +89,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="mixer_cc,mixer_up,mixer_down,enc_qkv")
     ap.add_argument("--schedules", default="0,1")
+    ap.add_argument("--dephase", default="0", help="first-round start offsets per group of 8 workgroups per XCD, "
+                    "in 10-ns ticks (experiment: group g = (b >> 3) & 3 waits g * value)")
     args = ap.parse_args()
+    L = sp.lib()
+    L.sdp_gemm_set_dephase.argtypes = [ctypes.c_int]
     dev = torch.device("cuda")
     bf = torch.bfloat16
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -101,12 +105,20 @@ def main():
         r = torch.randn(M, N, generator=g).to(bf).to(dev) if has_r else None
         y = torch.empty(M, N, dtype=bf, device=dev)
         print(f"{name} M={M} N={N} K={K}")
-        for sch in [int(c) for c in args.schedules.split(",")]:
+        for sch, dph in [(int(c), int(d)) for c in args.schedules.split(",") for d in args.dephase.split(",")]:
             sp.lib().sdp_gemm_set_schedule(sch)
+            assert L.sdp_gemm_set_dephase(dph) == 0
             run = lambda: sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, bias=b,  # noqa: E731
                                   resid=None if r is None else sp.dense(r), act=act)
             for _ in range(30):
                 run()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(20):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            print(f"  dephase {dph} ticks: {1e3 * e0.elapsed_time(e1) / 20:.1f} us per launch (events)")
             read_stamps(1)
             run()
             sk = sch and sp.lib().sdp_gemm_sk_applies(M, N, K)
