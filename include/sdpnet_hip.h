@@ -407,6 +407,13 @@ int sdp_ln_bwd_mixed(int x_dtype, int dy_dtype, const void* X, int64_t ldx, int 
  * DS = P * (DPm - sum(DPm * P)), DPm = DPd with the same mask. */
 int sdp_softmax_fwd(int dtype, const float* S, int64_t lds, void* P, void* Pd, int64_t ldp, int rows, int N, int Npad,
                     float scale, float p, uint64_t seed, void* stream);
+/* The same with an additive fp32 mask before the softmax (the masked attention of EncoderLayer in
+ * train mode, layers.py:291 SDPA attn_mask / :294-295 masked_fill(mask == 0, -inf)): row r = z * N + i
+ * of S adds mask[(z / mask_zdiv) * mask_sb + (z % mask_zdiv) * mask_sh + i * N + c] (strides 0
+ * broadcast over batch / head; -inf gives exact zeros, a fully masked row NaN as torch). */
+int sdp_softmax_fwd_mask(int dtype, const float* S, int64_t lds, void* P, void* Pd, int64_t ldp, int rows, int N,
+                         int Npad, float scale, float p, uint64_t seed, const float* mask, int64_t mask_sb,
+                         int64_t mask_sh, int mask_zdiv, void* stream);
 int sdp_softmax_bwd(int dtype, const void* P, int64_t ldp, const void* DPd, int64_t lddp, void* DS, int64_t ldds,
                     int rows, int N, int Npad, float p, uint64_t seed, void* stream);
 

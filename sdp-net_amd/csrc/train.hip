@@ -1237,23 +1237,40 @@ extern "C" int sdp_ln_bwd_mixed(int x_dtype, int dy_dtype, const void* X, int64_
 // (they feed the PV product as K padding).  Backward: dS = P * (dPm - sum(dPm * P)),
 // dPm = dPd with the same dropout mask.  One wave per row; S fp32.
 // ---------------------------------------------------------------------------
+// Optional additive fp32 attention mask of the materialised softmax (the masked manual /
+// SDPA attention of EncoderLayer, layers.py:289-298): row r = z * N + i of S (z = b * zdiv + h)
+// adds mask[(z / zdiv) * sb + (z % zdiv) * sh + i * N + c] (batch / head strides 0 = broadcast)
+// before the max; -inf entries give exact zeros.
+struct SmMask {
+  const float* m;
+  int64_t sb, sh;
+  int zdiv;
+  SDP_DEV const float* row(int64_t r, int N) const {
+    if (!m) return nullptr;
+    const int64_t z = r / N, i = r - z * N;
+    return m + (z / zdiv) * sb + (z % zdiv) * sh + i * N;
+  }
+};
+
 template <typename T>
 __global__ __launch_bounds__(256) void softmax_fwd_k(const float* __restrict__ S, int64_t lds, T* __restrict__ P,
                                                      T* __restrict__ Pd, int64_t ldp, int rows, int N, int Npad,
-                                                     float scale, float p, uint64_t seed) {
+                                                     float scale, float p, uint64_t seed, SmMask mk) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
   const float* sp_ = S + r * lds;
+  const float* mp = mk.row(r, N);
+  auto val = [&](int c) { return mp ? fmaf(sp_[c], scale, mp[c]) : sp_[c] * scale; };
   float mx = -INFINITY;
-  for (int c = lane; c < N; c += 64) mx = fmaxf(mx, sp_[c] * scale);
+  for (int c = lane; c < N; c += 64) mx = fmaxf(mx, val(c));
   mx = wave_max(mx);
   float sum = 0.f;
-  for (int c = lane; c < N; c += 64) sum += expf(sp_[c] * scale - mx);
+  for (int c = lane; c < N; c += 64) sum += expf(val(c) - mx);
   sum = wave_sum(sum);
   const float inv = 1.0f / sum, kp = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
   for (int c = lane; c < Npad; c += 64) {
-    float v = c < N ? expf(sp_[c] * scale - mx) * inv : 0.f;
+    float v = c < N ? expf(val(c) - mx) * inv : 0.f;
     P[r * ldp + c] = from_f<T>(v);
     if (Pd) {
       float d = v;
@@ -1314,11 +1331,12 @@ SDP_DEV void load4(const T* p, float (&v)[4]) {
 template <typename T>
 __global__ __launch_bounds__(256) void softmax_fwd_r(const float* __restrict__ S, int64_t lds, T* __restrict__ P,
                                                      T* __restrict__ Pd, int64_t ldp, int rows, int N, int Npad,
-                                                     float scale, float p, uint64_t seed) {
+                                                     float scale, float p, uint64_t seed, SmMask mk) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
   const float* sp_ = S + r * lds;
+  const float* mp = mk.row(r, N);
   float v[2][4];
   float mx = -INFINITY;
 #pragma unroll
@@ -1328,7 +1346,7 @@ __global__ __launch_bounds__(256) void softmax_fwd_r(const float* __restrict__ S
       const f32x4 t = *(const f32x4*)(sp_ + c);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        v[i][q] = c + q < N ? t[q] * scale : -INFINITY;
+        v[i][q] = c + q < N ? (mp ? fmaf(t[q], scale, mp[c + q]) : t[q] * scale) : -INFINITY;
         mx = fmaxf(mx, v[i][q]);
       }
     } else {
@@ -1402,30 +1420,43 @@ __global__ __launch_bounds__(256) void softmax_bwd_r(const T* __restrict__ P, in
   }
 }
 
+extern "C" int sdp_softmax_fwd_mask(int dtype, const float* S, int64_t lds, void* P, void* Pd, int64_t ldp, int rows,
+                                    int N, int Npad, float scale, float p, uint64_t seed, const float* mask,
+                                    int64_t mask_sb, int64_t mask_sh, int mask_zdiv, void* stream);
+
 extern "C" int sdp_softmax_fwd(int dtype, const float* S, int64_t lds, void* P, void* Pd, int64_t ldp, int rows, int N,
                                int Npad, float scale, float p, uint64_t seed, void* stream) {
-  if (!S || !P || rows < 0 || N <= 0 || Npad < N || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;
+  return sdp_softmax_fwd_mask(dtype, S, lds, P, Pd, ldp, rows, N, Npad, scale, p, seed, nullptr, 0, 0, 1, stream);
+}
+
+extern "C" int sdp_softmax_fwd_mask(int dtype, const float* S, int64_t lds, void* P, void* Pd, int64_t ldp, int rows,
+                                    int N, int Npad, float scale, float p, uint64_t seed, const float* mask,
+                                    int64_t mask_sb, int64_t mask_sh, int mask_zdiv, void* stream) {
+  if (!S || !P || rows < 0 || N <= 0 || Npad < N || p < 0.f || p >= 1.f || mask_zdiv <= 0 || mask_sb < 0 ||
+      mask_sh < 0)
+    return (int)hipErrorInvalidValue;
   if (rows == 0) return 0;
+  const SmMask mk{mask, mask_sb, mask_sh, mask_zdiv};
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((rows + 3) / 4);
   if (Npad <= 512 && Npad % 4 == 0 && lds % 4 == 0 && ldp % 4 == 0 && (uintptr_t)S % 16 == 0 && (uintptr_t)P % 16 == 0 &&
       (!Pd || (uintptr_t)Pd % 16 == 0)) {
     if (dtype == 1)
       hipLaunchKernelGGL(softmax_fwd_r<bf16_t>, grid, dim3(256), 0, s, S, lds, (bf16_t*)P, (bf16_t*)Pd, ldp, rows, N,
-                         Npad, scale, p, seed);
+                         Npad, scale, p, seed, mk);
     else if (dtype == 0)
       hipLaunchKernelGGL(softmax_fwd_r<float>, grid, dim3(256), 0, s, S, lds, (float*)P, (float*)Pd, ldp, rows, N,
-                         Npad, scale, p, seed);
+                         Npad, scale, p, seed, mk);
     else
       return (int)hipErrorInvalidValue;
     return SDP_CHECK_LAUNCH();
   }
   if (dtype == 1)
     hipLaunchKernelGGL(softmax_fwd_k<bf16_t>, grid, dim3(256), 0, s, S, lds, (bf16_t*)P, (bf16_t*)Pd, ldp, rows, N,
-                       Npad, scale, p, seed);
+                       Npad, scale, p, seed, mk);
   else if (dtype == 0)
     hipLaunchKernelGGL(softmax_fwd_k<float>, grid, dim3(256), 0, s, S, lds, (float*)P, (float*)Pd, ldp, rows, N, Npad,
-                       scale, p, seed);
+                       scale, p, seed, mk);
   else
     return (int)hipErrorInvalidValue;
   return SDP_CHECK_LAUNCH();

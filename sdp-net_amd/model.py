@@ -33,6 +33,10 @@ from layers import new_partials  # token-buffer plumbing of the fused path
 from sdpnet_engine import act_code, as_dtype, cached, compute_dtype, hooked as _hooked
 from training_utilities import KeLu
 
+# torch.compile of a training model: "layer" (default) = one custom op per sub-layer (DDP's
+# bucket all-reduce overlaps the compiled backward), "model" = one op pair for the whole model
+_COMPILE_TRAIN_OPS = os.environ.get("SDPNET_COMPILE_TRAIN_OPS", "layer")
+
 torch.set_float32_matmul_precision('high')  # model.py:9 (import side effect kept)
 
 # model.py:13-24
@@ -173,13 +177,18 @@ class MainModel(SdPModel):
             # backward runs on the HIP kernels too (sdpnet_train.py)
             if torch.compiler.is_compiling():
                 # torch.compile of a training model (cifar100_test.py:93, training_tools.py:39):
-                # one opaque op pair (sdpnet_ops.train_forward / train_backward)
+                # one opaque op per sub-layer, each with an op as its autograd formula
+                # (sdpnet_ops.train_layer), or the whole model as one op pair
+                # (SDPNET_COMPILE_TRAIN_OPS=model: sdpnet_ops.train_forward / train_backward)
                 if return_raw_outputs:
                     raise NotImplementedError("sdpnet training path returns logits only")
                 code = sdpnet_ops.DTYPE_CODES[compute_dtype(x, self)]
-                params = [p for p in self.parameters()]
-                logits, _ = torch.ops.sdpnet.train_forward(x, params, self._sdp_handle, num_registers, code)
-                return logits
+                if _COMPILE_TRAIN_OPS == "model":
+                    params = [p for p in self.parameters()]
+                    logits, _ = torch.ops.sdpnet.train_forward(x, params, self._sdp_handle, num_registers, code)
+                    return logits
+                import sdpnet_train
+                return sdpnet_train.compiled_train_forward(self, x, num_registers, code)
             import sdpnet_train
             return sdpnet_train.train_forward(self, x, num_registers, return_raw_outputs)
         if torch.compiler.is_compiling():

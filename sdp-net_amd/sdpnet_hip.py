@@ -108,6 +108,8 @@ _SIGS = {
     "sdp_ln_bwd": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _vp, _i64,
                     *_ROWMAP, _i32, _i32, _vp, _vp], _i32),
     "sdp_softmax_fwd": ([_i32, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _f32, _f32, _u64, _vp], _i32),
+    "sdp_softmax_fwd_mask": ([_i32, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _f32, _f32, _u64, _vp, _i64, _i64,
+                              _i32, _vp], _i32),
     "sdp_softmax_bwd": ([_i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _f32, _u64, _vp], _i32),
     "sdp_dw_wgrad_chunks": ([_i32], _i32),
     "sdp_dw_wgrad": ([_i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _i32, _i32, _i32, _i32, _i32, _vp, _vp], _i32),
@@ -780,11 +782,24 @@ def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows
 
 
 def softmax_fwd(S: torch.Tensor, P: torch.Tensor, Pd: Optional[torch.Tensor], rows: int, N: int, Npad: int,
-                scale: float, p: float = 0.0, seed: int = 0):
+                scale: float, p: float = 0.0, seed: int = 0, mask: Optional[Tuple[torch.Tensor, int, int, int]] = None):
+    """mask = (additive fp32 bias, batch stride, head stride, heads): bias[(z // heads) * sb +
+    (z % heads) * sh + i * N + c] is added to row z * N + i before the softmax."""
     _need_cuda(S, P, Pd)
     _req(S.dtype == torch.float32, "softmax S fp32")
-    rc = lib().sdp_softmax_fwd(dcode(P.dtype), S.data_ptr(), S.shape[-1], P.data_ptr(), _ptr(Pd), P.shape[-1], rows,
-                               N, Npad, float(scale), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(P))
+    if mask is None:
+        rc = lib().sdp_softmax_fwd(dcode(P.dtype), S.data_ptr(), S.shape[-1], P.data_ptr(), _ptr(Pd), P.shape[-1],
+                                   rows, N, Npad, float(scale), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(P))
+    else:
+        mb, sb, sh, zdiv = mask
+        _need_cuda(mb)
+        Z = rows // N
+        last = ((Z - 1) // zdiv) * sb + min(zdiv - 1, Z - 1) * sh + (N - 1) * N + N - 1
+        _req(mb.dtype == torch.float32 and rows % N == 0 and sb >= 0 and sh >= 0 and
+             last < mb.untyped_storage().nbytes() // 4 - mb.storage_offset(), "softmax mask bounds")
+        rc = lib().sdp_softmax_fwd_mask(dcode(P.dtype), S.data_ptr(), S.shape[-1], P.data_ptr(), _ptr(Pd),
+                                        P.shape[-1], rows, N, Npad, float(scale), float(p),
+                                        int(seed) & 0xFFFFFFFFFFFFFFFF, mb.data_ptr(), sb, sh, zdiv, _stream(P))
     _check(rc, "softmax_fwd")
 
 

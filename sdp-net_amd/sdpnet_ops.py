@@ -157,3 +157,78 @@ def _train_backward_formula(ctx, grad_logits, grad_key):
 
 
 train_forward.register_autograd(_train_backward_formula, setup_context=_train_setup_context)
+
+
+# ---------------------------------------------------------------------------
+# Training mode under torch.compile, per sub-layer (the default; SDPNET_COMPILE_TRAIN_OPS=model
+# selects the single op pair above): one op per patch-embedding / ConvMixer / EncoderLayer /
+# head (sdpnet_train.train_layers order), each with an autograd formula that is a second op:
+#
+#   sdpnet::train_layer(t, params, handle, layer, num_registers, dtype_code, batch) -> (out, key)
+#   sdpnet::train_layer_backward(grad_out, key, params, handle, layer) -> (grad_in, grads)
+#
+# so the compiled backward runs layer by layer and DDP (training_tools.py:36-39 compiles the
+# DDP-wrapped model) all-reduces a bucket while earlier layers' backward ops still run.  The
+# layer's ctx is parked under key.data_ptr() as for the whole-model pair.
+# ---------------------------------------------------------------------------
+@torch.library.custom_op("sdpnet::train_layer", mutates_args=(), device_types="cuda")
+def train_layer(t: Tensor, params: List[Tensor], handle: int, layer: int, num_registers: int, dtype_code: int,
+                batch: int) -> Tuple[Tensor, Tensor]:
+    import sdpnet_train
+    out, rec = sdpnet_train.layer_forward(lookup(handle), layer, t, num_registers, _DTYPES[dtype_code])
+    key = torch.empty(1, dtype=torch.int64, device=t.device)
+    _TAPES[key.data_ptr()] = rec
+    weakref.finalize(key, _drop_tape, key.data_ptr())
+    return out, key
+
+
+@train_layer.register_fake
+def _train_layer_fake(t, params, handle, layer, num_registers, dtype_code, batch):
+    import sdpnet_train
+    model = lookup(handle)
+    kind, _ = sdpnet_train.train_layers(model)[layer]
+    key = t.new_empty((1,), dtype=torch.int64)
+    dt = _DTYPES[dtype_code]
+    if kind == "embed":
+        B, C, Hp, Wp, ncls, R = _shapes(model, t, num_registers)
+        return t.new_empty((B * (R + Hp * Wp), C), dtype=sdpnet_train.stream_dtype(dt, C)), key
+    if kind == "head":
+        lins = [m for m in model.output_head.output_head if isinstance(m, torch.nn.Linear)]
+        return t.new_empty((batch, lins[-1].out_features), dtype=dt), key
+    return torch.empty_like(t), key
+
+
+@torch.library.custom_op("sdpnet::train_layer_backward", mutates_args=(), device_types="cuda")
+def train_layer_backward(grad_out: Tensor, key: Tensor, t: Tensor, params: List[Tensor], handle: int,
+                         layer: int) -> Tuple[Tensor, List[Tensor]]:
+    import sdpnet_train
+    rec = _TAPES.pop(key.data_ptr(), None)
+    if rec is None:
+        raise RuntimeError("sdpnet: no saved training forward for this layer's backward (backward run twice?)")
+    gin, grads = sdpnet_train.layer_backward(rec, grad_out)
+    if gin is None:  # the image input of layer 0 gets no gradient (ConvPatcher input, as eager)
+        gin = grad_out.new_empty((0,))
+    return gin, grads
+
+
+@train_layer_backward.register_fake
+def _train_layer_backward_fake(grad_out, key, t, params, handle, layer):
+    # t: the layer's forward input (shape / dtype of its gradient; the image for layer 0)
+    gin = grad_out.new_empty((0,)) if layer == 0 else torch.empty_like(t)
+    return gin, [torch.empty_like(p) for p in params]
+
+
+def _layer_setup_context(ctx, inputs, output):
+    t, params, handle, layer, num_registers, dtype_code, batch = inputs
+    ctx.save_for_backward(output[1], t, *params)
+    ctx.handle = handle
+    ctx.layer = layer
+
+
+def _layer_backward_formula(ctx, grad_out, grad_key):
+    key, t, *params = ctx.saved_tensors
+    gin, grads = torch.ops.sdpnet.train_layer_backward(grad_out, key, t, params, ctx.handle, ctx.layer)
+    return (None if ctx.layer == 0 else gin), list(grads), None, None, None, None, None
+
+
+train_layer.register_autograd(_layer_backward_formula, setup_context=_layer_setup_context)

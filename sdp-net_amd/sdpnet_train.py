@@ -520,7 +520,7 @@ def _enc_params(e) -> List[Optional[nn.Parameter]]:
             e.ff_linear2.weight, e.ff_linear2.bias]
 
 
-def _attn_materialized(qkvn, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seed):
+def _attn_materialized(qkvn, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seed, mask=None):
     """Attention with S / P materialised per (b, h) (fp32 path, and shapes the flash kernels
     do not take): S = QK^T (fp32) -> softmax (+ dropout) -> O = Pd V.  ``qkvn`` is the fp32
     operand copy in bf16 mode (P, dP and dS then stay fp32 as in the flash kernels; O is
@@ -533,7 +533,7 @@ def _attn_materialized(qkvn, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seed):
     Pm = _empty((B, Hn, N, Np), adt, dev)
     Pd = _empty((B, Hn, N, Np), adt, dev) if p_att > 0 else Pm
     sp.softmax_fwd(Sm.view(-1, Np), Pm.view(-1, Np), Pd.view(-1, Np) if p_att > 0 else None, Z * N, N, Np,
-                   1.0 / math.sqrt(hd), p_att, seed)
+                   1.0 / math.sqrt(hd), p_att, seed, mask=mask)
     del Sm
     o = _empty((T, C), adt, dev)
     sp.gemm_flex(Pd, qkvn, o, N, hd, N, ta=False, tb=False, lda=Np, ldb=3 * C, ldc=C, Z=Z, zdiv=Hn,
@@ -563,7 +563,8 @@ def _attn_materialized_bwd(qkvn, Pm, Pd, do, dqkv, dqk, B, N, C, Hn, hd, Np, Z, 
 class _EncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, tok, geo, e, dt, rng, *params):
-        B, N = geo
+        B, N = geo[:2]
+        mask = geo[2] if len(geo) > 2 else None  # additive bias (EncoderLayer._mask_bias) + strides
         (n1g, n1b, wq, wk, wv, qg, qb, kg, kb, wo, n2g, n2b, w1, b1, w2, b2) = params
         C, Hn, hd = e.embedding_dim, e.n_head, e.head_dim
         T = B * N
@@ -604,14 +605,16 @@ class _EncoderFn(torch.autograd.Function):
         # attention (:289-298): S = QK^T, P = softmax(S / sqrt(hd)), Pd = dropout(P), O = Pd V
         Np = (N + 7) // 8 * 8
         Z = B * Hn
-        if sp.attn_train_applies(dt, N, hd):  # flash form: saves O and the row LSE only
+        if mask is None and sp.attn_train_applies(dt, N, hd):  # flash form: saves O and the row LSE only
             o = _empty((T, C), dt, dev)
             lse = _empty((Z * N,), torch.float32, dev)
             sp.attn_train_fwd(qkvn, o, lse, B, N, Hn, hd, 1.0 / math.sqrt(hd), p_att, seeds[0])
             Pm = Pd = None
-        else:  # bf16: operands cast to fp32 once (small / odd head dims only)
+        else:  # masked attention, fp32, or head dims the flash kernels do not take (bf16: operands cast to
+            # fp32 once; the mask enters the materialised softmax)
             qkva = qkvn if dt == torch.float32 else sp.cast(qkvn, torch.float32)
-            o, lse, Pm, Pd = _attn_materialized(qkva, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seeds[0])
+            mk = None if mask is None else (mask[0], mask[1], mask[2], Hn)
+            o, lse, Pm, Pd = _attn_materialized(qkva, B, N, C, Hn, hd, Np, Z, dt, dev, p_att, seeds[0], mask=mk)
 
         # x = x + drop_path1(dropout(o_proj(o)))                       (:300-303)
         zo = _linear(o, W_["wo"], None, dt)
@@ -936,10 +939,13 @@ class _ToTokFn(torch.autograd.Function):
         return dx, dreg, None
 
 
-def _no_mask(mask):
-    if mask is not None:
-        raise NotImplementedError("sdpnet training path: attention masks are not supported in train mode "
-                                  "(MainModel never passes one, model.py:129-149)")
+def _enc_geo(e, B: int, N: int, mask):
+    """(B, N) or (B, N, (bias, batch stride, head stride)): a mask takes the materialised attention
+    (layers.py:289-298: SDPA attn_mask semantics for fast_att, masked_fill(mask == 0, -inf) for the
+    manual path, via EncoderLayer._mask_bias as in eval)."""
+    if mask is None:
+        return (B, N)
+    return (B, N, e._mask_bias(mask, B, N))
 
 
 def train_conv_mixer(m, x: torch.Tensor) -> torch.Tensor:
@@ -953,17 +959,15 @@ def train_conv_mixer(m, x: torch.Tensor) -> torch.Tensor:
 
 def train_encoder(e, x: torch.Tensor, reg: torch.Tensor, mask=None):
     """EncoderLayer.forward in train mode (layers.py:268-316): (x, registers) -> (x, registers)."""
-    _no_mask(mask)
     dt = compute_dtype(x, e)
     B, C, H, W = x.shape
     tok = _ToTokFn.apply(x, reg, stream_dtype(dt, C))
-    tok = _EncoderFn.apply(tok, (B, reg.shape[1] + H * W), e, dt, _RNG(), *_enc_params(e))
+    tok = _EncoderFn.apply(tok, _enc_geo(e, B, reg.shape[1] + H * W, mask), e, dt, _RNG(), *_enc_params(e))
     return _RawOutFn.apply(tok, (B, reg.shape[1], H, W, C))
 
 
 def train_block(blk, x: torch.Tensor, reg: torch.Tensor, mask=None):
     """Block.forward in train mode (layers.py:381-386), one token buffer for the whole block."""
-    _no_mask(mask)
     dt = compute_dtype(x, blk)
     B, C, H, W = x.shape
     R = reg.shape[1]
@@ -976,7 +980,8 @@ def train_block(blk, x: torch.Tensor, reg: torch.Tensor, mask=None):
         return t
 
     def enc(t):
-        return _EncoderFn.apply(t, (B, R + H * W), blk.t_block, dt, rng, *_enc_params(blk.t_block))
+        return _EncoderFn.apply(t, _enc_geo(blk.t_block, B, R + H * W, mask), blk.t_block, dt, rng,
+                                *_enc_params(blk.t_block))
 
     tok = enc(mixers(tok)) if blk.conv_first else mixers(enc(tok))
     return _RawOutFn.apply(tok, (B, R, H, W, C))
@@ -1292,6 +1297,124 @@ def tape_backward(tape, dlogits: torch.Tensor, params: List[torch.Tensor]) -> Li
             t = t.clone()
         out.append(t)
     return out
+
+
+# ---------------------------------------------------------------------------
+# Per-sub-layer form for torch.compile (sdpnet_ops.train_layer / train_layer_backward): one
+# opaque op per patch-embedding / ConvMixer / EncoderLayer / head, each with its own autograd
+# formula, so a compiled backward is a chain of per-layer ops and DDP's bucket hooks (and
+# Dynamo's DDPOptimizer graph splits) see each layer's gradients as soon as its backward op
+# returns -- the overlap the eager Functions give (training_tools.py:36-39 compiles DDP(model)).
+# The forward session (seed source, prepared bf16 weights, geometry) lives on the model between
+# the first and the last layer op of one forward; same Functions, same kernels, same RNG draws
+# in the same order as train_forward, so the compiled step is bit-identical to the eager one.
+# ---------------------------------------------------------------------------
+def train_layers(model):
+    """The sub-layers of a training forward in execution order: (kind, module)."""
+    out = [("embed", model)]
+    for blk in model.blocks:                                           # model.py:139-140
+        mx = [("mixer", m) for m in blk.conv_blocks]
+        en = [("enc", blk.t_block)]
+        out += (mx + en) if blk.conv_first else (en + mx)
+    out += [("enc", model.final_block.t_block), ("head", model.output_head)]
+    return out
+
+
+def layer_params(model, kind: str, mod) -> List[Optional[nn.Parameter]]:
+    if kind == "embed":
+        emb = model.embedding_layer
+        conv_emb = not hasattr(emb, "horizontal_embedding_layer")
+        eh = None if conv_emb else emb.horizontal_embedding_layer.weight
+        ew = None if conv_emb else emb.vertical_embedding_layer.weight
+        return [model.conv_init.conv.weight, eh, ew, emb.register_embedding_layer.weight]
+    if kind == "mixer":
+        return _mixer_params(mod)
+    if kind == "enc":
+        return _enc_params(mod)
+    return _head_params(mod)
+
+
+class _Session:
+    pass
+
+
+def layer_forward(model, layer: int, t: torch.Tensor, num_registers: int, dt):
+    """Forward of sub-layer ``layer`` (train_layers order) with its ctx returned for the
+    backward op.  Layer 0 takes the image and opens the session, the last layer closes it."""
+    global _WPREP
+    kind, mod = train_layers(model)[layer]
+    params = layer_params(model, kind, mod)
+    ctx = _Ctx()
+    if kind == "embed":
+        S = _Session()
+        B, _, Hi, Wi = t.shape
+        p = model.conv_init.patch_size
+        Hp, Wp = Hi // p, Wi // p
+        emb = model.embedding_layer
+        conv_emb = not hasattr(emb, "horizontal_embedding_layer")
+        R = num_reg_rows(emb.register.shape[0] if conv_emb else emb.max_num_registers, num_registers)
+        if not conv_emb:
+            eh, ew = emb.horizontal_embedding_layer.weight, emb.vertical_embedding_layer.weight
+            if Hp > eh.shape[0] or Wp > ew.shape[0]:
+                raise RuntimeError(f"image grid {Hp}x{Wp} exceeds max_image_size {[ew.shape[0], eh.shape[0]]}")
+        S.geo = (B, R, Hp, Wp, Hp * Wp + R, model.conv_init.conv.out_channels)
+        S.dt = dt
+        _WPREP = _prep_weights(model, dt)
+        S.wprep = _WPREP
+        S.rng = _RNG()
+        model._sdp_session = S
+        C = S.geo[5]
+        xin = t if t.dtype == dt else as_dtype(t, dt)
+        with torch.no_grad():
+            out = _EmbedFn.forward(ctx, xin, (B, R, Hp, Wp, num_registers, stream_dtype(dt, C)), model, dt, *params)
+        return out, (_EmbedFn, ctx, 4, params)
+    S = getattr(model, "_sdp_session", None)
+    if S is None:
+        raise RuntimeError("sdpnet: training layer op run outside a forward (layer 0 opens it)")
+    B, R, Hp, Wp, N, C = S.geo
+    _WPREP = S.wprep
+    try:
+        with torch.no_grad():
+            if kind == "mixer":
+                out = _MixerFn.forward(ctx, t, (B, R, Hp, Wp), mod, S.dt, *params)
+                rec = (_MixerFn, ctx, 4, params)
+            elif kind == "enc":
+                out = _EncoderFn.forward(ctx, t, (B, N), mod, S.dt, S.rng, *params)
+                rec = (_EncoderFn, ctx, 5, params)
+            else:
+                out = _HeadFn.forward(ctx, t, (B, R, Hp * Wp, N, C), mod, S.dt, S.rng, *params)
+                rec = (_HeadFn, ctx, 5, params)
+    finally:
+        _WPREP = None
+    if kind == "head":
+        model._sdp_session = None
+    return out, rec
+
+
+def layer_backward(rec, g: torch.Tensor):
+    """(grad of the layer's input or None, one fp32 gradient per non-None parameter)."""
+    fn, ctx, lead, params = rec
+    with torch.no_grad():
+        outs = fn.backward(ctx, g.contiguous())
+    grads = []
+    for prm, gp in zip(params, outs[lead:]):
+        if prm is None:
+            continue
+        t = gp.reshape(prm.shape).to(prm.dtype) if gp is not None else torch.zeros_like(prm)
+        if t._base is not None:  # e.g. the q/k/v slices of one fused dW: op outputs may not alias
+            t = t.clone()
+        grads.append(t)
+    return (outs[0] if fn is not _EmbedFn else None), grads
+
+
+def compiled_train_forward(model, x: torch.Tensor, num_registers: int, dtype_code: int) -> torch.Tensor:
+    """The training forward as a chain of sdpnet::train_layer ops (traced by Dynamo)."""
+    t = x
+    B = x.shape[0]
+    for i, (kind, mod) in enumerate(train_layers(model)):
+        params = [q for q in layer_params(model, kind, mod) if q is not None]
+        t, _ = torch.ops.sdpnet.train_layer(t, params, model._sdp_handle, i, num_registers, dtype_code, B)
+    return t
 
 
 # ---------------------------------------------------------------------------

@@ -87,8 +87,55 @@ def test_encoder_layer_train_mode_matches_oracle_autograd(fast):
     xc, rc = _leaf(x), _leaf(r)
     ox, orr = orc.encoder_layer(xc, rc, osd, "", 4, "gelu", True, fast)
     _check(enc, [yx, yr], [ox, orr], osd, "", [xd, rd], [xc, rc])
-    with pytest.raises(NotImplementedError, match="mask"):
-        enc(xd, rd, torch.ones(18, 18, device=DEV))
+
+
+@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("bshape", [(3, 1), (1, 4)])
+def test_encoder_layer_train_mode_with_mask_matches_oracle_autograd(fast, bshape):
+    """A masked EncoderLayer in train mode (layers.py:289-298): SDPA attn_mask semantics (bool,
+    True = attend) on the fast path, masked_fill(mask == 0, -inf) on the manual path, broadcast
+    over batch or heads; the masked route is the materialised softmax.  Outputs and every
+    parameter / input gradient against oracle autograd."""
+    from layers import EncoderLayer
+    enc = EncoderLayer(64, n_head=4, fast_att=fast, activation_func=nn.GELU(), ff_dropout=0.0, att_dropout=0.0,
+                       drop_p=0.0)
+    osd = _sd(enc, 9)
+    enc = enc.to(DEV).train()
+    g = torch.Generator().manual_seed(12)
+    x, r = torch.randn(3, 64, 4, 4, generator=g), torch.randn(3, 2, 64, generator=g)
+    N = 18
+    keep = torch.rand(*bshape, N, N, generator=g) > 0.35
+    keep[..., 0] = True  # every query keeps one key (a fully masked row is NaN on both sides)
+    mask = keep if fast else keep.float()
+    xd, rd = _leaf(x.to(DEV)), _leaf(r.to(DEV))
+    yx, yr = enc(xd, rd, mask.to(DEV))
+    xc, rc = _leaf(x), _leaf(r)
+    ox, orr = orc.encoder_layer(xc, rc, osd, "", 4, "gelu", True, fast, mask)
+    _check(enc, [yx, yr], [ox, orr], osd, "", [xd, rd], [xc, rc])
+
+
+def test_masked_encoder_layer_dropout_on_attention_weights():
+    """Manual path (fast_att=False) in train mode with a mask and dropout: the attention weights
+    are dropped with the layer's dropout p (layers.py:297), so two seeds give different outputs,
+    the same seed the same output, and the backward stays finite."""
+    from layers import EncoderLayer
+    enc = EncoderLayer(64, n_head=4, fast_att=False, activation_func=nn.GELU(), ff_dropout=0.3, att_dropout=0.0,
+                       drop_p=0.0).to(DEV).train()
+    g = torch.Generator().manual_seed(13)
+    x, r = torch.randn(2, 64, 4, 4, generator=g).to(DEV), torch.randn(2, 2, 64, generator=g).to(DEV)
+    mask = (torch.rand(18, 18, generator=g) > 0.3).float().to(DEV)
+    mask[:, 0] = 1
+    outs = []
+    for seed in (1, 1, 2):
+        torch.manual_seed(seed)
+        xd = x.clone().requires_grad_(True)
+        yx, yr = enc(xd, r, mask)
+        (yx.float().square().sum() + yr.float().sum()).backward()
+        assert torch.isfinite(xd.grad).all()
+        assert all(torch.isfinite(p.grad).all() for p in enc.parameters() if p.grad is not None)
+        outs.append(yx.detach().clone())
+        enc.zero_grad(set_to_none=True)
+    assert torch.equal(outs[0], outs[1]) and not torch.equal(outs[0], outs[2])
 
 
 def test_conv_mixer_and_layernorm_train_mode_match_oracle_autograd():

@@ -25,13 +25,15 @@ def main(path):
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r["Queue_Id"])
                 for r in rows)
     pats = [e for e in ev if "patchify" in e[2]]
-    # a two-stream forward starts with a patchify on each queue within 1 ms; take the last
-    # window between two consecutive such forward starts
-    paired = [p for p in pats if any(o[3] != p[3] and abs(o[0] - p[0]) < 1_000_000 for o in pats)]
-    q0 = paired[-1][3] if paired else pats[-1][3]
-    fwd = sorted(p[0] for p in (paired or pats) if p[3] == q0)
-    # the timed replays are back to back: take the middle window among those of typical length
-    # (the last forward of bench.py is the eager event pass behind a sleep)
+    # one forward per sub-batch stream per step, each stream's chain starting with a patchify;
+    # graph replays run back to back, so the two streams' chains need not start together.  The
+    # timed replays are the longest sequence on one queue: windows = its consecutive patchify
+    # starts (one step each), all queues' kernels inside a window are analysed.
+    byq = collections.defaultdict(list)
+    for p in pats:
+        byq[p[3]].append(p[0])
+    q0 = max(byq, key=lambda q: len(byq[q]))
+    fwd = sorted(byq[q0])
     wins = [(fwd[i], fwd[i + 1]) for i in range(len(fwd) - 1)]
     lens = sorted(b_ - a_ for a_, b_ in wins)
     med = lens[len(lens) // 2]
