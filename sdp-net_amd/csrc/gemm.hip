@@ -810,6 +810,9 @@ typedef __attribute__((ext_vector_type(4))) int i32x4;
 // workgroup events, 64 per workgroup; stamp = event code << 56 | s_memrealtime (100 MHz).
 __device__ unsigned long long g_gemm_stamps[8192 * 64];
 __device__ int g_gemm_dephase;  // experiment: first-round workgroup b waits ((b >> 3) & 3) * this many 10-ns ticks
+// phase timeline of workgroup 0: waves 0 (group 0) and 4 (group 1), s_memtime (shader clock) at
+// each MFMA section's start (after its barrier + lgkmcnt wait) and after its last MFMA issue
+__device__ unsigned long long g_phase_stamps[2 * 64];
 #define SDP_STAMP(code)                                                                            \
   do {                                                                                             \
     if (tid == 0 && nstamp < 64)                                                                   \
@@ -1023,14 +1026,25 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
           acc[in * 2 + i][jm * 4 + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i * 2 + ks], xf[j * 2 + ks], acc[in * 2 + i][jm * 4 + j], 0, 0, 0);
   };
+#ifdef SDP_GEMM_STAMPS
+  int pst = 0;
+  auto pstamp = [&]() {
+    if (b == 0 && (wave & 3) == 0 && lane == 0 && pst < 64)
+      g_phase_stamps[(wave >> 2) * 64 + pst++] = __builtin_amdgcn_s_memtime();
+  };
+#else
+  auto pstamp = [&]() {};
+#endif
   auto mfma_section = [&](auto&& body) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    pstamp();
     __builtin_amdgcn_s_setprio(1);
     body();
     __builtin_amdgcn_s_setprio(0);
+    pstamp();
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -1349,6 +1363,11 @@ extern "C" int sdp_gemm_sk_status(void* stream, unsigned* out) {
 }
 
 #ifdef SDP_GEMM_STAMPS
+extern "C" int sdp_gemm_phase_stamps(void* dst) {
+  hipError_t rc = hipDeviceSynchronize();
+  if (rc == hipSuccess) rc = hipMemcpyFromSymbol(dst, HIP_SYMBOL(fast::g_phase_stamps), sizeof(fast::g_phase_stamps));
+  return (int)rc;
+}
 extern "C" int sdp_gemm_set_dephase(int ticks) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(fast::g_gemm_dephase), &ticks, sizeof(int));
 }
