@@ -113,6 +113,11 @@ int sdp_gemm_set_epi_spec(int on);
 int sdp_gemm_set_timeline(void* buf, int slots);
 int sdp_gemm_timeline_count(void);
 
+/* Timing experiments only: bit 0 makes sdp_dwconv, bit 1 sdp_attention, bit 2 sdp_ln_stats return
+ * without launching (results WRONG) -- bounds what a faster kernel could give the step.  Default 0.
+ * Returns the previous mask. */
+int sdp_debug_skip(int mask);
+
 /* Tile raster of the 8-phase GEMM: M-blocks per group (consecutive blocks walk a group of
  * gm M-blocks before the next N-tile).  1 = row-major, -1 = auto (8 when N spans >= 12
  * tiles, else 1).  Results do not depend on it.  Returns the previous value. */

@@ -431,3 +431,14 @@ extern "C" int sdp_stream_create_cu_mask(int part, int nparts, int interleave, v
   *out = (void*)s;
   return 0;
 }
+
+
+// Timing experiments only (tools/r4_skip.sh): bit 0 skips sdp_dwconv, bit 1 sdp_attention, bit 2
+// sdp_ln_stats -- the results are then WRONG; it bounds what a faster kernel could give the step.
+// 0 (default) skips nothing.  Returns the previous mask.
+int g_sdp_debug_skip = 0;
+extern "C" int sdp_debug_skip(int mask) {
+  const int old = g_sdp_debug_skip;
+  g_sdp_debug_skip = mask;
+  return old;
+}

@@ -42,6 +42,7 @@ _SIGS = {
     "sdp_gemm_set_epi_spec": ([_i32], _i32),
     "sdp_gemm_set_timeline": ([_vp, _i32], _i32),
     "sdp_gemm_timeline_count": ([], _i32),
+    "sdp_debug_skip": ([_i32], _i32),
     "sdp_gemm_set_group_m": ([_i32], _i32),
     "sdp_gemm_set_exact_gelu": ([_i32], _i32),
     "sdp_gemm_workspace_bytes": ([], _i64),
@@ -179,6 +180,9 @@ def lib():
         kern = os.environ.get("SDPNET_GEMM_EPI_SPEC")  # compile-time-flag GEMM epilogues (1 default)
         if kern:
             L.sdp_gemm_set_epi_spec(int(kern))
+        kern = os.environ.get("SDPNET_DEBUG_SKIP")  # timing experiments only: skip kernels (wrong results)
+        if kern:
+            L.sdp_debug_skip(int(kern))
         kern = os.environ.get("SDPNET_GEMM_GROUP_M")  # tile raster of the 8-phase GEMM (-1 auto, 1 row-major)
         if kern:
             L.sdp_gemm_set_group_m(int(kern))
