@@ -102,6 +102,11 @@ int sdp_gemm_set_store_policy(int nt);
  * bit-identical; the emitted LN partials agree to fp32 rounding.  Returns the previous value. */
 int sdp_gemm_set_epi_spec(int on);
 
+/* Phases per K-tile of the fast GEMM's data-parallel main loop: 2 (default, 32 MFMAs per
+ * wave-group section, half the group-to-group hand-overs) or 4 (16 MFMAs per section).  Same
+ * arithmetic order, bit-identical outputs.  Returns the previous value. */
+int sdp_gemm_set_kloop_phases(int n);
+
 /* Launch timeline of the bf16 fast GEMM (measurement only; bench.py's roofline inside a replayed
  * HIP graph, where events cannot be recorded).  sdp_gemm_set_timeline(buf, slots): while buf
  * (device memory, 2 x u64 per slot, caller-initialised to {UINT64_MAX, 0}) is set, fast-GEMM

@@ -824,7 +824,9 @@ __device__ unsigned long long g_phase_stamps[2 * 64];
 #endif
 
 // EPI: 1 = permlane-paired register epilogue, 4 = whole-line LDS-staged epilogue.
-template <int ACT, int EPI, bool SK>
+// PH2 = true: the same K-tile in 2 phases of 32 MFMAs per wave group instead of 4 of 16 (half the
+// group-to-group hand-overs; see the k-loop below).
+template <int ACT, int EPI, bool SK, bool PH2 = false>
 __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
                                                          const bf16_t* __restrict__ W, int64_t ldw, Epi<bf16_t> epi,
                                                          int M, int N, int K, int tiles_m, int tiles_n, SkArgs sk) {
@@ -1050,6 +1052,49 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  if constexpr (PH2) {
+    // 2 phases per K-tile: P0 = Q(m0, n0) + Q(m0, n1) (reads w0, w1, xf(m-half 0)), P1 = Q(m1, n1) +
+    // Q(m1, n0) (reads xf(m-half 1)), 32 MFMAs per section.  A wave retires its fragment reads
+    // (lgkmcnt(0)) BEFORE the section's first barrier, so a region read in phase p may be
+    // re-staged from phase p + 1.  Schedule (tile t): P0 issues S3(t+1), P1 issues S1(t+2) S2(t+2);
+    // P0 waits vmcnt(8) = retires S3(t) (read in P1), P1 waits vmcnt(8) = retires S1(t+1) S2(t+1)
+    // (read in P0 of t+1): two phases (~one K-tile of MFMA) between issue and retirement.
+    auto section = [&](auto&& body) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      pstamp();
+      __builtin_amdgcn_s_setprio(1);
+      body();
+      __builtin_amdgcn_s_setprio(0);
+      pstamp();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    S1(0); S2(0); S3(0);
+    if (kn > 1) { S1(1); S2(1); SDP_VMCNT(8); }
+    else SDP_VMCNT(2);
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one barrier
+    SDP_STAMP(4);
+    __builtin_amdgcn_sched_barrier(0);
+    for (int t = 0; t < kn; ++t) {
+      const char* xt = smem + (t & 1) * BUF8;
+      const char* wt = xt + TILE_BYTES;
+      const bool more1 = t + 1 < kn, more2 = t + 2 < kn;
+      read_w(wt, 0, w0);
+      read_w(wt, 1, w1);
+      read_x(xt, 0);
+      if (more1) { S3(t + 1); SDP_VMCNT(8); } else SDP_VMCNT(0);
+      section([&] { quad(0, 0, w0); quad(0, 1, w1); });
+      read_x(xt, 1);
+      if (more2) { S1(t + 2); S2(t + 2); SDP_VMCNT(8); }
+      else if (more1) SDP_VMCNT(2);
+      section([&] { quad(1, 1, w1); quad(1, 0, w0); });
+    }
+  } else {
   // prologue: S1(0) S2(0) S3(0) [S1(1) S2(1)]; retire S1(0)
   S1(0); S2(0); S3(0);
   if (kn > 1) { S1(1); S2(1); SDP_VMCNT(10); }
@@ -1081,6 +1126,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     else if (more1) SDP_VMCNT(4);
     mfma_section([&] { quad(1, 0, w0); });
   }
+  }  // !PH2
   if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
   SDP_STAMP(5);
   if (SK && mode == SEG_HEAD) {
@@ -1275,6 +1321,16 @@ static unsigned long long* tl_take() {
   std::lock_guard<std::mutex> lk(g_tl_mu);
   if (!g_tl_buf || g_tl_next >= g_tl_slots) return nullptr;
   return g_tl_buf + 2 * (g_tl_next++);
+}
+
+// Phases per K-tile of the 8-phase kernel's main loop: 2 (default: 32 MFMAs per wave-group section,
+// half the group-to-group hand-overs: 3.2k vs 4.3k cycles per K-tile, profiles/r04_gemm_ph2.md) or
+// 4 (16 MFMAs per section).  Data-parallel schedule only (stream-K segments keep 4).
+static int g_kloop_phases = 2;
+extern "C" int sdp_gemm_set_kloop_phases(int n) {
+  const int old = g_kloop_phases;
+  if (n == 2 || n == 4) g_kloop_phases = n;
+  return old;
 }
 
 // 1 (default): the model's epilogue flag combinations take tile_epilogue_fl; 0: the run-time
@@ -1522,6 +1578,9 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
     if (ws)                                                                                                         \
       hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, true>), dim3(sk.G), dim3(fast::NTHREADS), 0, s,                 \
                          (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);                 \
+    else if (g_kloop_phases == 2)                                                                                   \
+      hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false, true>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,       \
+                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);                 \
     else                                                                                                            \
       hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,             \
                          (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);                 \
@@ -1548,8 +1607,14 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
                          fl == (fast::EF_BIAS | fast::EF_RESID | fast::EF_PART));
       if (spec) {
 #define SDP_8PH_DP(A, E)                                                                                   \
-  hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,        \
-                     (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk)
+  do {                                                                                                      \
+    if (g_kloop_phases == 2)                                                                                \
+      hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false, true>), dim3(tm * tn), dim3(fast::NTHREADS), 0, \
+                         s, (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);      \
+    else                                                                                                    \
+      hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,    \
+                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);        \
+  } while (0)
 #define SDP_8PH_FL(A)                                                           \
   do {                                                                          \
     if (fl == (fast::EF_BIAS | fast::EF_LN)) SDP_8PH_DP(A, 16 + 3);             \

@@ -40,6 +40,7 @@ _SIGS = {
     "sdp_gemm_set_fast_kernel": ([_i32], _i32),
     "sdp_gemm_set_store_policy": ([_i32], _i32),
     "sdp_gemm_set_epi_spec": ([_i32], _i32),
+    "sdp_gemm_set_kloop_phases": ([_i32], _i32),
     "sdp_gemm_set_timeline": ([_vp, _i32], _i32),
     "sdp_gemm_timeline_count": ([], _i32),
     "sdp_debug_skip": ([_i32], _i32),
@@ -180,6 +181,9 @@ def lib():
         kern = os.environ.get("SDPNET_GEMM_EPI_SPEC")  # compile-time-flag GEMM epilogues (1 default)
         if kern:
             L.sdp_gemm_set_epi_spec(int(kern))
+        kern = os.environ.get("SDPNET_GEMM_KLOOP_PHASES")  # 2 (default) or 4 phases per K-tile
+        if kern:
+            L.sdp_gemm_set_kloop_phases(int(kern))
         kern = os.environ.get("SDPNET_DEBUG_SKIP")  # timing experiments only: skip kernels (wrong results)
         if kern:
             L.sdp_debug_skip(int(kern))

@@ -516,6 +516,40 @@ def test_gemm_specialised_epilogue_bit_identical(act, combo, M, N, K):
         close(p1[:, R:, :, 1], p0[:, R:, :, 1], torch.float32, rel=1e-4, what="partial M2")
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(512, 256, 64), (700, 320, 128), (1536, 768, 192), (2048, 512, 768),
+                                   (1000, 2304, 3072)])
+def test_gemm_kloop_phases_bit_identical(spec, M, N, K):
+    """The 2-phase main loop (sdp_gemm_set_kloop_phases(2), the default) runs the MFMAs in the
+    4-phase loop's accumulation order: outputs are bit-identical for 1, 2, 3 and many K-tiles,
+    ragged M / N, through the run-time and the compile-time-flag epilogues."""
+    x = rnd(M, K, dtype=BF, seed=91)
+    w = rnd(N, K, dtype=BF, seed=92, scale=0.05)
+    b = rnd(N, seed=93)
+    r = rnd(M, N, dtype=BF, seed=94)
+    outs = []
+    old_spec = sp.lib().sdp_gemm_set_epi_spec(spec)
+    try:
+        for ph in (4, 2):
+            old = sp.lib().sdp_gemm_set_kloop_phases(ph)
+            try:
+                y = torch.empty(M, N, dtype=BF, device=DEV)
+                part = torch.empty(M, N // 64, 2, device=DEV) if N % 64 == 0 else None
+                sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, bias=b, resid=sp.dense(r), act=1, part=part)
+                torch.cuda.synchronize()
+                outs.append((y, part))
+            finally:
+                sp.lib().sdp_gemm_set_kloop_phases(old)
+    finally:
+        sp.lib().sdp_gemm_set_epi_spec(old_spec)
+    assert torch.equal(outs[0][0], outs[1][0]), "2-phase main loop output differs"
+    if outs[0][1] is not None:
+        assert torch.equal(outs[0][1], outs[1][1]), "2-phase main loop LN partials differ"
+    ref = F.gelu(x.float() @ w.float().t() + b) + r.float()
+    close(outs[1][0], ref, BF, what="2-phase GEMM vs fp32")
+
+
 # ------------------------------------------------- stream-K schedule of the 8-phase GEMM
 def _gemm_both_schedules(run):
     """run() -> output tensor; returns (data-parallel result, stream-K result)."""

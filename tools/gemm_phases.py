@@ -49,18 +49,19 @@ def main():
         buf = np.zeros(128, dtype=np.uint64)
         assert L.sdp_gemm_phase_stamps(buf.ctypes.data) == 0
         st = buf.reshape(2, 64).astype(np.int64)
+        nph = int(os.environ.get("SDPNET_GEMM_KLOOP_PHASES", "4"))  # MFMA sections per K-tile
         t0 = min(st[0, 0], st[1, 0])
         st = st - t0
         print(f"{name} M={M} N={N} K={K}  (cycles from group 0's first MFMA section)")
         print("  kt ph | g0 start  len | g1 start  len | g0end->g1start  g1end->g0next")
-        for i in range(32):
-            kt, ph = divmod(i, 4)
+        for i in range(8 * nph):
+            kt, ph = divmod(i, nph)
             a0, e0 = st[0, 2 * i], st[0, 2 * i + 1]
             a1, e1 = st[1, 2 * i], st[1, 2 * i + 1]
-            nx = st[0, 2 * i + 2] if i < 31 else e1
+            nx = st[0, 2 * i + 2] if i < 8 * nph - 1 else e1
             print(f"  {kt:2d} {ph:2d} | {a0:8d} {e0 - a0:4d} | {a1:8d} {e1 - a1:4d} | {a1 - e0:8d} {nx - e1:12d}")
-        per = (st[0, 2 * 28] - st[0, 2 * 4]) / 24
-        print(f"  mean cycles per phase (both groups' sections) over K-tiles 1..6: {per:.0f} (MFMA floor 512)")
+        per = (st[0, 2 * 7 * nph] - st[0, 2 * nph]) / 6
+        print(f"  mean cycles per K-tile (both groups' sections) over K-tiles 1..6: {per:.0f} (MFMA floor 2048)")
 
 
 if __name__ == "__main__":
