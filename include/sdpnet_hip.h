@@ -104,7 +104,8 @@ int sdp_gemm_set_epi_spec(int on);
 
 /* Phases per K-tile of the fast GEMM's data-parallel main loop: 2 (default, 32 MFMAs per
  * wave-group section, half the group-to-group hand-overs) or 4 (16 MFMAs per section).  Same
- * arithmetic order, bit-identical outputs.  Returns the previous value. */
+ * arithmetic order, bit-identical outputs.  Also selects the weight-gradient kernel's loop
+ * (sdp_gemm_wgrad).  Returns the previous value; any other n only queries it. */
 int sdp_gemm_set_kloop_phases(int n);
 
 /* Launch timeline of the bf16 fast GEMM (measurement only; bench.py's roofline inside a replayed

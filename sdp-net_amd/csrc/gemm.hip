@@ -812,7 +812,7 @@ __device__ unsigned long long g_gemm_stamps[8192 * 64];
 __device__ int g_gemm_dephase;  // experiment: first-round workgroup b waits ((b >> 3) & 3) * this many 10-ns ticks
 // phase timeline of workgroup 0: waves 0 (group 0) and 4 (group 1), s_memtime (shader clock) at
 // each MFMA section's start (after its barrier + lgkmcnt wait) and after its last MFMA issue
-__device__ unsigned long long g_phase_stamps[2 * 64];
+__device__ unsigned long long g_phase_stamps[2 * 2 * 64];  // [s_memtime x 2 groups][s_memrealtime x 2 groups]
 #define SDP_STAMP(code)                                                                            \
   do {                                                                                             \
     if (tid == 0 && nstamp < 64)                                                                   \
@@ -1032,7 +1032,11 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   int pst = 0;
   auto pstamp = [&]() {
     if (b == 0 && (wave & 3) == 0 && lane == 0 && pst < 64)
-      g_phase_stamps[(wave >> 2) * 64 + pst++] = __builtin_amdgcn_s_memtime();
+    {
+      g_phase_stamps[(wave >> 2) * 64 + pst] = __builtin_amdgcn_s_memtime();
+      if (pst == 0 || pst == 31) g_phase_stamps[128 + (wave >> 2) * 64 + pst] = __builtin_amdgcn_s_memrealtime();
+      ++pst;
+    }
   };
 #else
   auto pstamp = [&]() {};

@@ -34,6 +34,7 @@ typedef short v4i16 __attribute__((ext_vector_type(4)));
 
 #define SDP_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
+template <bool PH2>
 __global__ __launch_bounds__(NTHREADS) void gemm_wgrad_8ph(const bf16_t* __restrict__ A, int64_t lda,
                                                          const bf16_t* __restrict__ B, int64_t ldb,
                                                          float* __restrict__ C, int64_t ldc, int64_t split_stride,
@@ -174,6 +175,43 @@ __global__ __launch_bounds__(NTHREADS) void gemm_wgrad_8ph(const bf16_t* __restr
       __builtin_amdgcn_sched_barrier(0);
     };
 
+    if constexpr (PH2) {
+      // 2 phases per K-tile (32 MFMAs per section): the schedule and retire counts of
+      // gemm_bf16_8ph's 2-phase loop (csrc/gemm.hip), which reads its staged regions in the same
+      // phases (w0, w1, x half 0 in P0; x half 1 in P1)
+      auto section = [&](auto&& body) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        body();
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      S1(0); S2(0); S3(0);
+      if (kn > 1) { S1(1); S2(1); SDP_VMCNT(8); }
+      else SDP_VMCNT(2);
+      __builtin_amdgcn_s_barrier();
+      if (wm == 1) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      for (int t = 0; t < kn; ++t) {
+        const char* buf = smem + (t & 1) * BUF;
+        const bool more1 = t + 1 < kn, more2 = t + 2 < kn;
+        read_w(buf, 0, w0);
+        read_w(buf, 1, w1);
+        read_x(buf, 0);
+        if (more1) { S3(t + 1); SDP_VMCNT(8); } else SDP_VMCNT(0);
+        section([&] { quad(0, 0, w0); quad(0, 1, w1); });
+        read_x(buf, 1);
+        if (more2) { S1(t + 2); S2(t + 2); SDP_VMCNT(8); }
+        else if (more1) SDP_VMCNT(2);
+        section([&] { quad(1, 1, w1); quad(1, 0, w0); });
+      }
+      if (wm == 0) __builtin_amdgcn_s_barrier();
+    } else {
     // prologue / schedule / retire counts exactly as gemm_bf16_8ph (same pieces per sub-stage)
     S1(0); S2(0); S3(0);
     if (kn > 1) { S1(1); S2(1); SDP_VMCNT(10); }
@@ -200,6 +238,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_wgrad_8ph(const bf16_t* __restr
       mfma_section([&] { quad(1, 0, w0); });
     }
     if (wm == 0) __builtin_amdgcn_s_barrier();
+    }  // !PH2
   }
 
   // ---- fp32 epilogue: D[j][i] per 16x16 block, lane (fr, fq) holds j = 4 fq + r, i = fr:
@@ -231,9 +270,15 @@ extern "C" int sdp_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t
   const int ti = ni / wg::BM, tj = nj / wg::BN;
   const int64_t nwg = (int64_t)ti * tj * splits;
   if (nwg > (1 << 30)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(wg::gemm_wgrad_8ph, dim3((unsigned)nwg), dim3(wg::NTHREADS), 0, (hipStream_t)stream,
-                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, split_stride, ti, tj, nkt, kchunk_tiles,
-                     ktok, (const bf16_t*)zrow);
+  // the main-loop phase count follows the forward GEMM's (sdp_gemm_set_kloop_phases; 0 = query)
+  if (sdp_gemm_set_kloop_phases(0) == 2)
+    hipLaunchKernelGGL(wg::gemm_wgrad_8ph<true>, dim3((unsigned)nwg), dim3(wg::NTHREADS), 0, (hipStream_t)stream,
+                       (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, split_stride, ti, tj, nkt, kchunk_tiles,
+                       ktok, (const bf16_t*)zrow);
+  else
+    hipLaunchKernelGGL(wg::gemm_wgrad_8ph<false>, dim3((unsigned)nwg), dim3(wg::NTHREADS), 0, (hipStream_t)stream,
+                       (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, split_stride, ti, tj, nkt, kchunk_tiles,
+                       ktok, (const bf16_t*)zrow);
   return SDP_CHECK_LAUNCH();
 }
 

@@ -233,6 +233,26 @@ def test_gemm_wgrad_8ph(N, K, M, kchunk):
     close(slabs.sum(0), dy.float().t() @ x.float(), 1e-5, "wgrad sum")
 
 
+@pytest.mark.parametrize("N,K,M,kchunk", [(256, 256, 64, 1), (256, 512, 640, 3), (768, 768, 30720, 18),
+                                          (256, 256, 37, 1), (768, 512, 4136, 5)])
+def test_gemm_wgrad_kloop_phases_bit_identical(N, K, M, kchunk):
+    # the 2-phase main loop (default) accumulates in the 4-phase loop's order: identical slabs
+    dy = rnd(M, N, seed=35, dtype=BF, scale=0.5)
+    x = rnd(M, K, seed=36, dtype=BF)
+    splits = -(-(-(-M // 64)) // kchunk)
+    outs = []
+    for ph in (4, 2):
+        old = sp.lib().sdp_gemm_set_kloop_phases(ph)
+        try:
+            slabs = torch.full((splits, N, K), float("nan"), device=DEV)
+            sp.gemm_wgrad(dy, x, slabs, M, kchunk, split_stride=N * K)
+            torch.cuda.synchronize()
+            outs.append(slabs)
+        finally:
+            sp.lib().sdp_gemm_set_kloop_phases(old)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_gemm_wgrad_8ph_strided_and_training_dispatch():
     import sdpnet_train as st
     # strided token rows (ld > N), a 40-token partial last K-tile, bit-reproducible

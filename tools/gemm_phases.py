@@ -3,7 +3,8 @@
   make -C sdp-net_amd/csrc stamps
   python tools/gemm_phases.py [--shapes mixer_down,enc_qkv]
 
-Workgroup 0's waves 0 (group 0) and 4 (group 1) stamp s_memtime (shader clock) at every MFMA
+Workgroup 0's waves 0 (group 0) and 4 (group 1) stamp s_memtime (shader clock) and s_memrealtime
+(100 MHz) at every MFMA
 section's start (after its barrier and lgkmcnt wait) and after its last MFMA issue, for the first
 8 K-tiles (stamps build, sdp-net_amd/lib_stamps; never loaded by the product).  Prints per phase
 of each K-tile: the MFMA section length of each group (16 MFMAs = 256 cycles of issue at one
@@ -46,10 +47,11 @@ def main():
             run()
         torch.cuda.synchronize()
         run()
-        buf = np.zeros(128, dtype=np.uint64)
+        buf = np.zeros(256, dtype=np.uint64)
         assert L.sdp_gemm_phase_stamps(buf.ctypes.data) == 0
-        st = buf.reshape(2, 64).astype(np.int64)
-        nph = int(os.environ.get("SDPNET_GEMM_KLOOP_PHASES", "4"))  # MFMA sections per K-tile
+        st = buf[:128].reshape(2, 64).astype(np.int64)
+        rt = buf[128:].reshape(2, 64).astype(np.int64)
+        nph = L.sdp_gemm_set_kloop_phases(0)  # MFMA sections per K-tile (0: query only)
         t0 = min(st[0, 0], st[1, 0])
         st = st - t0
         print(f"{name} M={M} N={N} K={K}  (cycles from group 0's first MFMA section)")
@@ -62,6 +64,9 @@ def main():
             print(f"  {kt:2d} {ph:2d} | {a0:8d} {e0 - a0:4d} | {a1:8d} {e1 - a1:4d} | {a1 - e0:8d} {nx - e1:12d}")
         per = (st[0, 2 * 7 * nph] - st[0, 2 * nph]) / 6
         print(f"  mean cycles per K-tile (both groups' sections) over K-tiles 1..6: {per:.0f} (MFMA floor 2048)")
+        last = 31  # the second s_memrealtime stamp
+        ghz = (st[0, last] - st[0, 0]) / max(1, rt[0, last] - rt[0, 0]) * 0.1  # s_memrealtime: 100 MHz
+        print(f"  shader clock over the 8 K-tiles (s_memtime / s_memrealtime): {ghz:.2f} GHz")
 
 
 if __name__ == "__main__":
