@@ -78,7 +78,7 @@ def flops_per_image(cfg, img=224, num_registers=3):
     return patch + cfg["num_blocks"] * (cfg["conv_block_num"] * mixer + enc) + enc + head
 
 
-def measured_traffic(kernel):
+def measured_traffic(kernel, config="m"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/r*_gemm_traffic.json, written by tools/prof_summary.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command,
@@ -90,7 +90,7 @@ def measured_traffic(kernel):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("kernel") == kernel:
+        if d.get("kernel") == kernel and d.get("config", "m") == config:
             return int(d["hbm_bytes_per_launch"]), os.path.relpath(f, REPO)
     return None, None
 
@@ -429,7 +429,7 @@ def main():
     achieved = fast_fl / (union_ms_step * 1e-3) / 1e12
     per_launch_tf = fast_fl / (fast_ms * 1e-3) / 1e12 if fast_ms else 0.0
     kname = FAST_GEMM_NAMES.get(sp.lib().sdp_gemm_set_fast_kernel(0), "?")
-    traffic, traffic_src = measured_traffic(kname) if args.config == "m" else (None, None)
+    traffic, traffic_src = measured_traffic(kname, args.config) if args.config in ("m", "xl") else (None, None)
     gf = flops_per_image(cfg) / 1e9
     tokens = (224 // cfg["patch_size"]) ** 2 + min(4, cfg["max_num_registers"])
     value = total_imgs / el

@@ -250,6 +250,9 @@ def _wprep(key, dt):
 
 
 _WGRAD_8PH = os.environ.get("SDPNET_WGRAD_8PH", "1") != "0"
+# workgroups per weight gradient (tiles x K splits): one per CU fills the chip when the dW runs
+# alone; fewer splits write fewer fp32 slabs while the dX GEMM shares the chip (A/B knob)
+_WGRAD_WGS = int(os.environ.get("SDPNET_WGRAD_WGS", "256"))
 # dropout of the encoder's output projections fused into the drop-path / residual pass (A/B knob)
 _DMODE = 1 if os.environ.get("SDPNET_FUSED_DROPOUT", "1") != "0" else 0
 
@@ -270,7 +273,7 @@ def _wgrad_8ph(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     K = x.shape[1]
     nkt = -(-M // 64)
     tiles = (N // 256) * (K // 256)
-    target = max(1, min(nkt, 256 // tiles))
+    target = max(1, min(nkt, _WGRAD_WGS // tiles))
     kchunk = -(-nkt // target)
     splits = -(-nkt // kchunk)
     dw = _empty((N, K), torch.float32, dy.device)

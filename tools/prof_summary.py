@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--cmd", default="bench.py --steps 3 --warmup 1 --no-graph --streams 1 --no-cpu-baseline "
                                      "--prof-steps 1", help="the profiled bench.py arguments (for the summary text)")
     ap.add_argument("--graph", action="store_true", help="the profiled command replays the 2-stream HIP graph")
+    ap.add_argument("--config", default="m", help="bench.py --config of the profiled command (m, xl)")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
 
@@ -94,7 +95,8 @@ def main():
     fetch = pmc_per_family(args.fetch, "FETCH_SIZE")
     write = pmc_per_family(args.write, "WRITE_SIZE")
 
-    L = [f"# {args.round}: rocprofv3 kernel summary of bench.py (SdP-Net-M, bs 256, bf16, 1 GPU)", ""]
+    what = {"m": "SdP-Net-M, bs 256", "xl": "SdP-Net-XL, bs 512"}.get(args.config, args.config)
+    L = [f"# {args.round}: rocprofv3 kernel summary of bench.py ({what}, bf16, 1 GPU)", ""]
     L.append("Command (kernel trace): `rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv "
              f"-- python {args.cmd}`  ")
     L.append("PMC passes: the same command under `rocprofv3 --pmc FETCH_SIZE` and, separately, `--pmc WRITE_SIZE`.  ")
@@ -137,7 +139,7 @@ def main():
         if kname in fetch and kname in write and fetch[kname][1]:
             n = fetch[kname][1]
             per = (2 * fetch[kname][0] + write[kname][0]) * 1024 / n
-            traffic = dict(kernel=kname, launches=n, fetch_size_kib_sum=fetch[kname][0],
+            traffic = dict(kernel=kname, config=args.config, launches=n, fetch_size_kib_sum=fetch[kname][0],
                            write_size_kib_sum=write[kname][0], hbm_bytes_per_launch=int(per),
                            algorithmic_bytes_per_launch=rf["algorithmic_bytes_per_launch"],
                            method="(2*FETCH_SIZE + WRITE_SIZE)*1024 per dispatch, separate --pmc passes, "
