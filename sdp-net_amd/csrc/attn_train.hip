@@ -60,15 +60,29 @@ SDP_DEV bf16x8 tr_frag(const bf16_t* T, int ld, int k0, int c0, int lane) {
 }
 
 // Stage rows [0, rows) (row r of the source at src + r * lds, hd columns) into an LDS tile
-// [NP][ld] with zeroed padding rows (r >= valid) and columns (>= hd).
+// [NP][ld] with zeroed padding rows (r >= valid) and columns (>= hd).  Batches of BATCH chunks
+// per thread: the batch's global loads are all in flight before its first LDS write (a
+// load -> store loop pays one full memory latency per chunk).
+template <int BATCH>
 SDP_DEV void stage_rows(bf16_t* dst, int ld, int NP, const bf16_t* src, int64_t lds, int valid, int hd, int cols,
                         int tid, int nthr) {
   const int cpr = cols / 8;  // 16-B chunks per LDS row
-  for (int idx = tid; idx < NP * cpr; idx += nthr) {
-    const int r = idx / cpr, c8 = (idx - r * cpr) * 8;
-    bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (r < valid && c8 < hd) v = *(const bf16x8*)(src + (int64_t)r * lds + c8);
-    *(bf16x8*)(dst + (size_t)r * ld + c8) = v;
+  const int total = NP * cpr;
+  for (int base = tid; base < total; base += nthr * BATCH) {
+    bf16x8 v[BATCH];
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int idx = base + u * nthr;
+      const int r = idx / cpr, c8 = (idx - r * cpr) * 8;
+      v[u] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (idx < total && r < valid && c8 < hd) v[u] = *(const bf16x8*)(src + (int64_t)r * lds + c8);
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int idx = base + u * nthr;
+      const int r = idx / cpr, c8 = (idx - r * cpr) * 8;
+      if (idx < total) *(bf16x8*)(dst + (size_t)r * ld + c8) = v[u];
+    }
   }
 }
 
@@ -89,8 +103,8 @@ __global__ __launch_bounds__(640) void attn_fwd_k(const bf16_t* __restrict__ QKV
   const int C = H * hd;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
   const bf16_t* base = QKV + (int64_t)b * N * ldq + hh * hd;
-  stage_rows(Ks, LD, NP, base + C, ldq, N, hd, 32 * HDT, tid, blockDim.x);
-  stage_rows(Vs, LD, NP, base + 2 * C, ldq, N, hd, 32 * HDT, tid, blockDim.x);
+  stage_rows<4>(Ks, LD, NP, base + C, ldq, N, hd, 32 * HDT, tid, blockDim.x);
+  stage_rows<4>(Vs, LD, NP, base + 2 * C, ldq, N, hd, 32 * HDT, tid, blockDim.x);
   __syncthreads();
   const int r = lane & 31, hf = lane >> 5;
   const int nds = hd / 16, nqt = NP / 32;
@@ -179,8 +193,12 @@ __global__ __launch_bounds__(640) void attn_fwd_k(const bf16_t* __restrict__ QKV
 }
 
 // ---------------------------------------------------------------------------
-// dK, dV: workgroup = (b, h, group of KTW key tiles), wave = one 32-key tile (K, V fragments of
-// its keys in registers, dK^T / dV^T accumulators); the query tiles stream through LDS.
+// dK, dV: workgroup = (b, h, group of ktw key tiles) + one producer wave.  Compute wave w owns
+// the 32-key tile grp * ktw + w (K, V fragments of its keys in registers, dK^T / dV^T
+// accumulators); the query tiles stream through a double-buffered LDS ring filled by the last
+// wave of the workgroup: while the compute waves work on query tile qt, the producer loads tile
+// qt + 1 (Q rows, dO rows, LSE, D: 12 KiB of 16-B loads, all in flight at once) and writes it to
+// the other buffer -- one barrier per query tile, the global-load latency off the compute path.
 // ---------------------------------------------------------------------------
 template <int HDT>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kv_k(const bf16_t* __restrict__ QKV, int64_t ldq,
@@ -191,21 +209,76 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_k(const bf16_t* __restrict
                                                      float scale_log2, float scale, uint32_t thresh, float inv_keep,
                                                      uint64_t seed) {
   constexpr int LD = 32 * HDT + 8;
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[32 * LD];
-  __shared__ __attribute__((aligned(16))) bf16_t Gs[32 * LD];  // dO tile
-  __shared__ float Ls[32], Ds[32];
+  constexpr int CPR = 4 * HDT;  // 16-B chunks per staged row (32 * HDT columns)
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[2][32 * LD];
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[2][32 * LD];  // dO tiles
+  __shared__ __attribute__((aligned(16))) float Ls[2][32], Ds[2][32];
   const int bh = blockIdx.x / groups, grp = blockIdx.x - bh * groups;
   const int b = bh / H, hh = bh % H;
   const int C = H * hd;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hf = lane >> 5;
   const int nds = hd / 16;
-  const int NP = (N + 31) / 32 * 32, nkt = NP / 32;
+  const int NP = (N + 31) / 32 * 32, nqt = NP / 32;
+  const bool producer = wave == ktw;  // wave-uniform
   const int kt = grp * ktw + wave;
-  const bool active = kt < nkt;  // (the last group may hold fewer tiles; idle waves still stage)
+  const bool active = !producer && kt < nqt;  // (the last group may hold fewer key tiles)
   const bf16_t* base = QKV + (int64_t)b * N * ldq + hh * hd;
-  const int key = kt * 32 + r;
+  const bf16_t* gbase = dO + (int64_t)b * N * lddo + hh * hd;
+
+  // producer: query tile qt -> registers (12 chunks of Q + dO rows per lane, LSE / D)
+  constexpr int NCH = (2 * 32 * CPR + 63) / 64;
+  bf16x8 pv[NCH];
+  float pl = 0.f, pd = 0.f;
+  auto p_load = [&](int qt) {
+    const int q0 = qt * 32, valid = min(32, N - q0);
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = u * 64 + lane;  // [matrix][row][chunk]
+      const int mtx = idx / (32 * CPR), rem = idx - mtx * 32 * CPR;
+      const int rr = rem / CPR, c8 = (rem - rr * CPR) * 8;
+      pv[u] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (mtx < 2 && rr < valid && c8 < hd)
+        pv[u] = mtx == 0 ? *(const bf16x8*)(base + (int64_t)(q0 + rr) * ldq + c8)
+                         : *(const bf16x8*)(gbase + (int64_t)(q0 + rr) * lddo + c8);
+    }
+    if (lane < 32) {
+      pl = lane < valid ? lse[(int64_t)bh * N + q0 + lane] : INFINITY;  // padded queries: P = 0
+      pd = lane < valid ? D[(int64_t)bh * N + q0 + lane] : 0.f;
+    }
+  };
+  auto p_store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = u * 64 + lane;
+      const int mtx = idx / (32 * CPR), rem = idx - mtx * 32 * CPR;
+      const int rr = rem / CPR, c8 = (rem - rr * CPR) * 8;
+      if (mtx < 2) *(bf16x8*)((mtx == 0 ? Qs[buf] : Gs[buf]) + rr * LD + c8) = pv[u];
+    }
+    if (lane < 32) {
+      Ls[buf][lane] = pl;
+      Ds[buf][lane] = pd;
+    }
+  };
+
+  // the producer and the compute waves run separate loops with the same barrier sequence
+  // (nqt + 1 barriers), so neither keeps the other's registers live
+  if (producer) {
+    p_load(0);
+    p_store(0);
+    __syncthreads();
+    for (int qt = 0; qt < nqt; ++qt) {
+      if (qt + 1 < nqt) {
+        p_load(qt + 1);
+        p_store((qt & 1) ^ 1);  // last read in iteration qt - 1, whose barrier has passed
+      }
+      __syncthreads();
+    }
+    return;
+  }
   bf16x8 kf[2 * HDT], vf[2 * HDT];
+  f32x16 adk[HDT], adv[HDT];
+  const int key = kt * 32 + r;
 #pragma unroll
   for (int s = 0; s < 2 * HDT; ++s) {
     kf[s] = vf[s] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -214,61 +287,64 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_k(const bf16_t* __restrict
       vf[s] = *(const bf16x8*)(base + (int64_t)key * ldq + 2 * C + 16 * s + 8 * hf);
     }
   }
-  f32x16 adk[HDT], adv[HDT];
 #pragma unroll
   for (int dt = 0; dt < HDT; ++dt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) adk[dt][i] = adv[dt][i] = 0.f;
-  const bf16_t* gbase = dO + (int64_t)b * N * lddo + hh * hd;
-  for (int qt = 0; qt < nkt; ++qt) {
-    __syncthreads();  // the previous tile's reads are done
-    const int q0 = qt * 32, valid = min(32, N - q0);
-    stage_rows(Qs, LD, 32, base + (int64_t)q0 * ldq, ldq, valid, hd, 32 * HDT, tid, blockDim.x);
-    stage_rows(Gs, LD, 32, gbase + (int64_t)q0 * lddo, lddo, valid, hd, 32 * HDT, tid, blockDim.x);
-    if (tid < 32) {
-      Ls[tid] = tid < valid ? lse[(int64_t)bh * N + q0 + tid] : INFINITY;  // padded queries: P = 0
-      Ds[tid] = tid < valid ? D[(int64_t)bh * N + q0 + tid] : 0.f;
+  __syncthreads();
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int cur = qt & 1;
+    if (active) {
+      const bf16_t* Q = Qs[cur];
+      const bf16_t* G = Gs[cur];
+      const int q0 = qt * 32;
+      // S[q][key] and dPd[q][key] (lane = key, registers = queries)
+      f32x16 st, dp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st[i] = dp[i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 2 * HDT; ++s) {
+        if (s < nds) {
+          const bf16x8 qa = *(const bf16x8*)(Q + (size_t)r * LD + 16 * s + 8 * hf);
+          const bf16x8 ga = *(const bf16x8*)(G + (size_t)r * LD + 16 * s + 8 * hf);
+          st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], st, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[s], dp, 0, 0, 0);
+        }
+      }
+      // LSE / D of the 16 queries this lane holds: rows (i & 3) + 8 (i >> 2) + 4 hf
+      f32x4 lq[4], dq4[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        lq[g] = *(const f32x4*)(&Ls[cur][8 * g + 4 * hf]);
+        dq4[g] = *(const f32x4*)(&Ds[cur][8 * g + 4 * hf]);
+      }
+      float pdv[16], ds[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qi = acc_row(i, hf);
+        const float pr = key < N ? __builtin_amdgcn_exp2f(st[i] * scale_log2 - lq[i >> 2][i & 3]) : 0.f;
+        const float kp = thresh ? keepf(seed, bh, q0 + qi, key, thresh, inv_keep) : 1.f;
+        pdv[i] = pr * kp;                                // dropout(P)
+        ds[i] = pr * (dp[i] * kp - dq4[i >> 2][i & 3]);  // P o (dP - D)
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pb, sb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pb[j] = (short)f2bf(pdv[8 * s2 + j]);
+          sb[j] = (short)f2bf(ds[8 * s2 + j]);
+        }
+#pragma unroll
+        for (int dt = 0; dt < HDT; ++dt) {
+          adv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(G, LD, 16 * s2 + 4 * hf, dt * 32, lane), pb,
+                                                            adv[dt], 0, 0, 0);
+          adk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Q, LD, 16 * s2 + 4 * hf, dt * 32, lane), sb,
+                                                            adk[dt], 0, 0, 0);
+        }
+      }
     }
     __syncthreads();
-    if (!active) continue;
-    // S[q][key] and dPd[q][key] (lane = key, registers = queries)
-    f32x16 st, dp;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) st[i] = dp[i] = 0.f;
-#pragma unroll
-    for (int s = 0; s < 2 * HDT; ++s) {
-      if (s < nds) {
-        const bf16x8 qa = *(const bf16x8*)(Qs + (size_t)r * LD + 16 * s + 8 * hf);
-        const bf16x8 ga = *(const bf16x8*)(Gs + (size_t)r * LD + 16 * s + 8 * hf);
-        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], st, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[s], dp, 0, 0, 0);
-      }
-    }
-    float pd[16], ds[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qi = acc_row(i, hf);
-      float pr = key < N ? __builtin_amdgcn_exp2f(st[i] * scale_log2 - Ls[qi]) : 0.f;
-      const float kp = thresh ? keepf(seed, bh, q0 + qi, key, thresh, inv_keep) : 1.f;
-      pd[i] = pr * kp;                     // dropout(P)
-      ds[i] = pr * (dp[i] * kp - Ds[qi]);  // P o (dP - D)
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 pb, sb;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        pb[j] = (short)f2bf(pd[8 * s2 + j]);
-        sb[j] = (short)f2bf(ds[8 * s2 + j]);
-      }
-#pragma unroll
-      for (int dt = 0; dt < HDT; ++dt) {
-        adv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Gs, LD, 16 * s2 + 4 * hf, dt * 32, lane), pb,
-                                                          adv[dt], 0, 0, 0);
-        adk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qs, LD, 16 * s2 + 4 * hf, dt * 32, lane), sb,
-                                                          adk[dt], 0, 0, 0);
-      }
-    }
   }
   if (!active || key >= N) return;
   bf16_t* krow = dK + ((int64_t)b * N + key) * lddk + hh * hd;
@@ -292,72 +368,116 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_k(const bf16_t* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// dQ: one workgroup per (b, h), K and V of the head in LDS, one wave per 32-query tile
-// (lane = query, registers = keys: the forward's layout).
+// dQ (and D = rowsum(dO o O)): workgroup = (b, h, group of qtw query tiles) + one producer wave;
+// compute wave w owns the 32-query tile grp * qtw + w (lane = query, registers = keys: the
+// forward's layout) and loops over the key tiles, which the producer streams through a
+// double-buffered LDS ring (K and V rows of tile kt + 1 loaded while tile kt is consumed; one
+// barrier per key tile) -- the dK / dV kernel's structure with the roles of queries and keys
+// swapped.
 // ---------------------------------------------------------------------------
 template <int HDT>
-__global__ __launch_bounds__(640) void attn_bwd_q_k(const bf16_t* __restrict__ QKV, int64_t ldq,
+__global__ __launch_bounds__(256, 2) void attn_bwd_q_k(const bf16_t* __restrict__ QKV, int64_t ldq,
                                                     const bf16_t* __restrict__ O, int64_t ldo,
                                                     const bf16_t* __restrict__ dO, int64_t lddo,
                                                     const float* __restrict__ lse, float* __restrict__ D,
                                                     bf16_t* __restrict__ dQ, int64_t lddq, int N, int H, int hd,
-                                                    float scale_log2, float scale, uint32_t thresh, float inv_keep,
-                                                    uint64_t seed) {
-  extern __shared__ __attribute__((aligned(16))) char sm[];
+                                                    int qtw, int groups, float scale_log2, float scale,
+                                                    uint32_t thresh, float inv_keep, uint64_t seed) {
   constexpr int LD = 32 * HDT + 8;
-  const int NP = (N + 31) / 32 * 32;
-  bf16_t* Ks = (bf16_t*)sm;
-  bf16_t* Vs = Ks + (size_t)NP * LD;
-  const int bh = blockIdx.x, b = bh / H, hh = bh % H;
+  constexpr int CPR = 4 * HDT;  // 16-B chunks per staged row
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2][32 * LD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2][32 * LD];
+  const int bh = blockIdx.x / groups, grp = blockIdx.x - bh * groups;
+  const int b = bh / H, hh = bh % H;
   const int C = H * hd;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
-  const bf16_t* base = QKV + (int64_t)b * N * ldq + hh * hd;
-  stage_rows(Ks, LD, NP, base + C, ldq, N, hd, 32 * HDT, tid, blockDim.x);
-  stage_rows(Vs, LD, NP, base + 2 * C, ldq, N, hd, 32 * HDT, tid, blockDim.x);
-  __syncthreads();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hf = lane >> 5;
-  const int nds = hd / 16, nqt = NP / 32;
+  const int nds = hd / 16;
+  const int NP = (N + 31) / 32 * 32, nkt = NP / 32;
+  const bf16_t* base = QKV + (int64_t)b * N * ldq + hh * hd;
+  if (wave == qtw) {  // producer: key tile kt -> Ks / Vs [buf] (K and V rows, 16-B loads all in flight)
+    constexpr int NCH = (2 * 32 * CPR + 63) / 64;
+    bf16x8 pv[NCH];
+    auto p_load = [&](int kt) {
+      const int k0 = kt * 32, valid = min(32, N - k0);
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        const int idx = u * 64 + lane;  // [matrix][row][chunk]
+        const int mtx = idx / (32 * CPR), rem = idx - mtx * 32 * CPR;
+        const int rr = rem / CPR, c8 = (rem - rr * CPR) * 8;
+        pv[u] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (mtx < 2 && rr < valid && c8 < hd)
+          pv[u] = *(const bf16x8*)(base + (int64_t)(k0 + rr) * ldq + (mtx + 1) * C + c8);
+      }
+    };
+    auto p_store = [&](int buf) {
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        const int idx = u * 64 + lane;
+        const int mtx = idx / (32 * CPR), rem = idx - mtx * 32 * CPR;
+        const int rr = rem / CPR, c8 = (rem - rr * CPR) * 8;
+        if (mtx < 2) *(bf16x8*)((mtx == 0 ? Ks[buf] : Vs[buf]) + rr * LD + c8) = pv[u];
+      }
+    };
+    p_load(0);
+    p_store(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      if (kt + 1 < nkt) {
+        p_load(kt + 1);
+        p_store((kt & 1) ^ 1);  // last read in iteration kt - 1, whose barrier has passed
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  const int qt = grp * qtw + wave;
+  const bool active = qt < nkt;
+  const int q = qt * 32 + r;
+  const bool qok = active && q < N;
   const bf16_t* gbase = dO + (int64_t)b * N * lddo + hh * hd;
-  for (int qt = wave; qt < nqt; qt += nwaves) {
-    const int q = qt * 32 + r;
-    const bool qok = q < N;
-    bf16x8 qf[2 * HDT], gf[2 * HDT];
+  bf16x8 qf[2 * HDT], gf[2 * HDT];
+#pragma unroll
+  for (int s = 0; s < 2 * HDT; ++s) {
+    qf[s] = gf[s] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (s < nds && qok) {
+      qf[s] = *(const bf16x8*)(base + (int64_t)q * ldq + 16 * s + 8 * hf);
+      gf[s] = *(const bf16x8*)(gbase + (int64_t)q * lddo + 16 * s + 8 * hf);
+    }
+  }
+  const float lq = qok ? lse[(int64_t)bh * N + q] : INFINITY;
+  // D = rowsum(dO o O) for this query (its two lane halves hold the two halves of every
+  // 16-wide d step); written for attn_bwd_kv_k, which runs next
+  float dq_ = 0.f;
+  if (qok) {
+    const bf16_t* orow = O + ((int64_t)b * N + q) * ldo + hh * hd;
 #pragma unroll
     for (int s = 0; s < 2 * HDT; ++s) {
-      qf[s] = gf[s] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (s < nds && qok) {
-        qf[s] = *(const bf16x8*)(base + (int64_t)q * ldq + 16 * s + 8 * hf);
-        gf[s] = *(const bf16x8*)(gbase + (int64_t)q * lddo + 16 * s + 8 * hf);
+      if (s < nds) {
+        const bf16x8 ov = *(const bf16x8*)(orow + 16 * s + 8 * hf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dq_ = fmaf(bf2f((bf16_t)ov[e]), bf2f((bf16_t)gf[s][e]), dq_);
       }
     }
-    const float lq = qok ? lse[(int64_t)bh * N + q] : INFINITY;
-    // D = rowsum(dO o O) for this query (its two lane halves hold the two halves of every
-    // 16-wide d step); written for attn_bwd_kv_k, which runs next
-    float dq_ = 0.f;
-    if (qok) {
-      const bf16_t* orow = O + ((int64_t)b * N + q) * ldo + hh * hd;
+  }
+  dq_ += __shfl_xor(dq_, 32, 64);
+  if (qok && hf == 0) D[(int64_t)bh * N + q] = dq_;
+  f32x16 acc[HDT];
 #pragma unroll
-      for (int s = 0; s < 2 * HDT; ++s) {
-        if (s < nds) {
-          const bf16x8 ov = *(const bf16x8*)(orow + 16 * s + 8 * hf);
+  for (int dt = 0; dt < HDT; ++dt)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) dq_ = fmaf(bf2f((bf16_t)ov[e]), bf2f((bf16_t)gf[s][e]), dq_);
-        }
-      }
-    }
-    dq_ += __shfl_xor(dq_, 32, 64);
-    if (qok && hf == 0) D[(int64_t)bh * N + q] = dq_;
-    f32x16 acc[HDT];
-#pragma unroll
-    for (int dt = 0; dt < HDT; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
-    for (int kt = 0; kt < nqt; ++kt) {
+    for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (active) {
+      const bf16_t* Kt = Ks[cur];
+      const bf16_t* Vt = Vs[cur];
       f32x16 st, dp;
 #pragma unroll
       for (int i = 0; i < 16; ++i) st[i] = dp[i] = 0.f;
-      const bf16_t* krow = Ks + (size_t)(kt * 32 + r) * LD + 8 * hf;
-      const bf16_t* vrow = Vs + (size_t)(kt * 32 + r) * LD + 8 * hf;
+      const bf16_t* krow = Kt + (size_t)r * LD + 8 * hf;
+      const bf16_t* vrow = Vt + (size_t)r * LD + 8 * hf;
 #pragma unroll
       for (int s = 0; s < 2 * HDT; ++s) {
         if (s < nds) {
@@ -380,25 +500,26 @@ __global__ __launch_bounds__(640) void attn_bwd_q_k(const bf16_t* __restrict__ Q
         for (int j = 0; j < 8; ++j) sb[j] = (short)f2bf(ds[8 * s2 + j]);
 #pragma unroll
         for (int dt = 0; dt < HDT; ++dt)
-          acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Ks, LD, kt * 32 + 16 * s2 + 4 * hf, dt * 32, lane),
-                                                            sb, acc[dt], 0, 0, 0);
+          acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Kt, LD, 16 * s2 + 4 * hf, dt * 32, lane), sb,
+                                                            acc[dt], 0, 0, 0);
       }
     }
-    if (qok) {
-      bf16_t* row = dQ + ((int64_t)b * N + q) * lddq + hh * hd;
+    __syncthreads();
+  }
+  if (qok) {
+    bf16_t* row = dQ + ((int64_t)b * N + q) * lddq + hh * hd;
 #pragma unroll
-      for (int dt = 0; dt < HDT; ++dt)
+    for (int dt = 0; dt < HDT; ++dt)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d = dt * 32 + 8 * g + 4 * hf;
-          if (d < hd) {
-            bf16x4 o;
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hf;
+        if (d < hd) {
+          bf16x4 o;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(acc[dt][4 * g + e] * scale);
-            *(bf16x4*)(row + d) = o;
-          }
+          for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(acc[dt][4 * g + e] * scale);
+          *(bf16x4*)(row + d) = o;
         }
-    }
+      }
   }
 }
 
@@ -458,19 +579,15 @@ static int launch_bwd(const void* qkv, int64_t ldq, const void* o, int64_t ldo, 
                       int64_t lddv, int B, int N, int H, int hd, float scale, uint32_t thresh, float inv_keep,
                       uint64_t seed, hipStream_t s) {
   const int nkt = (N + 31) / 32;
-  // dQ (and D = rowsum(dO o O)) first: the dK / dV kernel reads D
-  const size_t bytes = kv_lds_bytes(N, HDT);
-  hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_q_k<HDT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)bytes);
-  if (e != hipSuccess) return (int)e;
-  const int waves = std::min(10, nkt);
-  hipLaunchKernelGGL(attn_bwd_q_k<HDT>, dim3(B * H), dim3(64 * waves), bytes, s, (const bf16_t*)qkv, ldq,
-                     (const bf16_t*)o, ldo, (const bf16_t*)dO, lddo, lse, D, (bf16_t*)dq, lddq, N, H, hd,
-                     scale * 1.4426950408889634f, scale, thresh, inv_keep, seed);
+  // dQ (and D = rowsum(dO o O)) first: the dK / dV kernel reads D.  Both: at most 3 compute
+  // waves + the producer per workgroup (launch bound 256)
+  const int groups = (nkt + 2) / 3, ktw = (nkt + groups - 1) / groups;
+  hipLaunchKernelGGL(attn_bwd_q_k<HDT>, dim3(B * H * groups), dim3(64 * (ktw + 1)), 0, s, (const bf16_t*)qkv, ldq,
+                     (const bf16_t*)o, ldo, (const bf16_t*)dO, lddo, lse, D, (bf16_t*)dq, lddq, N, H, hd, ktw,
+                     groups, scale * 1.4426950408889634f, scale, thresh, inv_keep, seed);
   int rc = SDP_CHECK_LAUNCH();
   if (rc) return rc;
-  const int groups = (nkt + 3) / 4, ktw = (nkt + groups - 1) / groups;
-  hipLaunchKernelGGL(attn_bwd_kv_k<HDT>, dim3(B * H * groups), dim3(64 * ktw), 0, s, (const bf16_t*)qkv, ldq,
+  hipLaunchKernelGGL(attn_bwd_kv_k<HDT>, dim3(B * H * groups), dim3(64 * (ktw + 1)), 0, s, (const bf16_t*)qkv, ldq,
                      (const bf16_t*)dO, lddo, lse, (const float*)D, (bf16_t*)dk, lddk, (bf16_t*)dv, lddv, N, H, hd,
                      ktw, groups, scale * 1.4426950408889634f, scale, thresh, inv_keep, seed);
   return SDP_CHECK_LAUNCH();
