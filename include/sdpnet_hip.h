@@ -489,7 +489,8 @@ int sdp_adamw_finish(float* state, float* scale_tracker, float growth, float bac
  * in a fixed order into state[0].  Same result as sdp_grad_sumsq without float atomics. */
 /*
  * Flash-style training attention (layers.py:289-291, F.scaled_dot_product_attention with
- * dropout_p; bf16 only, hd % 16 == 0, hd <= 128, K + V of one head <= 160 KiB of LDS).
+ * dropout_p; bf16 only, hd % 16 == 0, hd <= 128, any N: every kernel streams 32-row tiles of the
+ * head through a double-buffered LDS ring filled by a producer wave).
  * q, k, v of head h are columns h*hd, C + h*hd, 2C + h*hd of the [B*N, ldq] rows (C = H*hd).
  *   sdp_attn_train_fwd: O = dropout(softmax(scale Q K^T)) V into [B*N, ldo] rows; lse[(b*H+h)*N+q]
  *     = log2 sum_k exp2(scale log2(e) q.k) (fp32).  S and P are never stored.

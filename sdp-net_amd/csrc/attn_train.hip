@@ -59,58 +59,82 @@ SDP_DEV bf16x8 tr_frag(const bf16_t* T, int ld, int k0, int c0, int lane) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// Stage rows [0, rows) (row r of the source at src + r * lds, hd columns) into an LDS tile
-// [NP][ld] with zeroed padding rows (r >= valid) and columns (>= hd).  Batches of BATCH chunks
-// per thread: the batch's global loads are all in flight before its first LDS write (a
-// load -> store loop pays one full memory latency per chunk).
-template <int BATCH>
-SDP_DEV void stage_rows(bf16_t* dst, int ld, int NP, const bf16_t* src, int64_t lds, int valid, int hd, int cols,
-                        int tid, int nthr) {
-  const int cpr = cols / 8;  // 16-B chunks per LDS row
-  const int total = NP * cpr;
-  for (int base = tid; base < total; base += nthr * BATCH) {
-    bf16x8 v[BATCH];
+// ---------------------------------------------------------------------------
+// Producer wave of the streaming kernels: key tile kt of the head (K and V rows, hd columns,
+// zero padding) -> Kb / Vb + buf * 32 * LD, for kt = 0 .. nkt-1 into alternate buffers.  Its
+// barrier sequence (one after tile 0, then one per tile) matches the compute waves' (one before
+// their loop, one per tile): tile kt + 1 is loaded while the compute waves consume tile kt, and
+// written to the buffer they finished reading in iteration kt - 1.
+// ---------------------------------------------------------------------------
+template <int HDT>
+SDP_DEV void kv_ring_producer(const bf16_t* base, int64_t ldq, int C, int N, int hd, int nkt, bf16_t* Kb,
+                              bf16_t* Vb, int lane) {
+  constexpr int LD = 32 * HDT + 8;
+  constexpr int CPR = 4 * HDT;  // 16-B chunks per staged row
+  constexpr int NCH = (2 * 32 * CPR + 63) / 64;
+  bf16x8 pv[NCH];
+  auto p_load = [&](int kt) {
+    const int k0 = kt * 32, valid = min(32, N - k0);
 #pragma unroll
-    for (int u = 0; u < BATCH; ++u) {
-      const int idx = base + u * nthr;
-      const int r = idx / cpr, c8 = (idx - r * cpr) * 8;
-      v[u] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (idx < total && r < valid && c8 < hd) v[u] = *(const bf16x8*)(src + (int64_t)r * lds + c8);
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = u * 64 + lane;  // [matrix][row][chunk]
+      const int mtx = idx / (32 * CPR), rem = idx - mtx * 32 * CPR;
+      const int rr = rem / CPR, c8 = (rem - rr * CPR) * 8;
+      pv[u] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (mtx < 2 && rr < valid && c8 < hd) pv[u] = *(const bf16x8*)(base + (int64_t)(k0 + rr) * ldq + (mtx + 1) * C + c8);
     }
+  };
+  auto p_store = [&](int buf) {
 #pragma unroll
-    for (int u = 0; u < BATCH; ++u) {
-      const int idx = base + u * nthr;
-      const int r = idx / cpr, c8 = (idx - r * cpr) * 8;
-      if (idx < total) *(bf16x8*)(dst + (size_t)r * ld + c8) = v[u];
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = u * 64 + lane;
+      const int mtx = idx / (32 * CPR), rem = idx - mtx * 32 * CPR;
+      const int rr = rem / CPR, c8 = (rem - rr * CPR) * 8;
+      if (mtx < 2) *(bf16x8*)((mtx == 0 ? Kb : Vb) + buf * 32 * LD + rr * LD + c8) = pv[u];
     }
+  };
+  p_load(0);
+  p_store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 1 < nkt) {
+      p_load(kt + 1);
+      p_store((kt & 1) ^ 1);
+    }
+    __syncthreads();
   }
 }
 
 // ---------------------------------------------------------------------------
-// Forward: one workgroup per (b, h), K and V of the head in LDS, one wave per 32-query tile.
+// Forward: workgroup = (b, h, group of qtw query tiles) + one producer wave streaming the key
+// tiles (K, V rows) through a double-buffered LDS ring; compute wave w owns the 32-query tile
+// grp * qtw + w and runs the online softmax over the key tiles as they arrive.
 // ---------------------------------------------------------------------------
 template <int HDT>
-__global__ __launch_bounds__(640) void attn_fwd_k(const bf16_t* __restrict__ QKV, int64_t ldq,
+__global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16_t* __restrict__ QKV, int64_t ldq,
                                                   bf16_t* __restrict__ O, int64_t ldo, float* __restrict__ lse,
-                                                  int N, int H, int hd, float scale_log2, uint32_t thresh,
-                                                  float inv_keep, uint64_t seed) {
-  extern __shared__ __attribute__((aligned(16))) char sm[];
+                                                  int N, int H, int hd, int qtw, int groups, float scale_log2,
+                                                  uint32_t thresh, float inv_keep, uint64_t seed) {
   constexpr int LD = 32 * HDT + 8;
-  const int NP = (N + 31) / 32 * 32;
-  bf16_t* Ks = (bf16_t*)sm;
-  bf16_t* Vs = Ks + (size_t)NP * LD;
-  const int bh = blockIdx.x, b = bh / H, hh = bh % H;
+  __shared__ __attribute__((aligned(16))) bf16_t Kr[2][32 * LD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vr[2][32 * LD];
+  const int bh = blockIdx.x / groups, grp = blockIdx.x - bh * groups;
+  const int b = bh / H, hh = bh % H;
   const int C = H * hd;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int NP = (N + 31) / 32 * 32, nqt = NP / 32;
   const bf16_t* base = QKV + (int64_t)b * N * ldq + hh * hd;
-  stage_rows<4>(Ks, LD, NP, base + C, ldq, N, hd, 32 * HDT, tid, blockDim.x);
-  stage_rows<4>(Vs, LD, NP, base + 2 * C, ldq, N, hd, 32 * HDT, tid, blockDim.x);
-  __syncthreads();
+  if (wave == qtw) {
+    kv_ring_producer<HDT>(base, ldq, C, N, hd, nqt, &Kr[0][0], &Vr[0][0], lane);
+    return;
+  }
   const int r = lane & 31, hf = lane >> 5;
-  const int nds = hd / 16, nqt = NP / 32;
-  for (int qt = wave; qt < nqt; qt += nwaves) {
+  const int nds = hd / 16;
+  {
+    const int qt = grp * qtw + wave;
+    const bool active = qt < nqt;
     const int q = qt * 32 + r;
-    const bool qok = q < N;
+    const bool qok = active && q < N;
     bf16x8 qf[2 * HDT];
 #pragma unroll
     for (int s = 0; s < 2 * HDT; ++s) {
@@ -123,11 +147,18 @@ __global__ __launch_bounds__(640) void attn_fwd_k(const bf16_t* __restrict__ QKV
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
     float m = -INFINITY, l = 0.f;
+    __syncthreads();
     for (int kt = 0; kt < nqt; ++kt) {
+      if (!active) {
+        __syncthreads();
+        continue;
+      }
+      const bf16_t* Kt = Kr[kt & 1];
+      const bf16_t* Vt = Vr[kt & 1];
       f32x16 st;
 #pragma unroll
       for (int i = 0; i < 16; ++i) st[i] = 0.f;
-      const bf16_t* krow = Ks + (size_t)(kt * 32 + r) * LD + 8 * hf;
+      const bf16_t* krow = Kt + (size_t)r * LD + 8 * hf;
 #pragma unroll
       for (int s = 0; s < 2 * HDT; ++s)
         if (s < nds) st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(krow + 16 * s), qf[s], st, 0, 0, 0);
@@ -167,9 +198,10 @@ __global__ __launch_bounds__(640) void attn_fwd_k(const bf16_t* __restrict__ QKV
         for (int j = 0; j < 8; ++j) pb[j] = (short)f2bf(pv[8 * s2 + j]);
 #pragma unroll
         for (int dt = 0; dt < HDT; ++dt)
-          acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vs, LD, kt * 32 + 16 * s2 + 4 * hf, dt * 32, lane),
+          acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vt, LD, 16 * s2 + 4 * hf, dt * 32, lane),
                                                             pb, acc[dt], 0, 0, 0);
       }
+      __syncthreads();
     }
     l += __shfl_xor(l, 32, 64);
     if (qok) {
@@ -384,7 +416,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_k(const bf16_t* __restrict_
                                                     int qtw, int groups, float scale_log2, float scale,
                                                     uint32_t thresh, float inv_keep, uint64_t seed) {
   constexpr int LD = 32 * HDT + 8;
-  constexpr int CPR = 4 * HDT;  // 16-B chunks per staged row
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2][32 * LD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[2][32 * LD];
   const int bh = blockIdx.x / groups, grp = blockIdx.x - bh * groups;
@@ -395,40 +426,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_k(const bf16_t* __restrict_
   const int nds = hd / 16;
   const int NP = (N + 31) / 32 * 32, nkt = NP / 32;
   const bf16_t* base = QKV + (int64_t)b * N * ldq + hh * hd;
-  if (wave == qtw) {  // producer: key tile kt -> Ks / Vs [buf] (K and V rows, 16-B loads all in flight)
-    constexpr int NCH = (2 * 32 * CPR + 63) / 64;
-    bf16x8 pv[NCH];
-    auto p_load = [&](int kt) {
-      const int k0 = kt * 32, valid = min(32, N - k0);
-#pragma unroll
-      for (int u = 0; u < NCH; ++u) {
-        const int idx = u * 64 + lane;  // [matrix][row][chunk]
-        const int mtx = idx / (32 * CPR), rem = idx - mtx * 32 * CPR;
-        const int rr = rem / CPR, c8 = (rem - rr * CPR) * 8;
-        pv[u] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (mtx < 2 && rr < valid && c8 < hd)
-          pv[u] = *(const bf16x8*)(base + (int64_t)(k0 + rr) * ldq + (mtx + 1) * C + c8);
-      }
-    };
-    auto p_store = [&](int buf) {
-#pragma unroll
-      for (int u = 0; u < NCH; ++u) {
-        const int idx = u * 64 + lane;
-        const int mtx = idx / (32 * CPR), rem = idx - mtx * 32 * CPR;
-        const int rr = rem / CPR, c8 = (rem - rr * CPR) * 8;
-        if (mtx < 2) *(bf16x8*)((mtx == 0 ? Ks[buf] : Vs[buf]) + rr * LD + c8) = pv[u];
-      }
-    };
-    p_load(0);
-    p_store(0);
-    __syncthreads();
-    for (int kt = 0; kt < nkt; ++kt) {
-      if (kt + 1 < nkt) {
-        p_load(kt + 1);
-        p_store((kt & 1) ^ 1);  // last read in iteration kt - 1, whose barrier has passed
-      }
-      __syncthreads();
-    }
+  if (wave == qtw) {
+    kv_ring_producer<HDT>(base, ldq, C, N, hd, nkt, &Ks[0][0], &Vs[0][0], lane);
     return;
   }
   const int qt = grp * qtw + wave;
@@ -544,11 +543,9 @@ static void drop_params(float p, uint32_t* thresh, float* inv_keep) {
   *inv_keep = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
 }
 
-static size_t kv_lds_bytes(int N, int HDT) { return (size_t)2 * ((N + 31) / 32 * 32) * (32 * HDT + 8) * 2; }
-
+// every kernel streams the key / query tiles through a fixed 2-buffer LDS ring: any N
 extern "C" int sdp_attn_train_applies(int dtype, int N, int hd) {
-  if (dtype != 1 || N < 1 || hd < 16 || hd > 128 || hd % 16) return 0;
-  return kv_lds_bytes(N, (hd + 31) / 32) <= 160 * 1024 ? 1 : 0;
+  return (dtype == 1 && N >= 1 && hd >= 16 && hd <= 128 && hd % 16 == 0) ? 1 : 0;
 }
 
 #define SDP_HDT_DISPATCH(hd, KERN, ...)                                    \
@@ -563,13 +560,11 @@ extern "C" int sdp_attn_train_applies(int dtype, int N, int hd) {
 template <int HDT>
 static int launch_fwd(const void* qkv, int64_t ldq, void* o, int64_t ldo, float* lse, int B, int N, int H, int hd,
                       float scale, uint32_t thresh, float inv_keep, uint64_t seed, hipStream_t s) {
-  const size_t bytes = kv_lds_bytes(N, HDT);
-  hipError_t e = hipFuncSetAttribute((const void*)attn_fwd_k<HDT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)bytes);
-  if (e != hipSuccess) return (int)e;
-  const int waves = std::min(10, (N + 31) / 32);
-  hipLaunchKernelGGL(attn_fwd_k<HDT>, dim3(B * H), dim3(64 * waves), bytes, s, (const bf16_t*)qkv, ldq, (bf16_t*)o,
-                     ldo, lse, N, H, hd, scale * 1.4426950408889634f, thresh, inv_keep, seed);
+  // at most 3 compute waves + the producer per workgroup (launch bound 256)
+  const int nqt = (N + 31) / 32;
+  const int groups = (nqt + 2) / 3, qtw = (nqt + groups - 1) / groups;
+  hipLaunchKernelGGL(attn_fwd_k<HDT>, dim3(B * H * groups), dim3(64 * (qtw + 1)), 0, s, (const bf16_t*)qkv, ldq,
+                     (bf16_t*)o, ldo, lse, N, H, hd, qtw, groups, scale * 1.4426950408889634f, thresh, inv_keep, seed);
   return SDP_CHECK_LAUNCH();
 }
 

@@ -492,7 +492,8 @@ def test_act_rowscale_add_matches_two_passes(dtype, act, C):
 
 # ------------------------------------------------- flash training attention (attn_train.hip)
 @pytest.mark.parametrize("B,N,H,hd", [(2, 260, 8, 96), (3, 200, 8, 96), (2, 53, 4, 16), (1, 77, 2, 64),
-                                      (1, 33, 2, 128), (2, 100, 4, 48), (1, 1, 2, 32), (2, 300, 2, 80)])
+                                      (1, 33, 2, 128), (2, 100, 4, 48), (1, 1, 2, 32), (2, 300, 2, 80),
+                                      (1, 700, 2, 96), (1, 64, 2, 96), (1, 96, 1, 128)])
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_flash_train_attention_vs_torch(B, N, H, hd, p):
     """O, the row LSE and dQ / dK / dV of the flash training kernels against torch fp32 autograd of
