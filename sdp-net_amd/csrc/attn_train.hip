@@ -590,8 +590,10 @@ static int launch_bwd(const void* qkv, int64_t ldq, const void* o, int64_t ldo, 
 
 extern "C" int sdp_attn_train_fwd(int dtype, const void* qkv, int64_t ldq, void* o, int64_t ldo, float* lse, int B,
                                   int N, int H, int hd, float scale, float p, uint64_t seed, void* stream) {
+  // bf16x8 loads of the qkv rows, bf16x4 stores of O rows
   if (!sdp_attn_train_applies(dtype, N, hd) || !qkv || !o || !lse || B < 0 || H <= 0 || p < 0.f || p >= 1.f ||
-      ldq % 8 || ldo % 8 || ldq < 3 * (int64_t)H * hd || ldo < (int64_t)H * hd)
+      ldq % 8 || ldo % 8 || ldq < 3 * (int64_t)H * hd || ldo < (int64_t)H * hd || (uintptr_t)qkv % 16 ||
+      (uintptr_t)o % 8)
     return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
   uint32_t thresh;
