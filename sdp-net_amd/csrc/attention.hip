@@ -1018,6 +1018,173 @@ __global__ __launch_bounds__(256, 2) void attn_fa4_bf16(const bf16_t* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// attn_fs_bf16 — streaming flash attention (the training kernels' structure, csrc/attn_train.hip):
+// workgroup = (b, h, <= 3 query tiles) + one producer wave.  The producer streams the head's
+// 32-row K / V tiles through a double-buffered LDS ring (padded rows, LD = HD + 8): lane l loads
+// row l & 31 of K (l < 32) or V, all CPR 16-B chunks in flight at once, k-normalises its K row in
+// registers (one-pass fp32 statistics, as attn_knorm32) and stores it; one barrier per key tile.
+// Compute wave w owns query tile grp * qtw + w: q-norm on its fragments, then the online softmax
+// over the key tiles as they arrive (S^T = K Q^T and O^T += V^T P^T in the swapped 32x32x16 form,
+// exp2 argument folded into one FMA).  LDS 26 KiB per workgroup at hd = 96, so several workgroups
+// share a CU and no K / V staging phase stands alone (attn_fa2 stages the whole head first).
+// ---------------------------------------------------------------------------
+template <int HDT>
+__global__ __launch_bounds__(256, 2) void attn_fs_bf16(const bf16_t* __restrict__ QKV, int64_t ldq,
+                                                    bf16_t* __restrict__ O, int64_t ldo, int N, int H, int qtw,
+                                                    int groups, const float* __restrict__ gq,
+                                                    const float* __restrict__ bq, const float* __restrict__ gk,
+                                                    const float* __restrict__ bk, float eps, float scale_log2) {
+  constexpr int HD = 32 * HDT, LD = HD + 8, CPR = HD / 8, NDS = HD / 16;
+  __shared__ __attribute__((aligned(16))) bf16_t Kr[2][32 * LD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vr[2][32 * LD];
+  __shared__ __attribute__((aligned(16))) float prm[2 * HD];  // k_norm gamma | beta
+  const int bh = blockIdx.x / groups, grp = blockIdx.x - bh * groups;
+  const int b = bh / H, hh = bh - b * H;
+  const int C = H * HD;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nkt = (N + 31) / 32;
+  const bf16_t* base = QKV + (int64_t)b * N * ldq + hh * HD;
+  const bool norm = gq != nullptr;
+  if (wave == qtw) {  // producer
+    if (norm)
+      for (int i = lane; i < 2 * HD; i += 64) prm[i] = i < HD ? gk[i] : bk[i - HD];
+    const int mtx = lane >> 5, row = lane & 31;
+    bf16x8 pv[CPR];
+    auto p_load = [&](int kt) {
+      const int kr = kt * 32 + row;
+      const bf16_t* src = base + (int64_t)(kr < N ? kr : N - 1) * ldq + (mtx + 1) * C;
+#pragma unroll
+      for (int u = 0; u < CPR; ++u) pv[u] = *(const bf16x8*)(src + 8 * u);
+      if (kr >= N)
+#pragma unroll
+        for (int u = 0; u < CPR; ++u) pv[u] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    };
+    auto p_store = [&](int buf) {
+      if (norm && mtx == 0) {
+        f32x2 st = {0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < CPR; ++u) st = frag_stats(pv[u], st);
+        const float mean = st.x * (1.0f / HD);
+        const float rstd = rsqrtf(fmaxf(st.y * (1.0f / HD) - mean * mean, 0.f) + eps);
+#pragma unroll
+        for (int u = 0; u < CPR; ++u) pv[u] = frag_norm(pv[u], mean, rstd, prm + 8 * u, prm + HD + 8 * u);
+      }
+      bf16_t* dst = (mtx == 0 ? &Kr[buf][0] : &Vr[buf][0]) + row * LD;
+#pragma unroll
+      for (int u = 0; u < CPR; ++u) *(bf16x8*)(dst + 8 * u) = pv[u];
+    };
+    p_load(0);
+    p_store(0);  // (prm was written by this wave: its LDS accesses are in order)
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      if (kt + 1 < nkt) {
+        p_load(kt + 1);
+        p_store((kt & 1) ^ 1);  // last read in iteration kt - 1, whose barrier has passed
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  const int r = lane & 31, hf = lane >> 5;
+  const int qt = grp * qtw + wave;
+  const bool active = qt < nkt;
+  const int q = qt * 32 + r;
+  const bool qok = active && q < N;
+  bf16x8 qf[2 * HDT];
+  attn_load_q<HDT>(base + (int64_t)(q < N ? q : N - 1) * ldq, hf, qf);
+  if (norm) attn_norm_q<HDT>(qf, qok, hf, gq, bq, eps);
+  f32x16 acc[HDT];
+#pragma unroll
+  for (int dt = 0; dt < HDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
+  float m = -INFINITY;
+  f32x2 l2 = {0.f, 0.f};
+  const f32x2 sl2 = {scale_log2, scale_log2};
+  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (active) {
+      const bf16_t* Kt = Kr[kt & 1];
+      const bf16_t* Vt = Vr[kt & 1];
+      f32x16 st;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st[i] = 0.f;
+      const bf16_t* krow = Kt + (size_t)r * LD + 8 * hf;
+#pragma unroll
+      for (int s2 = 0; s2 < NDS; ++s2)
+        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(krow + 16 * s2), qf[s2], st, 0, 0, 0);
+      if (kt * 32 + 32 > N) {  // padded keys of the last tile
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf >= N) st[i] = -INFINITY;
+      }
+      float tmax = fmaxf(fmaxf(st[0], st[1]), st[2]);
+#pragma unroll
+      for (int i = 3; i < 15; i += 2) tmax = fmaxf(fmaxf(tmax, st[i]), st[i + 1]);
+      tmax = xhalf_max(fmaxf(tmax, st[15]));
+      const float mn = fmaxf(m, tmax);
+      if (__any(mn > m)) {  // wave-uniform: rescale only when some running max moved
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
+        l2 *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < HDT; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
+        m = mn;
+      }
+      const float msc = -m * scale_log2;
+      const f32x2 msc2 = {msc, msc};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        u32x4 pk;
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const f32x2 a = f32x2{st[8 * s2 + j], st[8 * s2 + j + 1]} * sl2 + msc2;
+          const f32x2 p2 = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+          l2 += p2;
+          pk[j >> 1] = pack_bf16x2(p2.x, p2.y);
+        }
+        const bf16x8 pb = __builtin_bit_cast(bf16x8, pk);
+#pragma unroll
+        for (int dt = 0; dt < HDT; ++dt) {
+          const bf16_t* vb = Vt + (size_t)(16 * s2 + 4 * hf + tq) * LD + dt * 32 + 16 * ((lane >> 4) & 1) + 4 * tp;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)vb);
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(vb + 8 * LD));
+          const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb, acc[dt], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (!qok) return;
+  const float inv = 1.0f / xhalf_sum(l2.x + l2.y);
+  bf16_t* orow = O + ((int64_t)b * N + q) * ldo + hh * HD;
+#pragma unroll
+  for (int dt = 0; dt < HDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(acc[dt][4 * g + e] * inv);
+      *(bf16x4*)(orow + dt * 32 + 8 * g + 4 * hf) = o;
+    }
+}
+
+template <int HDT>
+static int launch_attn_fs(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H,
+                          const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
+                          hipStream_t s) {
+  // at most 3 compute waves + the producer per workgroup (launch bound 256)
+  const int nqt = (N + 31) / 32;
+  const int groups = (nqt + 2) / 3, qtw = (nqt + groups - 1) / groups;
+  hipLaunchKernelGGL(attn_fs_bf16<HDT>, dim3(B * H * groups), dim3(64 * (qtw + 1)), 0, s, (const bf16_t*)QKV, ldq,
+                     (bf16_t*)O, ldo, N, H, qtw, groups, gq, bq, gk, bk, eps, scale * 1.4426950408889634f);
+  return SDP_CHECK_LAUNCH();
+}
+
 static int g_attn_per_cu = 0;  // fa4 workgroups per CU (0 = as many as LDS and registers allow)
 
 // Set the fa4 workgroups per CU (0 = occupancy-derived); returns the old value.
@@ -1100,16 +1267,17 @@ static size_t attn_fa_bytes(int N, int hd) {
 }
 
 // bf16 flash kernel selection: 2 = attn_fa_bf16, 3 = attn_fa2_bf16, 4 (default) =
-// attn_fa4_bf16 (each where it applies, else the next lower one)
+// attn_fa4_bf16 (each where it applies, else the next lower one), 5 = attn_fs_bf16 (any N)
 static int g_attn_kernel = 4;
 extern "C" int sdp_attention_set_kernel(int k) {
   const int old = g_attn_kernel;
-  if (k >= 2 && k <= 4) g_attn_kernel = k;
+  if (k >= 2 && k <= 5) g_attn_kernel = k;
   return old;
 }
 
 extern "C" int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask) {
   if (dtype != 1 || has_mask || head_dim > 128 || head_dim % 16 != 0) return 0;
+  if (g_attn_kernel == 5 && head_dim % 32 == 0) return 5;
   if (g_attn_kernel >= 4 && head_dim % 32 == 0 && N <= 256 && attn_fa4_bytes(N, head_dim) <= 160 * 1024) return 4;
   if (g_attn_kernel >= 3 && head_dim % 32 == 0 && attn_fa2_bytes(N, head_dim) <= 160 * 1024) return 3;
   if (attn_fa_bytes(N, head_dim) > 160 * 1024) return 0;
@@ -1133,6 +1301,16 @@ extern "C" int sdp_attention(int dtype, const void* QKV, int64_t ldq, void* O, i
   const float scale = 1.0f / sqrtf((float)head_dim);
   const bool al = (ldq % 8 == 0) && (ldo % 4 == 0) && ((uintptr_t)QKV % 16 == 0) && ((uintptr_t)O % 8 == 0);
   const int variant = al ? sdp_attention_variant(dtype, N, n_head, head_dim, mask != nullptr) : 0;
+  if (variant == 5) {
+    const float *gq = norm ? q_gamma : nullptr, *bq = norm ? q_beta : nullptr;
+    const float *gk = norm ? k_gamma : nullptr, *bk = norm ? k_beta : nullptr;
+    switch (head_dim / 32) {
+      case 1: return launch_attn_fs<1>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      case 2: return launch_attn_fs<2>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      case 3: return launch_attn_fs<3>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      default: return launch_attn_fs<4>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+    }
+  }
   if (variant == 4) {
     const float *gq = norm ? q_gamma : nullptr, *bq = norm ? q_beta : nullptr;
     const float *gk = norm ? k_gamma : nullptr, *bk = norm ? k_beta : nullptr;

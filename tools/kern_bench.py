@@ -1,6 +1,6 @@
-"""Microbenchmark of the non-GEMM kernels at SdP-Net-M shapes (bs=256, bf16).
+"""Microbenchmark of the non-GEMM kernels at SdP-Net-M (bs=256) or -XL (bs=512) shapes, bf16.
 
-  python tools/kern_bench.py [--reps 20] [--only dw,attn,ln,stats]
+  python tools/kern_bench.py [--reps 20] [--only dw,attn,ln,stats] [--shape m|xl] [--attn-kerns 2,3,4,5]
 """
 import argparse
 import os
@@ -29,10 +29,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="dw,attn,ln,stats")
-    ap.add_argument("--attn-kerns", default="2,3,4")
+    ap.add_argument("--attn-kerns", default="2,3,4,5")
+    ap.add_argument("--shape", default="m", choices=["m", "xl"], help="M: bs 256, 14x14 patches; XL: bs 512, 16x16")
     args = ap.parse_args()
     dev, bf = "cuda", torch.bfloat16
-    B, R, H, W, C, heads = 256, 4, 14, 14, 768, 8
+    B, R, H, W, C, heads = (256, 4, 14, 14, 768, 8) if args.shape == "m" else (512, 4, 16, 16, 768, 8)
     P, N = H * W, R + H * W
     only = args.only.split(",")
     tok = torch.randn(B * N, C, device=dev).to(bf)
