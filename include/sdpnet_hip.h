@@ -96,7 +96,7 @@ int sdp_gemm_set_fast_kernel(int k);
 int sdp_gemm_set_store_policy(int nt);
 
 /* Epilogue specialisation of the whole-line fast-GEMM epilogue: 1 (default) = the model's
- * flag combinations (LN fold + bias; residual + LN partials [+ bias]) with no / GELU
+ * flag combinations (plain; bias; LN fold + bias; residual + LN partials [+ bias]) with no / GELU
  * activation run an instantiation with the flags fixed at compile time (packed residual add,
  * dot2 partial sums); 0 = the run-time-flag epilogue for every call.  Outputs are
  * bit-identical; the emitted LN partials agree to fp32 rounding.  Returns the previous value. */
@@ -246,6 +246,11 @@ int sdp_attn_set_per_cu(int n);
  */
 int sdp_patchify(int dtype_in, const void* img, int dtype_out, void* out, int B, int Hi, int Wi,
                  int p, int Kpad, void* stream);
+
+/* Adjoint of sdp_patchify (the ConvPatcher input gradient, layers.py:34-42 in training):
+ * image [B,3,Hi,Wi] <- rows [B*(Hi/p)*(Wi/p), Kpad]; pixels no patch covers get 0. */
+int sdp_unpatchify(int dtype_in, const void* rows, int dtype_out, void* img, int B, int Hi, int Wi,
+                   int p, int Kpad, void* stream);
 
 /* T[h*W + w][c] = Eh[h][c] + Ew[w][c]   (EmbeddingLayer, layers.py:157-163). */
 int sdp_pos_table(const float* eh, const float* ew, float* out, int H, int W, int C, void* stream);

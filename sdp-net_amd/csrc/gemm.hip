@@ -1607,8 +1607,8 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
       e.res_bytes = (uint32_t)rb;
       e.part_bytes = (uint32_t)pb;
       const bool spec = g_epi_spec && !ws && fk == 14 && small && !e.nt_store && (ak == ACT_NONE || ak == ACT_GELU) &&
-                        (fl == (fast::EF_BIAS | fast::EF_LN) || fl == (fast::EF_RESID | fast::EF_PART) ||
-                         fl == (fast::EF_BIAS | fast::EF_RESID | fast::EF_PART));
+                        (fl == 0 || fl == fast::EF_BIAS || fl == (fast::EF_BIAS | fast::EF_LN) ||
+                         fl == (fast::EF_RESID | fast::EF_PART) || fl == (fast::EF_BIAS | fast::EF_RESID | fast::EF_PART));
       if (spec) {
 #define SDP_8PH_DP(A, E)                                                                                   \
   do {                                                                                                      \
@@ -1623,6 +1623,8 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
   do {                                                                          \
     if (fl == (fast::EF_BIAS | fast::EF_LN)) SDP_8PH_DP(A, 16 + 3);             \
     else if (fl == (fast::EF_RESID | fast::EF_PART)) SDP_8PH_DP(A, 16 + 12);    \
+    else if (fl == 0) SDP_8PH_DP(A, 16 + 0);                                    \
+    else if (fl == fast::EF_BIAS) SDP_8PH_DP(A, 16 + 1);                        \
     else SDP_8PH_DP(A, 16 + 13);                                                \
   } while (0)
         if (ak == ACT_NONE) SDP_8PH_FL(ACT_NONE);

@@ -72,6 +72,50 @@ extern "C" int sdp_patchify(int dtype_in, const void* img, int dtype_out, void* 
   return SDP_CHECK_LAUNCH();
 }
 
+// adjoint of patchify_k: image gradient [B,3,Hi,Wi] from the patch-row gradient [B*Hp*Wp, Kpad]
+// (stride = kernel: every pixel belongs to at most one patch; the rows / columns past Hp*p / Wp*p
+// that the stride-p convolution drops get 0).  One thread per image element.
+template <typename TI, typename TO>
+__global__ void unpatchify_k(const TI* __restrict__ rows, TO* __restrict__ img, int B, int Hi, int Wi, int p, int Hp,
+                             int Wp, int Kpad) {
+  const int64_t total = (int64_t)B * 3 * Hi * Wi;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(idx % Wi);
+    const int64_t t = idx / Wi;
+    const int y = (int)(t % Hi);
+    const int64_t bc = t / Hi;
+    const int c = (int)(bc % 3), b = (int)(bc / 3);
+    float v = 0.f;
+    if (y < Hp * p && x < Wp * p) {
+      const int ph = y / p, i = y - ph * p, pw = x / p, j = x - pw * p;
+      v = to_f<TI>(rows[(((int64_t)b * Hp + ph) * Wp + pw) * Kpad + c * p * p + i * p + j]);
+    }
+    img[idx] = from_f<TO>(v);
+  }
+}
+
+extern "C" int sdp_unpatchify(int dtype_in, const void* rows, int dtype_out, void* img, int B, int Hi, int Wi, int p,
+                              int Kpad, void* stream) {
+  if (!rows || !img || p <= 0 || Kpad < 3 * p * p || B < 0 || Hi < 0 || Wi < 0) return (int)hipErrorInvalidValue;
+  const int Hp = Hi / p, Wp = Wi / p;
+  const int64_t total = (int64_t)B * 3 * Hi * Wi;
+  if (total == 0) return 0;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_in == 1 && dtype_out == 0)
+    hipLaunchKernelGGL((unpatchify_k<bf16_t, float>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)rows, (float*)img, B, Hi, Wi, p, Hp, Wp, Kpad);
+  else if (dtype_in == 0 && dtype_out == 0)
+    hipLaunchKernelGGL((unpatchify_k<float, float>), dim3(blocks), dim3(256), 0, s, (const float*)rows, (float*)img, B, Hi, Wi, p, Hp, Wp, Kpad);
+  else if (dtype_in == 1 && dtype_out == 1)
+    hipLaunchKernelGGL((unpatchify_k<bf16_t, bf16_t>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)rows, (bf16_t*)img, B, Hi, Wi, p, Hp, Wp, Kpad);
+  else if (dtype_in == 0 && dtype_out == 1)
+    hipLaunchKernelGGL((unpatchify_k<float, bf16_t>), dim3(blocks), dim3(256), 0, s, (const float*)rows, (bf16_t*)img, B, Hi, Wi, p, Hp, Wp, Kpad);
+  else
+    return (int)hipErrorInvalidValue;
+  return SDP_CHECK_LAUNCH();
+}
+
 __global__ void pos_table_k(const float* __restrict__ eh, const float* __restrict__ ew, float* __restrict__ out, int H,
                             int W, int C) {
   const int64_t total = (int64_t)H * W * C;

@@ -182,6 +182,9 @@ class MainModel(SdPModel):
                 # (SDPNET_COMPILE_TRAIN_OPS=model: sdpnet_ops.train_forward / train_backward)
                 if return_raw_outputs:
                     raise NotImplementedError("sdpnet training path returns logits only")
+                if x.requires_grad:  # the compiled ops give the image no gradient: refuse, never drop it
+                    raise NotImplementedError("sdpnet compiled training: no gradient into the input image "
+                                              "(the eager training path computes it)")
                 code = sdpnet_ops.DTYPE_CODES[compute_dtype(x, self)]
                 if _COMPILE_TRAIN_OPS == "model":
                     params = [p for p in self.parameters()]

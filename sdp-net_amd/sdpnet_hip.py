@@ -68,6 +68,7 @@ _SIGS = {
     "sdp_attention_variant": ([_i32, _i32, _i32, _i32, _i32], _i32),
     "sdp_attention_set_kernel": ([_i32], _i32),
     "sdp_patchify": ([_i32, _vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp], _i32),
+    "sdp_unpatchify": ([_i32, _vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp], _i32),
     "sdp_pos_table": ([_vp, _vp, _vp, _i32, _i32, _i32, _vp], _i32),
     "sdp_avgpool_table_bwd": ([_vp, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _vp], _i32),
     "sdp_avgpool_table": ([_vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp], _i32),
@@ -403,6 +404,17 @@ def patchify(img: torch.Tensor, out: torch.Tensor, p: int, kpad: int):
     rc = lib().sdp_patchify(dcode(img.dtype), img.data_ptr(), dcode(out.dtype), out.data_ptr(), B, Hi, Wi, p, kpad,
                             _stream(out))
     _check(rc, "patchify")
+
+
+def unpatchify(rows: torch.Tensor, img: torch.Tensor, p: int, kpad: int):
+    """img [B, 3, Hi, Wi] = the adjoint of patchify applied to rows [B*(Hi/p)*(Wi/p), kpad]."""
+    _need_cuda(rows, img)
+    _req(img.is_contiguous() and img.dim() == 4 and img.shape[1] == 3 and rows.is_contiguous())
+    B, _, Hi, Wi = img.shape
+    _req(rows.shape[0] == B * (Hi // p) * (Wi // p) and rows.shape[1] == kpad, "unpatchify rows shape")
+    rc = lib().sdp_unpatchify(dcode(rows.dtype), rows.data_ptr(), dcode(img.dtype), img.data_ptr(), B, Hi, Wi, p, kpad,
+                              _stream(img))
+    _check(rc, "unpatchify")
 
 
 def pos_table(eh: torch.Tensor, ew: torch.Tensor, out: torch.Tensor, H: int, W: int, C: int):

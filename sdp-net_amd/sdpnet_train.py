@@ -754,9 +754,12 @@ class _EmbedFn(torch.autograd.Function):
         table, R2 = emb._register_rows(nreg_arg)
         if R:
             sp.copy_rows(table.contiguous(), C, 0, tok, C, N * C, B, R, C)
+        # the image gradient (an input that requires grad, e.g. input-gradient attacks) needs w and the
+        # image geometry; the compiled per-layer path never asks for it (compiled_train_forward refuses)
+        need_dx = bool(getattr(ctx, "needs_input_grad", (False,))[0])
         ctx.st = dict(patches=patches, geo=(B, R, Hp, Wp, C, P, N, p, kp), dt=dt, sdt=sdt, conv_emb=conv_emb, act=act, z=z,
                       nrow_eh=None if conv_emb else eh.shape[0], nrow_ew=None if conv_emb else ew.shape[0],
-                      nreg=ereg.shape[0], wshape=wp.shape)
+                      nreg=ereg.shape[0], wshape=wp.shape, w=w if need_dx else None, img=(x.shape, x.dtype))
         return tok
 
     @staticmethod
@@ -771,6 +774,10 @@ class _EmbedFn(torch.autograd.Function):
             sp.act_bwd(S["z"], dimg, dimg, B * P, C, S["act"])
         dconv = dimg if sdt == dt else _dense_copy(_dense(dimg), B * P, C, dt)
         gw = _wgrad(dconv, S["patches"])[:, : 3 * p * p].contiguous().view(S["wshape"])
+        dx = None
+        if S["w"] is not None:  # the patch conv's input gradient: dpatches = dconv . W, then col2im
+            dx = _empty(S["img"][0], S["img"][1], dev)
+            sp.unpatchify(_dgrad(dconv, S["w"]), dx, p, kp)
         geh = gew = None
         if not S["conv_emb"]:
             dpos = _empty((P, C), torch.float32, dev)
@@ -784,7 +791,7 @@ class _EmbedFn(torch.autograd.Function):
             off = 1 if S["conv_emb"] else 0  # ConvEmbedding takes Embedding rows 1..R (layers.py:206)
             sp.seg_colsum(dtok, greg[off:], R, B, 1, N, C)
         ctx.st = None
-        return None, None, None, None, gw, geh, gew, greg
+        return dx, None, None, None, gw, geh, gew, greg
 
 
 # ---------------------------------------------------------------------------
@@ -1061,23 +1068,26 @@ class _PatchFn(torch.autograd.Function):
         rows = _linear(patches, wm, None, dt)
         out = _empty((B, C, Hp, Wp), dt, x.device)
         sp.rows_to_nchw(_dense(rows), out)
-        ctx.st = (patches, w.shape, 3 * p * p, dt)
+        need_dx = ctx.needs_input_grad[0]
+        ctx.st = (patches, w.shape, 3 * p * p, dt, wm if need_dx else None, (x.shape, x.dtype), p, kp)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        patches, wshape, k, dt = ctx.st
+        patches, wshape, k, dt, wm, (xshape, xdt), p, kp = ctx.st
         B, C, Hp, Wp = dout.shape
         dr = _empty((B * Hp * Wp, C), dt, dout.device)
         sp.nchw_to_rows(dout.contiguous(), _dense(dr))
         gw = _wgrad(dr, patches)[:, :k].contiguous().view(wshape)
+        dx = None
+        if wm is not None:  # input gradient: dpatches = dY . W (rows), then the adjoint of patchify
+            dx = _empty(xshape, xdt, dout.device)
+            sp.unpatchify(_dgrad(dr, wm), dx, p, kp)
         ctx.st = None
-        return None, gw, None, None
+        return dx, gw, None, None
 
 
 def train_patcher(pat, x: torch.Tensor) -> torch.Tensor:
-    if x.requires_grad:
-        raise NotImplementedError("sdpnet training path: no gradient into the input image of ConvPatcher")
     return _PatchFn.apply(x, pat.conv.weight, pat, compute_dtype(x, pat))
 
 
@@ -1185,8 +1195,8 @@ def _train_forward(model, x: torch.Tensor, num_registers: int, return_raw_output
     N = R + Hp * Wp
     C = model.conv_init.conv.out_channels
     rng = _RNG()
-    xin = x if x.dtype == dt else as_dtype(x, dt)
-    tok = _EmbedFn.apply(xin, (B, R, Hp, Wp, num_registers, stream_dtype(dt, C)), model, dt, model.conv_init.conv.weight, eh, ew,
+    # the image goes in as is (patchify converts to the compute dtype), so a gradient reaches it
+    tok = _EmbedFn.apply(x, (B, R, Hp, Wp, num_registers, stream_dtype(dt, C)), model, dt, model.conv_init.conv.weight, eh, ew,
                          emb.register_embedding_layer.weight)
 
     def enc(t, e):
@@ -1412,7 +1422,7 @@ def layer_backward(rec, g: torch.Tensor):
 
 def compiled_train_forward(model, x: torch.Tensor, num_registers: int, dtype_code: int) -> torch.Tensor:
     """The training forward as a chain of sdpnet::train_layer ops (traced by Dynamo)."""
-    t = x
+    t = x  # (MainModel.forward refuses an image that requires grad on this path)
     B = x.shape[0]
     for i, (kind, mod) in enumerate(train_layers(model)):
         params = [q for q in layer_params(model, kind, mod) if q is not None]

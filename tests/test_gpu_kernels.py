@@ -470,7 +470,7 @@ def test_gemm_emits_row_partials(kern, M, N, K):
 
 
 @pytest.mark.parametrize("act", [0, 1])
-@pytest.mark.parametrize("combo", ["ln_bias", "resid_part", "bias_resid_part"])
+@pytest.mark.parametrize("combo", ["ln_bias", "resid_part", "bias_resid_part", "plain", "bias"])
 @pytest.mark.parametrize("M,N,K", [(25088, 768, 768), (1003, 3072, 768), (70001, 768, 3072), (300, 2304, 768),
                                    (513, 320, 128)])
 def test_gemm_specialised_epilogue_bit_identical(act, combo, M, N, K):
@@ -483,7 +483,8 @@ def test_gemm_specialised_epilogue_bit_identical(act, combo, M, N, K):
     Nt = R + P
     x = rnd(Mt, K, dtype=BF, seed=81)
     w = rnd(N, K, dtype=BF, seed=82, scale=0.05)
-    b = rnd(N, seed=83) if combo != "resid_part" else None
+    b = rnd(N, seed=83) if combo in ("ln_bias", "bias", "bias_resid_part") else None
+    has_r = combo in ("resid_part", "bias_resid_part")
     tok0 = rnd(B_ * Nt, N, dtype=BF, seed=84)
     nch = N // 64
     ln = None
@@ -501,15 +502,15 @@ def test_gemm_specialised_epilogue_bit_identical(act, combo, M, N, K):
         try:
             tok = tok0.clone()
             img = sp.Rows(tok, N, P, Nt, R)
-            part = torch.full((B_ * Nt, nch, 2), float("nan"), device=DEV) if combo != "ln_bias" else None
-            resid = img if combo != "ln_bias" else None
+            part = torch.full((B_ * Nt, nch, 2), float("nan"), device=DEV) if has_r else None
+            resid = img if has_r else None
             sp.gemm(sp.dense(x), w, img, Mt, N, K, bias=b, resid=resid, act=act, ln=ln, part=part)
             torch.cuda.synchronize()
             outs.append((tok, part))
         finally:
             sp.lib().sdp_gemm_set_epi_spec(old)
     assert torch.equal(outs[0][0], outs[1][0]), "specialised epilogue output differs"
-    if combo != "ln_bias":
+    if has_r:
         p0, p1 = outs[0][1].view(B_, Nt, nch, 2), outs[1][1].view(B_, Nt, nch, 2)
         assert torch.isnan(p1[:, :R]).all()  # register rows untouched
         close(p1[:, R:, :, 0], p0[:, R:, :, 0], torch.float32, rel=1e-5, what="partial mean")

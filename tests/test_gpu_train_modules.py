@@ -175,9 +175,10 @@ def test_embedding_layers_patcher_and_heads_train_mode_match_oracle_autograd():
     pt = ConvPatcher(64, 16)
     psd = _sd(pt, 11)
     pt = pt.to(DEV).train()
-    img = torch.randn(2, 3, 64, 48, generator=torch.Generator().manual_seed(2))
-    _check(pt, [pt(img.to(DEV))], [orc.conv_patcher(img, {"conv_init.conv.weight": psd["conv.weight"]})], psd, "",
-           [], [])
+    img = torch.randn(2, 3, 70, 48, generator=torch.Generator().manual_seed(2))  # 70: 6 rows no patch covers
+    imgd, imgc = _leaf(img.to(DEV)), _leaf(img)
+    _check(pt, [pt(imgd)], [orc.conv_patcher(imgc, {"conv_init.conv.weight": psd["conv.weight"]})], psd, "",
+           [imgd], [imgc])
     for from_reg in (True, False):
         head = ClassificationHead(64, 10, from_register=from_reg, dropout=0.0, bias=True)
         hsd = _sd(head, 10, "output_head.")

@@ -382,7 +382,8 @@ def test_full_size_row_counts_against_oracle():
 def test_train_mode_embedding_activation_and_raw_outputs(conv_emb):
     """Train-mode surface the reference computes (layers.py:157-168 / :205, model.py:147-148):
     an embedding activation (GELU on x + pos) and return_raw_outputs=True, whose outputs carry
-    gradients back into the model.  fp32 gradients vs autograd through the oracle."""
+    gradients back into the model and into the input image (the patch conv's input gradient,
+    sdp_unpatchify).  fp32 gradients vs autograd through the oracle."""
     import model as ours
     import sdpnet_train
     cfg = dict(embedding_dim=64, num_blocks=1, n_head=4, conv_kernel_size=7, patch_size=16, max_image_size=[16, 16],
@@ -400,16 +401,20 @@ def test_train_mode_embedding_activation_and_raw_outputs(conv_emb):
             + 0.5 * regs.float().abs().mean()
 
     osd = {k: v.clone().requires_grad_(v.is_floating_point()) for k, v in sd.items()}
-    lo, xo, ro = orc.forward.__wrapped__(x, osd, cfg, return_raw_outputs=True)
+    xr = x.clone().requires_grad_(True)
+    lo, xo, ro = orc.forward.__wrapped__(xr, osd, cfg, return_raw_outputs=True)
     objective(lo, xo, ro).backward()
     m = m.to(DEV).train()
-    lg, xg, rg = m(x.to(DEV), return_raw_outputs=True)
+    xd = x.to(DEV).requires_grad_(True)
+    lg, xg, rg = m(xd, return_raw_outputs=True)
     assert xg.shape == xo.shape and rg.shape == ro.shape
     assert float((xg.cpu() - xo.detach()).abs().max()) <= 1e-4
     objective(lg, xg, rg).backward()
     fl = 1e-3 * max(float(osd[k].grad.abs().max()) for k, _ in m.named_parameters())
     worst = max((_rel(p.grad.cpu().numpy(), osd[k].grad.numpy(), fl), k) for k, p in m.named_parameters())
     assert worst[0] <= 1e-4, worst
+    assert xd.grad is not None and xd.grad.shape == xr.grad.shape
+    assert _rel(xd.grad.cpu().numpy(), xr.grad.numpy(), 1e-3 * float(xr.grad.abs().max())) <= 1e-4
 
 
 XL_TRAIN_CFG = dict(embedding_dim=768, num_blocks=2, n_head=8, conv_kernel_size=7, patch_size=14,
