@@ -51,14 +51,49 @@ __global__ void patchify_k(const TI* __restrict__ img, TO* __restrict__ out, int
   }
 }
 
+// One workgroup per patch row (b, ph, pw): the row's (b, ph, pw) decomposition is uniform and the
+// per-column image offset is 32-bit arithmetic on the column alone (the grid-stride form above
+// divides a 64-bit index five times per element).  Column-fastest threads: the loads walk the
+// patch's pixel rows (p contiguous floats each), the stores are one contiguous row.
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void patchify_rows_k(const TI* __restrict__ img, TO* __restrict__ out, int Hi,
+                                                       int Wi, int p, int Hp, int Wp, int Kpad) {
+  const int row = blockIdx.x;
+  const int pw = row % Wp, t = row / Wp, ph = t % Hp, b = t / Hp;
+  const TI* src = img + (int64_t)b * 3 * Hi * Wi + (int64_t)(ph * p) * Wi + pw * p;
+  TO* dst = out + (int64_t)row * Kpad;
+  const int pp = p * p;
+  for (int col = threadIdx.x; col < Kpad; col += 256) {
+    float v = 0.f;
+    if (col < 3 * pp) {
+      const int c = col / pp, ij = col - c * pp, i = ij / p, j = ij - i * p;
+      v = to_f<TI>(src[(c * Hi + i) * Wi + j]);
+    }
+    dst[col] = from_f<TO>(v);
+  }
+}
+
 extern "C" int sdp_patchify(int dtype_in, const void* img, int dtype_out, void* out, int B, int Hi, int Wi, int p,
                             int Kpad, void* stream) {
   if (!img || !out || p <= 0 || Kpad < 3 * p * p) return (int)hipErrorInvalidValue;
   const int Hp = Hi / p, Wp = Wi / p;
   const int64_t total = (int64_t)B * Hp * Wp * Kpad;
   if (total == 0) return 0;
-  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
   hipStream_t s = (hipStream_t)stream;
+  const int64_t rows = (int64_t)B * Hp * Wp;
+  if (rows < (1ll << 31) && (int64_t)3 * Hi * Wi < (1ll << 31)) {
+#define SDP_PATCH_ROWS(TI, TO)                                                                                   \
+  hipLaunchKernelGGL((patchify_rows_k<TI, TO>), dim3((unsigned)rows), dim3(256), 0, s, (const TI*)img, (TO*)out, \
+                     Hi, Wi, p, Hp, Wp, Kpad)
+    if (dtype_in == 0 && dtype_out == 1) SDP_PATCH_ROWS(float, bf16_t);
+    else if (dtype_in == 0 && dtype_out == 0) SDP_PATCH_ROWS(float, float);
+    else if (dtype_in == 1 && dtype_out == 1) SDP_PATCH_ROWS(bf16_t, bf16_t);
+    else if (dtype_in == 1 && dtype_out == 0) SDP_PATCH_ROWS(bf16_t, float);
+    else return (int)hipErrorInvalidValue;
+#undef SDP_PATCH_ROWS
+    return SDP_CHECK_LAUNCH();
+  }
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
   if (dtype_in == 0 && dtype_out == 1)
     hipLaunchKernelGGL((patchify_k<float, bf16_t>), dim3(blocks), dim3(256), 0, s, (const float*)img, (bf16_t*)out, B, Hi, Wi, p, Hp, Wp, Kpad);
   else if (dtype_in == 0 && dtype_out == 0)

@@ -2,7 +2,7 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
-timeout -k 10 400 $T tests/test_gpu_kernels.py -k "specialised or kloop or attention" > gpurun_out/r4_spec2_tests.log 2>&1 || { tail -30 gpurun_out/r4_spec2_tests.log; exit 1; }
+timeout -k 10 400 $T tests/test_gpu_kernels.py -k "specialised or kloop or attention or patchify" > gpurun_out/r4_spec2_tests.log 2>&1 || { tail -30 gpurun_out/r4_spec2_tests.log; exit 1; }
 tail -1 gpurun_out/r4_spec2_tests.log
 timeout -k 10 400 $T tests/test_gpu_train_modules.py tests/test_train.py -k "patcher or embedding_activation or compile" > gpurun_out/r4_spec2_tests2.log 2>&1 || { tail -30 gpurun_out/r4_spec2_tests2.log; exit 1; }
 tail -1 gpurun_out/r4_spec2_tests2.log
