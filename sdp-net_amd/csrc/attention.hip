@@ -300,7 +300,10 @@ __global__ __launch_bounds__(640) void attn_fa_bf16(const bf16_t* __restrict__ Q
 }
 
 #ifndef ATTN_CH
-#define ATTN_CH 4  // key tiles per softmax chunk of attn_qtile_chunked
+// key tiles per softmax chunk of attn_qtile_chunked for hd <= 96: 7 = the whole key range at
+// N <= 224 in one chunk (one max, no rescale of O), N <= 256 in two; 111.7 vs 117.5 us at the M
+// shape with 4 (tools/r4_ch.sh).  hd = 128 keeps 4 (register budget).
+#define ATTN_CH 7
 #endif
 // ---------------------------------------------------------------------------
 // Per-wave pieces of the two-workgroup / persistent flash kernels (hd = 32*HDT).
@@ -1007,11 +1010,11 @@ __global__ __launch_bounds__(256, 2) void attn_fa4_bf16(const bf16_t* __restrict
     bf16_t* obase = O + (int64_t)b * N * ldo + hh * HD;
     // slot 0 (query tile w), prefetching slot 1's Q
     if (norm) attn_norm_q<HDT>(qa, ok0, hf, prm, prm + HD, eps);
-    attn_qtile_chunked<HDT, NKT, ATTN_CH>(Ks, Vs, qa, N, scale_log2, lane, ok0 ? obase + q0 * ldo : nullptr,
+    attn_qtile_chunked<HDT, NKT, (HDT <= 3 ? ATTN_CH : 4)>(Ks, Vs, qa, N, scale_log2, lane, ok0 ? obase + q0 * ldo : nullptr,
                                           qkv_base(pair) + off1, qb);
     // slot 1 (query tile w + 4), prefetching the next pair's slot 0
     if (norm) attn_norm_q<HDT>(qb, ok1, hf, prm, prm + HD, eps);
-    attn_qtile_chunked<HDT, NKT, ATTN_CH>(Ks, Vs, qb, N, scale_log2, lane, ok1 ? obase + q1 * ldo : nullptr,
+    attn_qtile_chunked<HDT, NKT, (HDT <= 3 ? ATTN_CH : 4)>(Ks, Vs, qb, N, scale_log2, lane, ok1 ? obase + q1 * ldo : nullptr,
                                           qkv_base(nxt) + off0, qa);
     pair = nxt;
     __syncthreads();  // every wave is done with K / V before the next pair's DMA
