@@ -1063,15 +1063,22 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     // re-staged from phase p + 1.  Schedule (tile t): P0 issues S3(t+1), P1 issues S1(t+2) S2(t+2);
     // P0 waits vmcnt(8) = retires S3(t) (read in P1), P1 waits vmcnt(8) = retires S1(t+1) S2(t+1)
     // (read in P0 of t+1): two phases (~one K-tile of MFMA) between issue and retirement.
+#ifndef SDP_PH2_PRIO
+// 1 (default): static priority for wave group 1 (the younger half, the arbitration loser on every
+// segment), no per-section flips: M forward 10,099 / 10,107 -> 10,158 / 10,162 img/s over
+// per-section flips (0); no s_setprio at all (2) 10,074 / 10,101 (interleaved, tools/r4_prio.sh)
+#define SDP_PH2_PRIO 1
+#endif
+    if (SDP_PH2_PRIO == 1 && __builtin_amdgcn_readfirstlane(wm) == 1) __builtin_amdgcn_s_setprio(1);
     auto section = [&](auto&& body) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       pstamp();
-      __builtin_amdgcn_s_setprio(1);
+      if (SDP_PH2_PRIO == 0) __builtin_amdgcn_s_setprio(1);
       body();
-      __builtin_amdgcn_s_setprio(0);
+      if (SDP_PH2_PRIO == 0) __builtin_amdgcn_s_setprio(0);
       pstamp();
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();

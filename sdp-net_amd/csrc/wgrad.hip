@@ -179,14 +179,18 @@ __global__ __launch_bounds__(NTHREADS) void gemm_wgrad_8ph(const bf16_t* __restr
       // 2 phases per K-tile (32 MFMAs per section): the schedule and retire counts of
       // gemm_bf16_8ph's 2-phase loop (csrc/gemm.hip), which reads its staged regions in the same
       // phases (w0, w1, x half 0 in P0; x half 1 in P1)
+#ifndef SDP_WGRAD_PH2_PRIO
+#define SDP_WGRAD_PH2_PRIO 0  // 1: static priority for wave group 1 (gemm_bf16_8ph's PH2 default)
+#endif
+      if (SDP_WGRAD_PH2_PRIO == 1 && __builtin_amdgcn_readfirstlane(wm) == 1) __builtin_amdgcn_s_setprio(1);
       auto section = [&](auto&& body) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
+        if (SDP_WGRAD_PH2_PRIO == 0) __builtin_amdgcn_s_setprio(1);
         body();
-        __builtin_amdgcn_s_setprio(0);
+        if (SDP_WGRAD_PH2_PRIO == 0) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
