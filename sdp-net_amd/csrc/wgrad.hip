@@ -180,7 +180,10 @@ __global__ __launch_bounds__(NTHREADS) void gemm_wgrad_8ph(const bf16_t* __restr
       // gemm_bf16_8ph's 2-phase loop (csrc/gemm.hip), which reads its staged regions in the same
       // phases (w0, w1, x half 0 in P0; x half 1 in P1)
 #ifndef SDP_WGRAD_PH2_PRIO
-#define SDP_WGRAD_PH2_PRIO 0  // 1: static priority for wave group 1 (gemm_bf16_8ph's PH2 default)
+// 1 (default): static priority for wave group 1, as gemm_bf16_8ph's PH2 loop; XL bs120 training
+// 1,045 / 1,059 img/s (both kernels flipping per section) -> 1,054 / 1,063 (GEMM static) ->
+// 1,064 / 1,059 (both static), interleaved on one box (tools/r4_prio2.sh); 0 = per-section flips
+#define SDP_WGRAD_PH2_PRIO 1
 #endif
       if (SDP_WGRAD_PH2_PRIO == 1 && __builtin_amdgcn_readfirstlane(wm) == 1) __builtin_amdgcn_s_setprio(1);
       auto section = [&](auto&& body) {
