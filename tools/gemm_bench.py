@@ -39,9 +39,9 @@ def main():
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--kernels", default="14", help="bf16 fast kernel ids to A/B (9, 14)")
     ap.add_argument("--exact-gelu", default="0", help="GELU forms to A/B (0 tanh form, 1 exact erf)")
-    ap.add_argument("--schedules", default="1", help="tile schedules to A/B (0 data-parallel, 1 stream-K)")
+    ap.add_argument("--schedules", default="0", help="tile schedules to A/B (0 data-parallel, 1 stream-K)")
     ap.add_argument("--epi-spec", default="1", help="epilogue specialisation A/B (0 run-time flags, 1 compile-time)")
-    ap.add_argument("--kloop", default="4", help="main-loop phases per K-tile A/B (4, 2)")
+    ap.add_argument("--kloop", default="2", help="main-loop phases per K-tile A/B (4, 2)")
     ap.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) as a yardstick")
     args = ap.parse_args()
 
