@@ -993,12 +993,14 @@ static int launch_dw3(int variant, int k, const void* X, int64_t ldx, RowMap xm,
   else                                                                                                           \
     hipLaunchKernelGGL((dwconv3_mfma<KS, NT, false, PF>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx, xm, \
                        stats, lg, lb, Wt, bias, (bf16_t*)Y, ldy, ym, B, H, W, C, ncg, ipb, nunits)
-  // 16 waves x 2 channels, 3 images in flight
+  // 16 waves x 2 channels, 2 images in flight (k = 7 at the M shape: 1 / 2 / 3 / 4 images give
+  // 53.4 / 51.2-51.5 / 54.4 / 55.2 us alone and M forward 10,212 / 10,255 / 10,213 / 10,201 img/s,
+  // interleaved means, tools/r4_pf.sh)
   (void)variant;
   switch (k) {
-    case 3: SDP_DW3(3, 1024, 3); break;
-    case 5: SDP_DW3(5, 1024, 3); break;
-    case 7: SDP_DW3(7, 1024, 3); break;
+    case 3: SDP_DW3(3, 1024, 2); break;
+    case 5: SDP_DW3(5, 1024, 2); break;
+    case 7: SDP_DW3(7, 1024, 2); break;
     default: return -1;
   }
 #undef SDP_DW3
