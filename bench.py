@@ -1,6 +1,6 @@
 """SdP-Net forward benchmark on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N --steps K --warmup W] [--config m|xl]
+  python bench.py [--gpus N --steps K --warmup W] [--config m|xl|xl_train] [--no-secondary]
 
 --gpus N > 1 started outside torch.distributed.run re-launches itself as a CHILD
 `python -m torch.distributed.run --nproc-per-node N ... bench.py ...` (before any
@@ -10,20 +10,29 @@ per-rank devices.  --dry-run runs the same launch / barrier / max-over-ranks
 timing path on CPU with gloo and a trivial step (launcher test; no model).
 
 Workload (BASELINE.json configs[1]): SdP-Net-M (12 blocks, d=768, patch 16,
-canonical config SURVEY.md §0) bf16 eval forward, batch 256 synthetic N(0,1)
-224x224 images per GPU, random-init weights (reference init), inputs resident in
-HBM before timing.  A step = one full forward of one batch (logits), replayed
-from a HIP graph captured after warmup.  Multi-GPU: one process per GPU, each
-its own independent batch shard (weak scaling), no data-path collective; barrier
-+ max-over-ranks timing only.
+canonical config SURVEY.md §0) bf16 eval forward in the reference's form --
+an fp32 batch under torch.autocast("cuda", bfloat16) (training_tools.py:85) --
+256 synthetic N(0,1) 224x224 images per GPU, random-init weights (reference
+init), inputs resident in HBM before timing.  A step = one full forward of one
+batch (logits), replayed from a HIP graph captured after warmup.  Multi-GPU: one
+process per GPU, each its own independent batch shard (weak scaling), no
+data-path collective; barrier + max-over-ranks timing only.
+
+Integrity: the bench times the product library only.  It refuses a diagnostic
+build (sdp_build_info() != 0: kernel-skip or stamp code compiled in) and a
+non-zero kernel-skip mask, and records every SDPNET_* environment variable
+(`config.knobs`, empty in a default run) and the loaded library's md5.
 
 Also reported on the same JSON line:
   roofline     — dominant kernel (the bf16 fast GEMM, ~98 % of FLOPs): algorithmic
-                 FLOPs of its launches / their HIP-event durations (on the launch
-                 stream), vs the dense bf16 MFMA peak.
+                 FLOPs per step / the union of its launch intervals in a replay of
+                 the timed schedule, vs the dense bf16 MFMA peak.
+  secondary    — (N=1, default on) the other single-GPU BASELINE configs timed in the
+                 same process after the headline: configs[2] XL bs512 forward and
+                 configs[4]'s per-GPU XL training step (bs 120).
   cpu_baseline — the oracle (the reference's math in stock PyTorch CPU ops,
-                 oracle/sdpnet_oracle.py) on this host's cores, bounded sample,
-                 rank 0 at N=1 only.
+                 oracle/sdpnet_oracle.py) on this host's cores, bounded samples of
+                 M bs16, configs[0] XXS bs4 and XL bs16, rank 0 at N=1 only.
 """
 import argparse
 import json
@@ -95,23 +104,31 @@ def measured_traffic(kernel, config="m"):
     return None, None
 
 
-def cpu_baseline(model_cpu_sd, cfg, seconds=12.0, name="SdP-Net-M"):
+XXS_CFG = dict(M_CFG, embedding_dim=128, num_blocks=7)   # BASELINE.json configs[0]
+
+
+def cpu_baseline(cpu_sds, headline="SdP-Net-M", seconds=10.0):
+    """The oracle's fp32 eval forward on this host's cores: M bs16 for ~`seconds`
+    (the headline's CPU counterpart), configs[0] XXS bs4 for ~5 s, XL bs16 for one batch.
+    cpu_sds: {name: (state_dict, cfg)} built from the same seeded models as the GPU runs."""
     import torch
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import sdpnet_oracle as orc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, len(os.sched_getaffinity(0))))
     torch.set_num_threads(threads)
-    bs = 16
-    x = torch.randn(bs, 3, 224, 224)
-    orc.forward(x[:2], model_cpu_sd, cfg)  # warm
-    n, t0 = 0, time.perf_counter()
-    while True:
-        orc.forward(x, model_cpu_sd, cfg)
-        n += bs
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
+
+    def timed(sd, cfg, bs, secs, min_batches=1):
+        x = torch.randn(bs, 3, 224, 224, generator=torch.Generator().manual_seed(7))
+        orc.forward(x[:1], sd, cfg)  # warm
+        n, t0 = 0, time.perf_counter()
+        while True:
+            orc.forward(x, sd, cfg)
+            n += bs
+            if n >= min_batches * bs and time.perf_counter() - t0 >= secs:
+                break
+        return n, time.perf_counter() - t0
+
     import glob
     ratio = None  # oracle speed / the reference's own CPU forward, measured in the build container
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_cpu_ratio.json")), reverse=True):
@@ -121,10 +138,22 @@ def cpu_baseline(model_cpu_sd, cfg, seconds=12.0, name="SdP-Net-M"):
             break
         except (OSError, ValueError):
             continue
-    return {"value": round(n / dt, 3), "unit": "images/sec", "cores": threads, "kind": "port",
-            "port_vs_reference": ratio,
-            "sample": f"{name} fp32 eval forward, {n} images in batches of {bs}, {dt:.1f} s, "
-                      f"oracle/sdpnet_oracle.py (reference math, stock torch CPU ops)"}
+    plan = [("SdP-Net-M", 16, 0.0), ("SdP-Net-XXS", 4, 5.0), ("SdP-Net-XL", 16, 0.0)]
+    plan = [(nm, bs, seconds if nm == headline else secs) for nm, bs, secs in plan]
+    res = {}
+    for name, bs, secs in plan:
+        if name not in cpu_sds:
+            continue
+        sd, cfg = cpu_sds[name]
+        n, dt = timed(sd, cfg, bs, secs)
+        res[name] = {"value": round(n / dt, 3), "unit": "images/sec", "batch": bs, "images": n,
+                     "seconds": round(dt, 2)}
+    m = res.get(headline)
+    return {"value": m["value"] if m else None, "unit": "images/sec", "cores": threads, "kind": "port",
+            "port_vs_reference": ratio, "per_config": res,
+            "sample": "fp32 eval forward of the oracle (oracle/sdpnet_oracle.py: the reference math in stock torch "
+                      "CPU ops) on this host's cores: %s in batches of 16 for ~%.0f s (value); per_config: configs[0] "
+                      "XXS bs4 for ~5 s, M / XL one batch of 16 unless headline" % (headline, seconds)}
 
 
 def _free_port():
@@ -186,17 +215,39 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
-def train_bench(args, C, world, rank, local):
+def check_library(L, env):
+    """The integrity gate (VERDICT r04 'what's weak' 6): returns the SDPNET_* knobs of this run; refuses
+    (SystemExit) a diagnostic library or a non-zero kernel-skip mask, either of which could leave work
+    out of the timed region.  L: the loaded ctypes library (sdpnet_hip.lib()); env: os.environ."""
+    knobs = {k: v for k, v in sorted(env.items()) if k.startswith("SDPNET_")}
+    flags = int(L.sdp_build_info())
+    if flags:
+        raise SystemExit(f"bench.py: refusing to time a diagnostic library (sdp_build_info() = {flags}: "
+                         "kernel-skip / stamp code compiled in); build the product library (make -C sdp-net_amd/csrc)")
+    mask = int(L.sdp_debug_skip(0))
+    if mask or knobs.get("SDPNET_DEBUG_SKIP", "0").strip() not in ("", "0"):
+        raise SystemExit(f"bench.py: refusing to time with a kernel-skip mask (library mask {mask}, "
+                         f"SDPNET_DEBUG_SKIP={knobs.get('SDPNET_DEBUG_SKIP')!r}): results would be wrong")
+    return knobs
+
+
+def library_record(env=os.environ):
+    import hashlib
+    import sdpnet_hip as sp
+    knobs = check_library(sp.lib(), env)
+    with open(sp.LIB_PATH, "rb") as f:
+        md5 = hashlib.md5(f.read()).hexdigest()
+    return {"knobs": knobs, "lib": os.path.relpath(os.path.realpath(sp.LIB_PATH), REPO), "lib_md5": md5}
+
+
+def train_step_bench(C, B, steps, warmup, dev, world, rank, local, global_batch):
     """BASELINE.json configs[4]: one training step = bf16-autocast forward + label-smoothed CE
     (training_tools.py:85-88) + backward (DDP bucketed gradient all-reduce over RCCL when
     N > 1, training_tools.py:36, :91) + GradScaler unscale / clip_grad_norm_(5) / AdamW
-    (training_tools.py:94-99, fused into one HIP kernel) on each rank's 120 synthetic images."""
+    (training_tools.py:94-99, fused into one HIP kernel) on each rank's B synthetic images.
+    Returns the line's fields (timing = barrier + synchronize on both sides, max over ranks)."""
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
     import model as sdp
     import sdpnet_train
     import sharding
@@ -207,8 +258,6 @@ def train_bench(args, C, world, rank, local):
     if world > 1:
         net = torch.nn.parallel.DistributedDataParallel(m, device_ids=[local])
     opt = sdpnet_train.AdamW(m.parameters(), lr=0.0015, weight_decay=0.05)   # model_config_vit.yaml:49-51
-    lo, hi = sharding.shard_bounds(args.batch * world, world, rank)
-    B = hi - lo
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     x = torch.randn(B, 3, 224, 224, generator=g).to(dev)
     y = torch.randint(0, cfg["output_classes"], (B,), generator=g).to(dev)
@@ -222,7 +271,7 @@ def train_bench(args, C, world, rank, local):
         opt.step(grad_scale=None, max_norm=5.0)  # unscale / inf check / clip / AdamW / scale update
         return loss
 
-    for _ in range(max(1, args.warmup)):
+    for _ in range(max(1, warmup)):
         loss = step()
     torch.cuda.synchronize()
     if world > 1:
@@ -230,31 +279,47 @@ def train_bench(args, C, world, rank, local):
     torch.cuda.synchronize()
     taken0 = float(opt._steps[0])
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = sharding.max_over_ranks(time.perf_counter() - t0, device=dev)
-    total = int(sharding.sum_over_ranks(B * args.steps, device=dev))
+    total = int(sharding.sum_over_ranks(B * steps, device=dev))
     assert torch.isfinite(loss).all()
     # GradScaler skips (inf/nan grads) did no optimizer work: count them, none expected
-    skipped = int(args.steps - (float(opt._steps[0]) - taken0))
+    skipped = int(steps - (float(opt._steps[0]) - taken0))
     assert skipped == 0, f"{skipped} optimizer steps skipped by the GradScaler inside the timed region"
     gf = 3 * flops_per_image(cfg) / 1e9   # forward + dX + dW GEMMs (3x forward)
     value = total / el
     out = {
         "metric": C["metric"], "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3),
+        "steps": steps, "warmup": warmup, "ms_per_step": round(1e3 * el / steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic N(0,1) 224x224 images + random labels resident in HBM; random-init weights",
-        "config": {"workload": C["desc"], "global_batch": args.batch * world, "per_gpu_batch": B,
+        "config": {"workload": C["desc"], "global_batch": global_batch, "per_gpu_batch": B,
                    "parallelism": f"dp{world}" + (" DDP bucketed grad all-reduce over RCCL" if world > 1 else "")},
         "model_flops_per_image_gf": round(gf, 3),
         "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
         "skipped_steps": skipped, "grad_scale": float(opt.scaler[0]),
         "loss": round(float(loss.detach()), 4), "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
     }
+    del m, net, opt, x, y
+    return out
+
+
+def train_bench(args, C, world, rank, local):
+    import torch
+    import torch.distributed as dist
+    import sharding
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    rec = library_record()
+    lo, hi = sharding.shard_bounds(args.batch * world, world, rank)
+    out = train_step_bench(C, hi - lo, args.steps, args.warmup, dev, world, rank, local, args.batch * world)
+    out["config"].update(rec)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -262,112 +327,91 @@ def train_bench(args, C, world, rank, local):
         dist.destroy_process_group()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", choices=sorted(CONFIGS), default="m",
-                    help="m = the BASELINE metric's workload (default); xl = configs[2]")
-    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = the config's: M 256, XL 512)")
-    ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--prof-steps", type=int, default=1, help="forwards per profiled graph replay (roofline)")
-    ap.add_argument("--streams", type=int, default=0, help="sub-batch streams per GPU (0 = model default)")
-    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of the launch + timing path")
-    args = ap.parse_args()
-    C = CONFIGS[args.config]
-    cfg = C["cfg"]
-    if args.batch <= 0:
-        args.batch = C["batch"]
-
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args.gpus))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch N ranks with --gpus N")
-    if args.dry_run:
-        return dry_run(args, world, rank)
-    if C.get("train"):
-        return train_bench(args, C, world, rank, local)
-
+def forward_bench(C, B, steps, warmup, dev, world, rank, streams=0, graph=True, roofline=True, config="m"):
+    """One config's eval forward: an fp32 batch resident in HBM under torch.autocast("cuda", bf16)
+    (the reference's bf16 forward, training_tools.py:85; the patch kernel reads the fp32 image),
+    W warmup forwards, a HIP graph of one forward (both sub-batch streams), K timed replays
+    bracketed by barrier + synchronize, max over ranks.  Returns (fields, cpu state_dict or None)."""
     import torch
     import torch.distributed as dist
-
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    comm_world = dist.get_world_size() if world > 1 else 1
-    if comm_world != world:
-        raise SystemExit(f"bench.py: RCCL world size {comm_world} != {world}")
-    if world > 1:
-        devs = [None] * world
-        dist.all_gather_object(devs, f"rank{rank}:cuda:{local}:{torch.cuda.get_device_name(dev)}")
-    else:
-        devs = [f"rank0:cuda:{local}:{torch.cuda.get_device_name(dev)}"]
-
     import model as sdp
     import sdpnet_hip as sp
     import sharding
-
+    cfg = C["cfg"]
     torch.manual_seed(231424314)  # model_train.py:61
     m = sdp.MainModel.from_dict(**cfg).eval()
-    if args.streams > 0:
-        m.num_streams = args.streams
-    cpu_sd = {k: v.detach().clone() for k, v in m.state_dict().items()} if rank == 0 else None
+    if streams > 0:
+        m.num_streams = streams
+    cpu_sd = {k: v.detach().clone() for k, v in m.state_dict().items()} if rank == 0 and world == 1 else None
     m = m.to(dev)
-    # weak scaling: the global batch is world x per-GPU batch, each rank owns one
-    # contiguous shard (images are independent, no collective on the data path)
-    lo, hi = sharding.shard_bounds(args.batch * world, world, rank)
-    B = hi - lo
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
-    x = torch.randn(B, 3, 224, 224, generator=g).to(dev).to(torch.bfloat16)   # resident in HBM
+    x = torch.randn(B, 3, 224, 224, generator=g).to(dev)   # fp32, resident in HBM
 
     def step():
-        return m(x)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            return m(x)
 
-    for _ in range(max(1, args.warmup)):
+    for _ in range(max(1, warmup)):
         y = step()
     torch.cuda.synchronize()
-    graph = None
-    if not args.no_graph:
+    pgraph = None
+    if graph:
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             step()
         torch.cuda.current_stream().wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        pgraph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(pgraph):
             y = step()
-        graph.replay()
+        pgraph.replay()
         torch.cuda.synchronize()
-    run = graph.replay if graph is not None else step
+    run = pgraph.replay if pgraph is not None else step
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = sharding.max_over_ranks(time.perf_counter() - t0, device=dev)
-    total_imgs = int(sharding.sum_over_ranks(B * args.steps, device=dev))
-    assert torch.isfinite(y.float()).all()
+    total_imgs = int(sharding.sum_over_ranks(B * steps, device=dev))
+    assert y.dtype == torch.bfloat16 and torch.isfinite(y.float()).all()
+    value = total_imgs / el
+    ms_step = 1e3 * el / steps
+    gf = flops_per_image(cfg) / 1e9
+    tokens = (224 // cfg["patch_size"]) ** 2 + min(4, cfg["max_num_registers"])
+    out = {
+        "metric": C["metric"], "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
+        "steps": steps, "warmup": warmup, "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic N(0,1) 224x224 fp32 images resident in HBM, bf16 autocast; random-init weights "
+                "(reference init)",
+        "config": {"workload": C["desc"] + ", torch.autocast bf16 (bf16 storage / fp32 accumulate)"
+                               + (", eager launches" if not graph else ", HIP-graph replay"),
+                   "streams_per_gpu": m._num_streams(B), "per_gpu_batch": B, "image": 224, "tokens": tokens},
+        "model_flops_per_image_gf": round(gf, 3),
+        "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
+    }
+    if roofline:
+        out["roofline"] = gemm_roofline(step, dev, ms_step, config)
+    del pgraph, m, x, y
+    return out, cpu_sd
 
-    # ---- dominant-kernel roofline, measured on the timed schedule itself ------------------
-    # A second graph of the same step (same sub-batch streams, same kernels) is captured with the
-    # library's launch timeline on: every fast-GEMM launch folds its first-workgroup start and
-    # last-workgroup end (device clock, s_memrealtime at 100 MHz) into its own slot, which works
-    # inside a replayed graph where HIP events cannot be recorded.  Per replay: the launch
-    # intervals, their UNION (the wall time the GEMMs occupy in this schedule; two sub-batch
-    # streams overlap GEMMs with each other and with the other kernels) and the replay's own
-    # device-time span.  The timed graph itself has no timeline.
-    prof_steps = max(1, args.prof_steps)
+
+def gemm_roofline(step, dev, ms_step, config, prof_steps=1):
+    """Dominant-kernel roofline, measured on the timed schedule itself.  A second graph of the same
+    step (same sub-batch streams, same kernels) is captured with the library's launch timeline on:
+    every fast-GEMM launch folds its first-workgroup start and last-workgroup end (device clock,
+    s_memrealtime at 100 MHz) into its own slot, which works inside a replayed graph where HIP
+    events cannot be recorded.  Per replay: the launch intervals, their UNION (the wall time the
+    GEMMs occupy in this schedule; two sub-batch streams overlap GEMMs with each other and with the
+    other kernels) and the replay's own device-time span.  The timed graph itself has no timeline."""
+    import torch
+    import sdpnet_hip as sp
     tl = torch.empty(2 * 4096, dtype=torch.int64, device=dev)
     sp.gemm_timeline_begin(tl)
     try:
@@ -429,63 +473,127 @@ def main():
     achieved = fast_fl / (union_ms_step * 1e-3) / 1e12
     per_launch_tf = fast_fl / (fast_ms * 1e-3) / 1e12 if fast_ms else 0.0
     kname = FAST_GEMM_NAMES.get(sp.lib().sdp_gemm_set_fast_kernel(0), "?")
-    traffic, traffic_src = measured_traffic(kname, args.config) if args.config in ("m", "xl") else (None, None)
-    gf = flops_per_image(cfg) / 1e9
-    tokens = (224 // cfg["patch_size"]) ** 2 + min(4, cfg["max_num_registers"])
-    value = total_imgs / el
-    ms_step = 1e3 * el / args.steps
+    traffic, traffic_src = measured_traffic(kname, config) if config in ("m", "xl") else (None, None)
     # the GEMM union is measured on a replay of the timed schedule: it must fit in the timed step
     # (a 2 % margin for replay-to-replay clock variation; the line reports both)
     assert union_ms_step <= ms_step * 1.02, (union_ms_step, ms_step)
-    out = {
-        "metric": C["metric"],
-        "value": round(value, 2),
-        "unit": "images/sec",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1e3 * el / args.steps, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bf16",
-        "data": "synthetic N(0,1) 224x224 images resident in HBM; random-init weights (reference init)",
-        "config": {"workload": C["desc"] + ", bf16 storage / fp32 accumulate"
-                                + (", eager launches" if args.no_graph else ", HIP-graph replay"),
-                   "streams_per_gpu": m._num_streams(B),
-                   "global_batch": args.batch * world, "per_gpu_batch": B, "image": 224, "tokens": tokens,
-                   "parallelism": f"dp{world} independent batch shards (no collective)",
-                   "comm_world": comm_world, "comm_backend": "nccl (RCCL)" if world > 1 else None,
-                   "devices": devs},
-        "model_flops_per_image_gf": round(gf, 3),
-        "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
-        "roofline": {"bound": "mfma", "kernel": kname,
-                     "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "achieved_basis": "GEMM FLOPs per step / union of the GEMM launch intervals per step, "
-                                       "measured in a graph replay of the timed schedule (same sub-batch streams "
-                                       "and kernels; device-clock launch timeline, median of 5 replays)",
-                     "gemm_union_ms_per_step": round(union_ms_step, 3),
-                     "ms_per_step": round(ms_step, 3),
-                     "union_le_step": bool(union_ms_step <= ms_step),
-                     "profiled_replay_ms": round(med["replay_ms"], 3),
-                     "lower_bound_tflops": round(fast_fl / (ms_step * 1e-3) / 1e12, 1),
-                     "lower_bound_basis": "GEMM FLOPs per step / ms_per_step (no overlap assumption)",
-                     "per_launch_tflops": round(per_launch_tf, 1),
-                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
-                     "traffic_unit": "bytes per launch, L2-to-fabric (PMC 2*FETCH_SIZE+WRITE_SIZE; Infinity Cache hits included)", "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": int(fast_by / max(1, fast_n)),
-                     "launches_per_step": fast_n,
-                     "avg_launch_us": round(1e3 * fast_ms / max(1, fast_n), 2),
-                     "avg_launch_basis": "device-clock launch durations in the 2-stream graph replay (co-running "
-                                         "launches overlap, so these are not solo times)",
-                     "algorithmic_gflop_per_launch": round(fast_fl / max(1, fast_n) / 1e9, 3),
-                     "per_shape": per_shape},
-        "cpu_baseline": None,
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cpu_sd, cfg, name=C["name"])
+    return {"bound": "mfma", "kernel": kname,
+            "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "achieved_basis": "GEMM FLOPs per step / union of the GEMM launch intervals per step, "
+                              "measured in a graph replay of the timed schedule (same sub-batch streams "
+                              "and kernels; device-clock launch timeline, median of 5 replays)",
+            "gemm_union_ms_per_step": round(union_ms_step, 3),
+            "ms_per_step": round(ms_step, 3),
+            "union_le_step": bool(union_ms_step <= ms_step),
+            "profiled_replay_ms": round(med["replay_ms"], 3),
+            "lower_bound_tflops": round(fast_fl / (ms_step * 1e-3) / 1e12, 1),
+            "lower_bound_basis": "GEMM FLOPs per step / ms_per_step (no overlap assumption)",
+            "per_launch_tflops": round(per_launch_tf, 1),
+            "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+            "traffic_unit": "bytes per launch, L2-to-fabric (PMC 2*FETCH_SIZE+WRITE_SIZE; Infinity Cache hits "
+                            "included)", "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": int(fast_by / max(1, fast_n)),
+            "launches_per_step": fast_n,
+            "avg_launch_us": round(1e3 * fast_ms / max(1, fast_n), 2),
+            "avg_launch_basis": "device-clock launch durations in the 2-stream graph replay (co-running "
+                                "launches overlap, so these are not solo times)",
+            "algorithmic_gflop_per_launch": round(fast_fl / max(1, fast_n) / 1e9, 3),
+            "per_shape": per_shape}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="m",
+                    help="m = the BASELINE metric's workload (default); xl = configs[2]; xl_train = configs[4]")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = the config's: M 256, XL 512)")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the XL forward / XL training lines timed after the headline at N=1")
+    ap.add_argument("--secondary-steps", type=int, default=20)
+    ap.add_argument("--prof-steps", type=int, default=1, help="forwards per profiled graph replay (roofline)")
+    ap.add_argument("--streams", type=int, default=0, help="sub-batch streams per GPU (0 = model default)")
+    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of the launch + timing path")
+    args = ap.parse_args()
+    C = CONFIGS[args.config]
+    cfg = C["cfg"]
+    if args.batch <= 0:
+        args.batch = C["batch"]
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch N ranks with --gpus N")
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    if C.get("train"):
+        return train_bench(args, C, world, rank, local)
+
+    import torch
+    import torch.distributed as dist
+    import sharding
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    comm_world = dist.get_world_size() if world > 1 else 1
+    if comm_world != world:
+        raise SystemExit(f"bench.py: RCCL world size {comm_world} != {world}")
+    if world > 1:
+        devs = [None] * world
+        dist.all_gather_object(devs, f"rank{rank}:cuda:{local}:{torch.cuda.get_device_name(dev)}")
+    else:
+        devs = [f"rank0:cuda:{local}:{torch.cuda.get_device_name(dev)}"]
+    rec = library_record()
+
+    # weak scaling: the global batch is world x per-GPU batch, each rank owns one
+    # contiguous shard (images are independent, no collective on the data path)
+    lo, hi = sharding.shard_bounds(args.batch * world, world, rank)
+    out, cpu_sd = forward_bench(C, hi - lo, args.steps, args.warmup, dev, world, rank, streams=args.streams,
+                                graph=not args.no_graph, roofline=True, config=args.config)
+    out["config"].update({"global_batch": args.batch * world,
+                          "parallelism": f"dp{world} independent batch shards (no collective)",
+                          "comm_world": comm_world, "comm_backend": "nccl (RCCL)" if world > 1 else None,
+                          "devices": devs, **rec})
+    out["cpu_baseline"] = None
+    cpu_sds = {}
+    if cpu_sd is not None:
+        cpu_sds[C["name"]] = (cpu_sd, cfg)
+    if world == 1 and not args.no_secondary and args.config == "m":
+        # configs[2] and configs[4] under the same clock, after the headline's timed region
+        sec = {}
+        ks = max(1, min(args.secondary_steps, args.steps))
+        torch.cuda.empty_cache()
+        xl, xl_sd = forward_bench(CONFIGS["xl"], CONFIGS["xl"]["batch"], ks, min(args.warmup, 3), dev, 1, rank,
+                                  graph=not args.no_graph, roofline=False, config="xl")
+        sec["xl_fwd"] = {k: xl[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "model_mfma_frac",
+                                           "model_flops_per_image_gf")}
+        sec["xl_fwd"]["per_gpu_batch"] = CONFIGS["xl"]["batch"]
+        if xl_sd is not None:
+            cpu_sds["SdP-Net-XL"] = (xl_sd, XL_CFG)
+        torch.cuda.empty_cache()
+        tr = train_step_bench(CONFIGS["xl_train"], CONFIGS["xl_train"]["batch"], ks, min(args.warmup, 3), dev, 1, rank,
+                              local, CONFIGS["xl_train"]["batch"])
+        sec["xl_train"] = {k: tr[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "model_mfma_frac",
+                                             "model_flops_per_image_gf", "skipped_steps", "peak_mem_gb")}
+        sec["xl_train"]["per_gpu_batch"] = CONFIGS["xl_train"]["batch"]
+        out["secondary"] = sec
+        torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_sds:
+        if args.config == "m":
+            torch.manual_seed(231424314)
+            import model as sdp
+            cpu_sds["SdP-Net-XXS"] = (sdp.MainModel.from_dict(**XXS_CFG).state_dict(), XXS_CFG)
+        out["cpu_baseline"] = cpu_baseline(cpu_sds, headline=C["name"])
         cb = out["cpu_baseline"]["value"]
-        out["gpu_over_cpu"] = round(value / cb, 1) if cb else None
+        out["gpu_over_cpu"] = round(out["value"] / cb, 1) if cb else None
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -119,10 +119,16 @@ int sdp_gemm_set_kloop_phases(int n);
 int sdp_gemm_set_timeline(void* buf, int slots);
 int sdp_gemm_timeline_count(void);
 
-/* Timing experiments only: bit 0 makes sdp_dwconv, bit 1 sdp_attention, bit 2 sdp_ln_stats return
- * without launching (results WRONG) -- bounds what a faster kernel could give the step.  Default 0.
- * Returns the previous mask. */
+/* Timing experiments only, diagnostic library (`make stamps`, -DSDP_DIAG): bit 0 makes sdp_dwconv,
+ * bit 1 sdp_attention, bit 2 sdp_ln_stats return without launching (results WRONG) -- bounds what a
+ * faster kernel could give the step.  Returns the previous mask.  The product library has no skip
+ * paths: the mask stays 0 and a non-zero request returns -1.  Replaces nothing in the reference. */
 int sdp_debug_skip(int mask);
+
+/* Build flags of the loaded library: bit 0 = kernel skipping compiled in (SDP_DIAG), bit 1 = GEMM
+ * wall-clock stamps compiled in (SDP_GEMM_STAMPS); 0 = the product library (the only one bench.py
+ * times).  Replaces nothing in the reference. */
+int sdp_build_info(void);
 
 /* Tile raster of the 8-phase GEMM: M-blocks per group (consecutive blocks walk a group of
  * gm M-blocks before the next N-tile).  1 = row-major, -1 = auto (8 when N spans >= 12
@@ -133,30 +139,6 @@ int sdp_gemm_set_group_m(int gm);
  * v_rcp per element), 1 = exact erf (nn.GELU(), model.py:15; runtime-activation epilogue).
  * Used to bound the tanh form's share of the bf16 logits error.  Returns the previous value. */
 int sdp_gemm_set_exact_gelu(int on);
-
-/*
- * Stream-K schedule of the bf16 fast GEMM.  When a shape's 256x256 tile count T is at
- * least the CU count G and not a multiple of it, one persistent workgroup per CU takes
- * an equal contiguous share of the T * K/64 k-iterations; a tile split between two
- * workgroups is finished by the later one starting from the earlier one's fp32
- * accumulators, so every output is bit-identical to the data-parallel tile schedule.
- * The split needs caller-owned scratch per stream:
- *   sdp_gemm_workspace_bytes()   bytes needed (8 KiB + G x 256 KiB);
- *   sdp_gemm_set_workspace(stream, ws, bytes)  register ZERO-FILLED device memory (256-B
- *       aligned) for GEMMs launched on `stream` (ws = NULL unregisters).  The library keeps
- *       it zero between launches; streams without one use the data-parallel schedule.
- *   sdp_gemm_set_schedule(mode)  1 = stream-K where it applies, 0 = never (default: on the
- *       model shapes it measured slower than the data-parallel grid).
- *   sdp_gemm_sk_applies(M, N, K) 1 if such a launch takes stream-K (given a workspace).
- *   sdp_gemm_sk_status(stream, &n) synchronous: bounded-wait give-ups recorded on the
- *       stream's workspace (0 unless a split tile's producer never published).
- * Replaces nothing in the reference by itself: it schedules the GEMMs of sdp_gemm.
- */
-int64_t sdp_gemm_workspace_bytes(void);
-int sdp_gemm_set_workspace(void* stream, void* ws, int64_t bytes);
-int sdp_gemm_set_schedule(int mode);
-int sdp_gemm_sk_applies(int M, int N, int K);
-int sdp_gemm_sk_status(void* stream, unsigned* n);
 
 /*
  * LayerNorm statistics by parts: sdp_row_partials writes {mean, M2} of every
@@ -451,6 +433,18 @@ int sdp_ce_loss(int dtype, const void* logits, int64_t ldl, const int64_t* label
                 float grad_scale, void* dlogits, int64_t ldd, float* loss, void* stream);
 int sdp_ce_loss_ignore(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K, float eps,
                        float grad_scale, int64_t ignore_index, void* dlogits, int64_t ldd, float* loss, void* stream);
+/* Row count of a hard-label cross entropy: n[0] = #{i : labels[i] != ignore_index} as float, one
+ * pass over the labels (B >= 0).  Feeds sdp_ce_loss_counted.  Replaces the count inside
+ * nn.CrossEntropyLoss's 'mean' reduction (training_tools.py:76). */
+int sdp_ce_count(const int64_t* labels, int B, int64_t ignore_index, float* n, void* stream);
+
+/* sdp_ce_loss_ignore with the row count taken from nrows (device float, sdp_ce_count on the same
+ * stream) instead of every wave counting the labels: O(B) label reads in all, for per-token or
+ * per-pixel losses.  Same arithmetic and results. */
+int sdp_ce_loss_counted(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K, float eps,
+                        float grad_scale, int64_t ignore_index, const float* nrows, void* dlogits, int64_t ldd,
+                        float* loss, void* stream);
+
 /* The same loss on probability targets (fp32 rows [B][ldt], the CutMix / MixUp targets of
  * dataset_generator.py:105-110 fed to nn.CrossEntropyLoss): t' = (1 - eps) t + eps / K,
  * loss = mean_i -sum_k t'_ik log p_ik, dlogits = grad_scale / B * (p sum_k t' - t').  A hard
@@ -546,10 +540,6 @@ int sdp_rowscale_add_dropout(int x_dtype, int y_dtype, const void* X, int64_t ld
 int sdp_mt_cast_transpose_entry_bytes(void);
 int sdp_mt_cast_transpose(const void* entries, const void* tiles, int ntiles, void* stream);
 
-/* Experimental: a HIP stream restricted to part `part` of `nparts` CU subsets (contiguous CU
- * index ranges, or every nparts-th CU with interleave != 0), for the sub-batch streams of the
- * fused forward (SDPNET_CU_SPLIT).  *out receives the hipStream_t. */
-int sdp_stream_create_cu_mask(int part, int nparts, int interleave, void** out);
 
 #ifdef __cplusplus
 }

@@ -11,7 +11,6 @@
 //    query, online softmax over keys (fp32 throughout); q/k norms are applied
 //    first, in place on the QKV rows, by sdp_qk_headnorm.
 #include "common.h"
-extern int g_sdp_debug_skip;
 
 // ---------------------------------------------------------------------------
 // generic
@@ -1294,7 +1293,7 @@ extern "C" int sdp_attention(int dtype, const void* QKV, int64_t ldq, void* O, i
                              int n_head, int head_dim, const float* q_gamma, const float* q_beta,
                              const float* k_gamma, const float* k_beta, float eps, const float* mask, int64_t mask_sb,
                              int64_t mask_sh, void* stream) {
-  if (g_sdp_debug_skip & 2) return 0;  // timing experiment (misc.hip)
+  if (SDP_DIAG_SKIP(2)) return 0;  // timing experiment, diagnostic build only (misc.hip)
   if (!QKV || !O || B < 0 || N <= 0 || n_head <= 0 || head_dim <= 0 || head_dim > 128)
     return (int)hipErrorInvalidValue;
   const bool norm = q_gamma != nullptr;

@@ -144,3 +144,13 @@ SDP_DEV float wave_max(float v) {
 }
 
 #define SDP_CHECK_LAUNCH() (int)hipGetLastError()
+
+// Kernel skipping for timing experiments (tools/r4_skip.sh): compiled in only by the diagnostic
+// build (`make stamps`, -DSDP_DIAG, a separate library the product never loads).  In the product
+// library every skip test is the constant 0, so no entry point can return without its launch.
+#ifdef SDP_DIAG
+extern int g_sdp_debug_skip;
+#define SDP_DIAG_SKIP(bit) (g_sdp_debug_skip & (bit))
+#else
+#define SDP_DIAG_SKIP(bit) 0
+#endif

@@ -533,9 +533,9 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
 // offsets walked incrementally per row (the host guarantees every operand's extent < 2 GiB,
 // Epi::*_bytes) and rows past M or columns past N get an offset beyond the descriptor's range,
 // so the hardware drops those stores instead of a branch per row; the residual add works on
-// packed bf16 pairs; the row partials come from v_dot2c_f32_bf16 sums of the stored bf16
-// values (sum and sum of squares, one pass: M2 = sumsq - sum * mean, clamped at 0) reduced
-// over the row's 8 lanes with DPP adds.  Stored outputs are bit-identical to
+// packed bf16 pairs; the row partials come from the stored bf16 values in two passes (the
+// chunk sum by v_dot2c_f32_bf16, then the squared deviations from its mean by packed FMAs),
+// each reduced over the row's 8 lanes with DPP adds.  Stored outputs are bit-identical to
 // tile_epilogue_rows; the partials agree to fp32 rounding.
 enum { EF_BIAS = 1, EF_LN = 2, EF_RESID = 4, EF_PART = 8 };
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2n;
@@ -679,8 +679,12 @@ SDP_DEV void tile_epilogue_fl(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0
       ow.step8();
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4v, o), ors, ok ? rowoff + colb : OFF_DROP, 0, 0);
       if constexpr (HP) {
+        // two passes over the 8 values the lane holds: the chunk mean first (dot2 sum, 8-lane DPP
+        // reduction), then the sum of squared deviations -- no sumsq - sum * mean cancellation when
+        // a row's |mean| is far above its spread
         const bf16x2n one = {(__bf16)1.0f, (__bf16)1.0f};
-        float sm = 0.f, s2 = 0.f;
+        float sm = 0.f;
+        uint32_t uv[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           // opaque copy: hipcc (ROCm 7.2) miscompiles bit_cast<bf16x2>(u32 vector element) feeding
@@ -688,14 +692,19 @@ SDP_DEV void tile_epilogue_fl(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0
           // keeps the element
           uint32_t u = o[i];
           asm volatile("" : "+v"(u));
-          const bf16x2n x = __builtin_bit_cast(bf16x2n, u);
-          sm = __builtin_amdgcn_fdot2_f32_bf16(x, one, sm, false);
-          s2 = __builtin_amdgcn_fdot2_f32_bf16(x, x, s2, false);
+          uv[i] = u;
+          sm = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2n, u), one, sm, false);
         }
         sm = dpp_sum8(sm);
-        s2 = dpp_sum8(s2);
         const float mean = sm * (1.0f / 64.0f);
-        const float m2 = fmaxf(fmaf(-sm, mean, s2), 0.0f);
+        const f32x2 mu2 = {mean, mean};
+        f32x2 q2 = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x2 d = f32x2{__uint_as_float(uv[i] << 16), __uint_as_float(uv[i] & 0xffff0000u)} - mu2;
+          q2 = d * d + q2;
+        }
+        const float m2 = dpp_sum8(q2.x + q2.y);
         // the partials are addressed by the output's physical row (walk pw, nch * 8 B per row)
         const uint32_t poff = pw.off;
         pw.step8();
@@ -752,37 +761,6 @@ constexpr int BUF8 = 2 * TILE_BYTES;
 
 #define SDP_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
-// ---------------------------------------------------------------------------
-// Stream-K schedule (SK = true): a persistent grid of G workgroups (one per CU)
-// splits the T * nk K-iterations of the whole GEMM into G equal contiguous ranges
-// (T >= G, so a tile is split between at most two ranges).  Range p holds
-//   [tail of tile ts: k in ks..nk) [full tiles] [head of tile te: k in 0..ke)
-// and runs them in the order  head -> full tiles -> tail.  The head's fp32
-// accumulators go to slot p of the workspace (write-through sc1 stores, drained,
-// then a relaxed agent-scope flag); range p+1 finishes that tile LAST, starting its
-// own k-loop from those accumulators.  So every tile accumulates k = 0..nk-1 in
-// order into one fp32 accumulator exactly as the data-parallel kernel does: outputs
-// are bit-identical to it whatever the split (batch invariance survives).  A
-// consumer waits only for a head its producer computed FIRST, so the wait is short
-// and no range waits for work queued behind its own.  Tile boundaries fall at a
-// different time on every CU, so epilogue store bursts are spread over the launch
-// instead of arriving together once per tile round, and the last partial round of
-// the data-parallel grid disappears.
-// Flags return to 0 at the end of every launch (the consumer clears the word it
-// consumed), which keeps graph replays valid.  A wait gives up after ~2^22 polls (the
-// producer range is not resident, e.g. the chip is shared with another stream's kernels):
-// the consumer marks the flag abandoned (2), counts it in *status and recomputes the tile
-// from k = 0 -- same accumulation order, same bits; the producer, finding 2, resets it to 0.
-// ---------------------------------------------------------------------------
-struct SkArgs {
-  float* part;        // G slots x 64 Ki floats (one 256x256 fp32 tile each)
-  unsigned* flags;    // G words, zero between launches
-  unsigned* status;   // give-up counter
-  int64_t iters;      // T * nk
-  int G;              // persistent grid size (multiple of 8)
-};
-constexpr int SK_SLOT_FLOATS = BM * BN;
-
 // tile index -> (tm, tn).  group_m > 1: indices run down a group of group_m M-blocks
 // before moving to the next N-tile, so the tiles an XCD holds at once span ~group_m
 // X blocks x 32/group_m W slices instead of 32/tiles_n X blocks x every W slice.
@@ -799,11 +777,6 @@ SDP_DEV void tile_coords(int t, int tiles_m, int tiles_n, int group_m, int& tm, 
     tn = t % tiles_n;
   }
 }
-
-SDP_DEV __amdgpu_buffer_rsrc_t sk_rsrc(float* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(p, 0, SK_SLOT_FLOATS * 4, 0x00020000);
-}
-typedef __attribute__((ext_vector_type(4))) int i32x4;
 
 #ifdef SDP_GEMM_STAMPS
 // Diagnostic build only (tools/gemm_stamps.py, a separate library): wall-clock stamps of
@@ -826,12 +799,12 @@ __device__ unsigned long long g_phase_stamps[2 * 2 * 64];  // [s_memtime x 2 gro
 // EPI: 1 = permlane-paired register epilogue, 4 = whole-line LDS-staged epilogue.
 // PH2 = true: the same K-tile in 2 phases of 32 MFMAs per wave group instead of 4 of 16 (half the
 // group-to-group hand-overs; see the k-loop below).
-template <int ACT, int EPI, bool SK, bool PH2 = false>
+template <int ACT, int EPI, bool PH2 = false>
 __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
                                                          const bf16_t* __restrict__ W, int64_t ldw, Epi<bf16_t> epi,
-                                                         int M, int N, int K, int tiles_m, int tiles_n, SkArgs sk) {
-  // 2 K-tile buffers (+16 B: the stream-K tail's resume decision, broadcast to every wave)
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF8 + 16];
+                                                         int M, int N, int K, int tiles_m, int tiles_n) {
+  // 2 K-tile buffers
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF8];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -850,103 +823,19 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   }
 #endif
 
-  // ---- segment plan: (tile, first k-tile, k-tiles, mode) per segment
-  enum { SEG_FULL = 0, SEG_HEAD = 1, SEG_TAIL = 2 };
-  int nseg = 1, p = 0, ts = 0, ks = 0, te = 0, ke = nk, f0 = 0;
-  bool has_head = false, has_tail = false;
-  // SK: XCD x = b % 8 owns the raster tiles [a_x, a_x+1) (a_x = x T / 8), ordered column-major
-  // over its Gx = G / 8 workgroups (column j = local tiles j, j + Gx, j + 2 Gx, ...), so the
-  // tiles its workgroups hold at any moment are ~Gx consecutive raster tiles, as in the
-  // data-parallel grid; that stream is cut into Gx equal k-iteration ranges, range j = b / 8.
-  int a_x = 0, gx = 1, qx = 1, rx = 0;
-  if constexpr (SK) {
-    const int T = tiles_m * tiles_n, x = b & 7;
-    gx = sk.G >> 3;
-    a_x = (int)((int64_t)x * T / 8);
-    const int tx = (int)((int64_t)(x + 1) * T / 8) - a_x;
-    qx = tx / gx;
-    rx = tx - qx * gx;
-    const int64_t ix = (int64_t)tx * nk, j = b >> 3;
-    const int64_t s = j * ix / gx, e = (j + 1) * ix / gx;
-    ts = (int)(s / nk);
-    ks = (int)(s - (int64_t)ts * nk);
-    te = (int)((e - 1) / nk);
-    ke = (int)(e - (int64_t)te * nk);
-    has_head = ke < nk;
-    has_tail = ks > 0;
-    f0 = ts + (has_tail ? 1 : 0);
-    const int f1 = te - (has_head ? 1 : 0);
-    nseg = (has_head ? 1 : 0) + max(0, f1 - f0 + 1) + (has_tail ? 1 : 0);
-    p = b;
-  } else {
+  // XCD-aware tile order: consecutive blocks b, b + 8, ... share an XCD (round-robin dispatch), so
+  // XCD x = b % 8 takes a contiguous run of the raster (bijective for any tile count)
+  int tile;
+  {
     const int nwg = tiles_m * tiles_n;
     const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
-    f0 = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+    tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
   }
-
-  for (int seg = 0; seg < nseg; ++seg) {
-  int tile = f0, kb = 0, kn = nk, mode = SEG_FULL;
-  if constexpr (SK) {
-    if (has_head && seg == 0) { tile = te; kn = ke; mode = SEG_HEAD; }
-    else if (has_tail && seg == nseg - 1) { tile = ts; kb = ks; kn = nk - ks; mode = SEG_TAIL; }
-    else tile = f0 + seg - (has_head ? 1 : 0);
-    if (seg > 0) {  // the previous segment's epilogue staging (all of LDS) must be read out
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  }
-  SDP_STAMP(0x10 + mode);
-  if constexpr (SK) {  // column-major stream position -> raster tile
-    int c, r;
-    if (tile < (qx + 1) * rx) {
-      c = tile / (qx + 1);
-      r = tile - c * (qx + 1);
-    } else {
-      const int t2 = tile - (qx + 1) * rx;
-      c = rx + t2 / qx;
-      r = t2 - (c - rx) * qx;
-    }
-    tile = a_x + r * gx + c;
-  }
+  const int kb = 0, kn = nk;
+  SDP_STAMP(0x10);
   int tm, tn;
   tile_coords(tile, tiles_m, tiles_n, epi.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
-
-  // stream-K tail: continue the head's accumulation (range p-1 computed it first, so this rarely
-  // waits).  A wait that gives up (producer not resident: the grid shares the chip with other
-  // streams' kernels) marks the flag abandoned (0 -> 2) and recomputes the head's k-range itself:
-  // the same k = 0..nk-1 order into one accumulator, so the output stays bit-identical.
-  bool resume = false;
-  const int prev = p - 8;  // range j - 1 of the same XCD
-  if (SK && mode == SEG_TAIL) {
-    SDP_STAMP(2);
-    if (wave == 0) {
-      unsigned spins = 0;
-      unsigned f = 0;
-      while ((f = __hip_atomic_load(sk.flags + prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 22)) break;
-      }
-      if (f == 0u && lane == 0) {
-        unsigned expect = 0u;
-        if (__hip_atomic_compare_exchange_strong(sk.flags + prev, &expect, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-          __hip_atomic_fetch_add(sk.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          f = expect;  // published after all
-      }
-      if (lane == 0) *(volatile unsigned*)(smem + 2 * BUF8) = (f == 1u) ? 1u : 0u;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    resume = *(volatile unsigned*)(smem + 2 * BUF8) != 0u;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slot loads below the poll
-    SDP_STAMP(3);
-    if (!resume) {  // abandoned: this segment computes the whole tile
-      kb = 0;
-      kn = nk;
-    }
-  }
 
   // The wave's 8 DMA pieces per K-tile (8 rows x 128 B each): [0,1] S1-X,
   // [2,3] S1-W, [4,5] S2-W, [6,7] S3-X.  Source pointers advance by BK per tile.
@@ -987,21 +876,10 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   auto S3 = [&](int kt) { dma(6, kt); dma(7, kt); };
 
   f32x4 acc[4][8];
-  if (SK && resume) {
-    const __amdgpu_buffer_rsrc_t rs = sk_rsrc(sk.part + (int64_t)prev * SK_SLOT_FLOATS);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        acc[i][j] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((wave * 32 + i * 8 + j) * 64 + lane) * 16, 0, 16));
-    if (tid == 0) __hip_atomic_store(sk.flags + prev, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   bf16x8 xf[8], w0[4], w1[4];
   auto read_x = [&](const char* xt, int jm) {
@@ -1140,27 +1018,6 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   }  // !PH2
   if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
   SDP_STAMP(5);
-  if (SK && mode == SEG_HEAD) {
-    // publish the head's accumulators to slot p: sc1 (write-through) stores, every wave
-    // drains them, then one lane raises the flag (relaxed agent-scope store)
-    const __amdgpu_buffer_rsrc_t rs = sk_rsrc(sk.part + (int64_t)p * SK_SLOT_FLOATS);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[i][j]), rs,
-                                               ((wave * 32 + i * 8 + j) * 64 + lane) * 16, 0, 16);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (tid == 0) {  // 0 -> 1; a consumer that gave up left 2: reset for the next launch
-      unsigned expect = 0u;
-      if (!__hip_atomic_compare_exchange_strong(sk.flags + p, &expect, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT))
-        __hip_atomic_store(sk.flags + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    SDP_STAMP(6);
-    continue;
-  }
   if constexpr (EPI == 4) {  // whole-line epilogue, all eight row groups staged first (16 KiB
     // per wave: both K buffers, free once the balancing barrier above has passed); the host
     // routes resid_pre-with-activation and unaligned calls to EPI 1
@@ -1173,7 +1030,6 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
     tile_epilogue16<ACT>(epi, acc, m0, n0, M, N, wm, wn, fr, fq);
   }
   SDP_STAMP(6);
-  }  // segments
   if (epi.tline) {  // end of this workgroup: its stores have left (timeline runs only)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tid == 0) atomicMax(epi.tline + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1336,7 +1192,7 @@ static unsigned long long* tl_take() {
 
 // Phases per K-tile of the 8-phase kernel's main loop: 2 (default: 32 MFMAs per wave-group section,
 // half the group-to-group hand-overs: 3.2k vs 4.3k cycles per K-tile, profiles/r04_gemm_ph2.md) or
-// 4 (16 MFMAs per section).  Data-parallel schedule only (stream-K segments keep 4).
+// 4 (16 MFMAs per section).  
 static int g_kloop_phases = 2;
 extern "C" int sdp_gemm_set_kloop_phases(int n) {
   const int old = g_kloop_phases;
@@ -1360,75 +1216,6 @@ extern "C" int sdp_gemm_set_store_policy(int nt) {
   return old;
 }
 
-// ---- stream-K workspaces (caller-owned, registered per stream)
-// layout: [flags: 4 KiB][status: 4 KiB][G slots x 256 KiB fp32]
-static int g_sk_mode = 0;  // 1 = stream-K where it applies and a workspace is registered (measured slower, off)
-struct SkWorkspace {
-  void* stream;
-  char* base;
-};
-static SkWorkspace g_sk_ws[16];
-static std::mutex g_sk_mu;
-static int g_sk_grid = 0;
-
-static int sk_grid() {
-  if (!g_sk_grid) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      g_sk_grid = std::min(1024, cus & ~7);
-    if (g_sk_grid < 8) g_sk_grid = 8;
-  }
-  return g_sk_grid;
-}
-
-extern "C" int64_t sdp_gemm_workspace_bytes(void) {
-  return 8192 + (int64_t)sk_grid() * fast::SK_SLOT_FLOATS * 4;
-}
-
-extern "C" int sdp_gemm_set_workspace(void* stream, void* ws, int64_t bytes) {
-  std::lock_guard<std::mutex> lk(g_sk_mu);
-  for (auto& w : g_sk_ws)
-    if (w.base && w.stream == stream) w.base = nullptr;
-  if (!ws) return 0;
-  if (bytes < sdp_gemm_workspace_bytes() || (uintptr_t)ws % 256) return (int)hipErrorInvalidValue;
-  for (auto& w : g_sk_ws)
-    if (!w.base) {
-      w.stream = stream;
-      w.base = (char*)ws;
-      return 0;
-    }
-  return (int)hipErrorOutOfMemory;
-}
-
-extern "C" int sdp_gemm_set_schedule(int mode) {
-  int old = g_sk_mode;
-  if (mode == 0 || mode == 1) g_sk_mode = mode;
-  return old;
-}
-
-// 1 if a bf16 fast-kernel GEMM of this shape takes the stream-K schedule (given a workspace)
-extern "C" int sdp_gemm_sk_applies(int M, int N, int K) {
-  if (!g_sk_mode || M <= 0 || N <= 0 || K <= 0 || sdp_gemm_variant(1, M, N, K) != 1) return 0;
-  const int64_t T = (int64_t)((M + fast::BM - 1) / fast::BM) * ((N + fast::BN - 1) / fast::BN);
-  const int G = sk_grid();
-  return (T >= G && T % G != 0) ? 1 : 0;
-}
-
-// Give-up count of the stream-K waits on this stream's workspace (tests; synchronous).
-extern "C" int sdp_gemm_sk_status(void* stream, unsigned* out) {
-  char* ws = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(g_sk_mu);
-    for (auto& w : g_sk_ws)
-      if (w.base && w.stream == stream) ws = w.base;
-  }
-  if (!ws || !out) return (int)hipErrorInvalidValue;
-  hipError_t rc = hipStreamSynchronize((hipStream_t)stream);
-  if (rc == hipSuccess) rc = hipMemcpy(out, ws + 4096, sizeof(unsigned), hipMemcpyDeviceToHost);
-  return (int)rc;
-}
-
 #ifdef SDP_GEMM_STAMPS
 extern "C" int sdp_gemm_phase_stamps(void* dst) {
   hipError_t rc = hipDeviceSynchronize();
@@ -1449,13 +1236,6 @@ extern "C" int sdp_gemm_stamps(void* dst, int64_t bytes, int clear) {
   return (int)rc;
 }
 #endif
-
-static char* sk_lookup(void* stream) {
-  std::lock_guard<std::mutex> lk(g_sk_mu);
-  for (auto& w : g_sk_ws)
-    if (w.base && w.stream == stream) return w.base;
-  return nullptr;
-}
 
 int sdp_row_partials(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, int M, int C,
                      float* part, void* stream);
@@ -1504,13 +1284,12 @@ extern "C" int sdp_gemm_train_epi(int mode, const void* X, int64_t ldx, const vo
   e.act2 = act;
   e.p2 = p;
   e.seed2 = seed;
-  const fast::SkArgs sk{};
   hipStream_t s = (hipStream_t)stream;
   // the model's activations get their own instantiation (the activation folds at compile
   // time); any other code goes through the run-time switch on epi.act2
 #define SDP_TRN(A, E)                                                                                           \
-  hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,             \
-                     (const bf16_t*)X, ldx, dm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk)
+  hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, true>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,              \
+                     (const bf16_t*)X, ldx, dm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
   if (mode == 1) {
     if (act == ACT_GELU) SDP_TRN(ACT_GELU, 5);
     else if (act == ACT_RELU) SDP_TRN(ACT_RELU, 5);
@@ -1575,26 +1354,14 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
         e.part = part;
         if (part_done) *part_done = true;
       }
-      fast::SkArgs sk{};
-      char* ws = sdp_gemm_sk_applies(M, N, K) ? sk_lookup(stream) : nullptr;
-      if (ws) {
-        sk.flags = (unsigned*)ws;
-        sk.status = (unsigned*)(ws + 4096);
-        sk.part = (float*)(ws + 8192);
-        sk.G = sk_grid();
-        sk.iters = (int64_t)tm * tn * (K / fast::BK);
-      }
 #define SDP_8PH(A, E)                                                                                               \
   do {                                                                                                              \
-    if (ws)                                                                                                         \
-      hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, true>), dim3(sk.G), dim3(fast::NTHREADS), 0, s,                 \
-                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);                 \
-    else if (g_kloop_phases == 2)                                                                                   \
-      hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false, true>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,       \
-                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);                 \
+    if (g_kloop_phases == 2)                                                                                        \
+      hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, true>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,              \
+                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn);                     \
     else                                                                                                            \
       hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,             \
-                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);                 \
+                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn);                     \
   } while (0)
       // exact-erf GELU goes through the runtime-activation epilogue (apply_act)
       const int ak = (act == ACT_GELU && g_exact_gelu) ? -1 : act;
@@ -1613,31 +1380,21 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
       e.out_bytes = (uint32_t)ob;
       e.res_bytes = (uint32_t)rb;
       e.part_bytes = (uint32_t)pb;
-      const bool spec = g_epi_spec && !ws && fk == 14 && small && !e.nt_store && (ak == ACT_NONE || ak == ACT_GELU) &&
+      const bool spec = g_epi_spec && fk == 14 && small && !e.nt_store && (ak == ACT_NONE || ak == ACT_GELU) &&
                         (fl == 0 || fl == fast::EF_BIAS || fl == (fast::EF_BIAS | fast::EF_LN) ||
                          fl == (fast::EF_RESID | fast::EF_PART) || fl == (fast::EF_BIAS | fast::EF_RESID | fast::EF_PART));
       if (spec) {
-#define SDP_8PH_DP(A, E)                                                                                   \
-  do {                                                                                                      \
-    if (g_kloop_phases == 2)                                                                                \
-      hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false, true>), dim3(tm * tn), dim3(fast::NTHREADS), 0, \
-                         s, (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);      \
-    else                                                                                                    \
-      hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,    \
-                         (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, sk);        \
-  } while (0)
 #define SDP_8PH_FL(A)                                                           \
   do {                                                                          \
-    if (fl == (fast::EF_BIAS | fast::EF_LN)) SDP_8PH_DP(A, 16 + 3);             \
-    else if (fl == (fast::EF_RESID | fast::EF_PART)) SDP_8PH_DP(A, 16 + 12);    \
-    else if (fl == 0) SDP_8PH_DP(A, 16 + 0);                                    \
-    else if (fl == fast::EF_BIAS) SDP_8PH_DP(A, 16 + 1);                        \
-    else SDP_8PH_DP(A, 16 + 13);                                                \
+    if (fl == (fast::EF_BIAS | fast::EF_LN)) SDP_8PH(A, 16 + 3);                \
+    else if (fl == (fast::EF_RESID | fast::EF_PART)) SDP_8PH(A, 16 + 12);       \
+    else if (fl == 0) SDP_8PH(A, 16 + 0);                                       \
+    else if (fl == fast::EF_BIAS) SDP_8PH(A, 16 + 1);                           \
+    else SDP_8PH(A, 16 + 13);                                                   \
   } while (0)
         if (ak == ACT_NONE) SDP_8PH_FL(ACT_NONE);
         else SDP_8PH_FL(ACT_GELU);
 #undef SDP_8PH_FL
-#undef SDP_8PH_DP
       } else if (fk == 14) {
         if (ak == ACT_NONE) SDP_8PH(ACT_NONE, 4);
         else if (ak == ACT_GELU) SDP_8PH(ACT_GELU, 4);

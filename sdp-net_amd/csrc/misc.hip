@@ -486,38 +486,32 @@ extern "C" int sdp_fold_ln_weight(const float* W, const float* gamma, const floa
   return SDP_CHECK_LAUNCH();
 }
 
-// ---------------------------------------------------------------------------
-// Sub-batch stream restricted to a subset of the CUs (hipExtStreamCreateWithCUMask), for the
-// concurrent sub-batch schedule of the fused forward: part p of nparts gets the CUs whose
-// index i satisfies (interleave ? i % nparts : i * nparts / ncu) == p.  Experimental (A/B).
-// ---------------------------------------------------------------------------
-#include <hip/hip_ext.h>
-extern "C" int sdp_stream_create_cu_mask(int part, int nparts, int interleave, void** out) {
-  if (!out || nparts <= 0 || part < 0 || part >= nparts) return (int)hipErrorInvalidValue;
-  int dev = 0, ncu = 256;
-  (void)hipGetDevice(&dev);
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  uint32_t mask[32] = {0};
-  const int nw = (ncu + 31) / 32;
-  if (nw > 32) return (int)hipErrorInvalidValue;
-  for (int i = 0; i < ncu; ++i) {
-    const int p = interleave ? i % nparts : (int)((int64_t)i * nparts / ncu);
-    if (p == part) mask[i >> 5] |= 1u << (i & 31);
-  }
-  hipStream_t s = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)nw, mask);
-  if (e != hipSuccess) return (int)e;
-  *out = (void*)s;
-  return 0;
-}
 
-
-// Timing experiments only (tools/r4_skip.sh): bit 0 skips sdp_dwconv, bit 1 sdp_attention, bit 2
-// sdp_ln_stats -- the results are then WRONG; it bounds what a faster kernel could give the step.
-// 0 (default) skips nothing.  Returns the previous mask.
+// Timing experiments only (tools/r4_skip.sh, diagnostic build): bit 0 skips sdp_dwconv, bit 1
+// sdp_attention, bit 2 sdp_ln_stats -- the results are then WRONG; it bounds what a faster kernel
+// could give the step.  Returns the previous mask.  The product library has no skip paths: it keeps
+// the mask at 0 and returns -1 for any non-zero request (sdp_build_info() tells the builds apart).
+#ifdef SDP_DIAG
 int g_sdp_debug_skip = 0;
 extern "C" int sdp_debug_skip(int mask) {
   const int old = g_sdp_debug_skip;
   g_sdp_debug_skip = mask;
   return old;
+}
+#else
+extern "C" int sdp_debug_skip(int mask) { return mask ? -1 : 0; }
+#endif
+
+// Build flags of this library: bit 0 = diagnostic kernel skipping compiled in (SDP_DIAG), bit 1 =
+// GEMM wall-clock stamps compiled in (SDP_GEMM_STAMPS).  0 for the product library; bench.py
+// refuses to time anything else.
+extern "C" int sdp_build_info(void) {
+  int f = 0;
+#ifdef SDP_DIAG
+  f |= 1;
+#endif
+#ifdef SDP_GEMM_STAMPS
+  f |= 2;
+#endif
+  return f;
 }

@@ -14,7 +14,6 @@
 //    zeros, optional bias) on image rows of a token-major buffer, optionally on
 //    LN(x) computed while staging (ConvMixer layer_norm_1, layers.py:102).
 #include "common.h"
-extern int g_sdp_debug_skip;
 
 // ---------------------------------------------------------------------------
 // Row LayerNorm
@@ -363,7 +362,7 @@ __global__ __launch_bounds__(256) void ln_stats_k(const float* __restrict__ part
 
 extern "C" int sdp_ln_stats(const float* part, int x_grp, int64_t x_gstride, int x_off, int M, int C, float eps,
                             float* stats, void* stream) {
-  if (g_sdp_debug_skip & 4) return 0;  // timing experiment (misc.hip)
+  if (SDP_DIAG_SKIP(4)) return 0;  // timing experiment, diagnostic build only (misc.hip)
   if (!part || !stats || M < 0 || C <= 0) return (int)hipErrorInvalidValue;
   if (M == 0) return 0;
   const RowMap xm = mk_rmap(x_grp, x_gstride, x_off);
@@ -1021,7 +1020,7 @@ extern "C" int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int6
                           const float* stats, const float* ln_gamma, const float* ln_beta, const float* weight,
                           const float* bias, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off, int B,
                           int H, int W, int C, int k, void* stream) {
-  if (g_sdp_debug_skip & 1) return 0;  // timing experiment (misc.hip)
+  if (SDP_DIAG_SKIP(1)) return 0;  // timing experiment, diagnostic build only (misc.hip)
   if (!X || !Y || !weight || B < 0 || H <= 0 || W <= 0 || C <= 0) return (int)hipErrorInvalidValue;
   if (stats && (!ln_gamma || !ln_beta)) return (int)hipErrorInvalidValue;
   const int esz = dtype == 1 ? 2 : 4;

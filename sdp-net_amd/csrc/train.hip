@@ -1645,8 +1645,10 @@ extern "C" int sdp_dw_wgrad(int dtype, const void* A, int64_t lda, int a_grp, in
 // loss_sum += sum_i loss_i / n (atomic, fp32), n = B for soft targets and the number of rows
 // whose label is not ignore_index for hard labels (nn.CrossEntropyLoss's default
 // ignore_index = -100, reduction 'mean': an ignored row adds nothing to the loss and gets a zero
-// gradient row; every row ignored gives a NaN loss, as torch's 0 / 0).  One wave per row; every
-// wave counts the ignored labels itself (B int64 reads).  Any other hard label outside [0, K) is
+// gradient row; every row ignored gives a NaN loss, as torch's 0 / 0).  One wave per row; the
+// row count comes from sdp_ce_count (one pass over the labels, sdp_ce_loss_counted) or, in the
+// older entry points, every wave counts the labels itself (B reads per row: fine at
+// classification batch sizes, quadratic per token).  Any other hard label outside [0, K) is
 // never dereferenced: the row's loss and gradient become NaN, so the bad batch shows in the loss
 // instead of reading out of bounds (torch raises there).
 // ---------------------------------------------------------------------------
@@ -1654,15 +1656,20 @@ template <typename T, bool SOFT>
 __global__ __launch_bounds__(256) void ce_k(const T* __restrict__ L, int64_t ldl, const int64_t* __restrict__ y,
                                             const float* __restrict__ tg, int64_t ldt, int B, int K, float eps,
                                             float grad_scale, T* __restrict__ D, int64_t ldd,
-                                            float* __restrict__ loss, int64_t ignore) {
+                                            float* __restrict__ loss, int64_t ignore,
+                                            const float* __restrict__ counted) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= B) return;
   float nrows = (float)B;
   if constexpr (!SOFT) {
-    float cnt = 0.f;
-    for (int i = lane; i < B; i += 64) cnt += (y[i] != ignore) ? 1.f : 0.f;
-    nrows = wave_sum(cnt);
+    if (counted) {  // sdp_ce_count ran first (O(B) in all)
+      nrows = *counted;
+    } else {        // legacy entry points: every wave counts (B reads per row)
+      float cnt = 0.f;
+      for (int i = lane; i < B; i += 64) cnt += (y[i] != ignore) ? 1.f : 0.f;
+      nrows = wave_sum(cnt);
+    }
     if (y[r] == ignore) {  // no loss, zero gradient row
       if (r == 0 && lane == 0 && nrows == 0.f) atomicAdd(loss, NAN);
       if (D)
@@ -1720,7 +1727,7 @@ __global__ __launch_bounds__(256) void ce_k(const T* __restrict__ L, int64_t ldl
 template <bool SOFT>
 static int ce_launch(int dtype, const void* logits, int64_t ldl, const int64_t* labels, const float* targets,
                      int64_t ldt, int B, int K, float eps, float grad_scale, void* dlogits, int64_t ldd, float* loss,
-                     void* stream, int64_t ignore = -100) {
+                     void* stream, int64_t ignore = -100, const float* counted = nullptr) {
   if (!logits || !loss || B < 0 || K <= 0) return (int)hipErrorInvalidValue;
   if (SOFT ? !targets : !labels) return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
@@ -1728,10 +1735,10 @@ static int ce_launch(int dtype, const void* logits, int64_t ldl, const int64_t* 
   dim3 grid((B + 3) / 4);
   if (dtype == 1)
     hipLaunchKernelGGL((ce_k<bf16_t, SOFT>), grid, dim3(256), 0, s, (const bf16_t*)logits, ldl, labels, targets, ldt,
-                       B, K, eps, grad_scale, (bf16_t*)dlogits, ldd, loss, ignore);
+                       B, K, eps, grad_scale, (bf16_t*)dlogits, ldd, loss, ignore, counted);
   else if (dtype == 0)
     hipLaunchKernelGGL((ce_k<float, SOFT>), grid, dim3(256), 0, s, (const float*)logits, ldl, labels, targets, ldt, B,
-                       K, eps, grad_scale, (float*)dlogits, ldd, loss, ignore);
+                       K, eps, grad_scale, (float*)dlogits, ldd, loss, ignore, counted);
   else
     return (int)hipErrorInvalidValue;
   return SDP_CHECK_LAUNCH();
@@ -1747,6 +1754,36 @@ extern "C" int sdp_ce_loss_ignore(int dtype, const void* logits, int64_t ldl, co
                                   float* loss, void* stream) {
   return ce_launch<false>(dtype, logits, ldl, labels, nullptr, 0, B, K, eps, grad_scale, dlogits, ldd, loss, stream,
                           ignore_index);
+}
+
+// n[0] = number of labels != ignore_index (float), one workgroup sweeping the labels once.
+__global__ __launch_bounds__(1024) void ce_count_k(const int64_t* __restrict__ y, int B, int64_t ignore,
+                                                   float* __restrict__ n) {
+  __shared__ float ws[16];
+  float c = 0.f;
+  for (int i = threadIdx.x; i < B; i += 1024) c += (y[i] != ignore) ? 1.f : 0.f;
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += ws[w];
+    n[0] = t;
+  }
+}
+
+extern "C" int sdp_ce_count(const int64_t* labels, int B, int64_t ignore_index, float* n, void* stream) {
+  if (!labels || !n || B < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ce_count_k, dim3(1), dim3(1024), 0, (hipStream_t)stream, labels, B, ignore_index, n);
+  return SDP_CHECK_LAUNCH();
+}
+
+extern "C" int sdp_ce_loss_counted(int dtype, const void* logits, int64_t ldl, const int64_t* labels, int B, int K,
+                                   float eps, float grad_scale, int64_t ignore_index, const float* nrows,
+                                   void* dlogits, int64_t ldd, float* loss, void* stream) {
+  if (!nrows) return (int)hipErrorInvalidValue;
+  return ce_launch<false>(dtype, logits, ldl, labels, nullptr, 0, B, K, eps, grad_scale, dlogits, ldd, loss, stream,
+                          ignore_index, nrows);
 }
 
 extern "C" int sdp_ce_loss_soft(int dtype, const void* logits, int64_t ldl, const float* targets, int64_t ldt, int B,

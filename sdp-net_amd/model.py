@@ -55,23 +55,6 @@ activations = {
 Rows = sp.Rows
 
 
-def _sub_streams(device, ns: int, split: str):
-    """The sub-batch streams of the fused forward: plain HIP streams, or (A/B knob
-    SDPNET_CU_SPLIT=contig|inter) streams restricted to disjoint CU subsets."""
-    if split not in ("contig", "inter"):
-        return [torch.cuda.Stream(device=device) for _ in range(ns)]
-    import ctypes
-    out = []
-    with torch.cuda.device(device):
-        for i in range(ns):
-            h = ctypes.c_void_p()
-            rc = sp.lib().sdp_stream_create_cu_mask(i, ns, 1 if split == "inter" else 0, ctypes.byref(h))
-            if rc:
-                raise RuntimeError(f"sdp_stream_create_cu_mask failed ({rc})")
-            out.append(torch.cuda.ExternalStream(h.value, device=device))
-    return out
-
-
 class MainModel(SdPModel):
     def __init__(self,
                  embedding_dim: int = 128,
@@ -222,19 +205,17 @@ class MainModel(SdPModel):
             # Independent sub-batches on concurrent HIP streams: one chunk's tail waves and
             # memory-bound kernels overlap the other's GEMMs (no data dependence between images).
             main = torch.cuda.current_stream(x.device)
-            split = getattr(self, "cu_split", None) or os.environ.get("SDPNET_CU_SPLIT", "")
-            streams = self.__dict__.setdefault("_sdp_streams", {}).setdefault(
-                (x.device, ns, split), _sub_streams(x.device, ns, split))
+            streams = self.__dict__.setdefault("_sdp_streams", {})
+            if (x.device, ns) not in streams:
+                streams[(x.device, ns)] = [torch.cuda.Stream(device=x.device) for _ in range(ns)]
+            streams = streams[(x.device, ns)]
             step = (B + ns - 1) // ns
-            offset = float(getattr(self, "stream_offset_us", 0.0) or os.environ.get("SDPNET_STREAM_OFFSET_US", 0))
             for i, s in enumerate(streams):
                 lo, hi = i * step, min(B, (i + 1) * step)
                 if lo >= hi:
                     continue
                 s.wait_stream(main)
                 with torch.cuda.stream(s):
-                    if i and offset > 0:  # de-phase the sub-batch streams (A/B knob)
-                        torch.cuda._sleep(int(offset * 2400 * i))
                     self._forward_chunk(x[lo:hi], logits[lo:hi], num_registers, dt, Hp, Wp, C, False)
             for s in streams:
                 main.wait_stream(s)

@@ -44,17 +44,12 @@ _SIGS = {
     "sdp_gemm_set_timeline": ([_vp, _i32], _i32),
     "sdp_gemm_timeline_count": ([], _i32),
     "sdp_debug_skip": ([_i32], _i32),
+    "sdp_build_info": ([], _i32),
     "sdp_gemm_set_group_m": ([_i32], _i32),
     "sdp_gemm_set_exact_gelu": ([_i32], _i32),
-    "sdp_gemm_workspace_bytes": ([], _i64),
-    "sdp_gemm_set_workspace": ([_vp, _vp, _i64], _i32),
-    "sdp_gemm_set_schedule": ([_i32], _i32),
-    "sdp_stream_create_cu_mask": ([_i32, _i32, _i32, _vp], _i32),
     "sdp_mt_cast_transpose_entry_bytes": ([], _i32),
     "sdp_mt_cast_transpose": ([_vp, _vp, _i32, _vp], _i32),
     "sdp_gemm_wgrad": ([_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp], _i32),
-    "sdp_gemm_sk_applies": ([_i32, _i32, _i32], _i32),
-    "sdp_gemm_sk_status": ([_vp, _vp], _i32),
     "sdp_layernorm": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _f32, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_qk_headnorm": ([_i32, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp], _i32),
     "sdp_rowstats": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _i32, _i32, _vp], _i32),
@@ -118,6 +113,8 @@ _SIGS = {
     "sdp_dw_wgrad": ([_i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _i32, _i32, _i32, _i32, _i32, _vp, _vp], _i32),
     "sdp_ce_loss": ([_i32, _vp, _i64, _vp, _i32, _i32, _f32, _f32, _vp, _i64, _vp, _vp], _i32),
     "sdp_ce_loss_ignore": ([_i32, _vp, _i64, _vp, _i32, _i32, _f32, _f32, _i64, _vp, _i64, _vp, _vp], _i32),
+    "sdp_ce_count": ([_vp, _i32, _i64, _vp, _vp], _i32),
+    "sdp_ce_loss_counted": ([_i32, _vp, _i64, _vp, _i32, _i32, _f32, _f32, _i64, _vp, _vp, _i64, _vp, _vp], _i32),
     "sdp_ce_loss_soft": ([_i32, _vp, _i64, _vp, _i64, _i32, _i32, _f32, _f32, _vp, _i64, _vp, _vp], _i32),
     "sdp_mt_block_bytes": ([], _i32),
     "sdp_grad_sumsq": ([_vp, _vp, _vp, _i32, _vp, _vp], _i32),
@@ -185,15 +182,14 @@ def lib():
         kern = os.environ.get("SDPNET_GEMM_KLOOP_PHASES")  # 2 (default) or 4 phases per K-tile
         if kern:
             L.sdp_gemm_set_kloop_phases(int(kern))
-        kern = os.environ.get("SDPNET_DEBUG_SKIP")  # timing experiments only: skip kernels (wrong results)
-        if kern:
-            L.sdp_debug_skip(int(kern))
+        kern = os.environ.get("SDPNET_DEBUG_SKIP")  # timing experiments, diagnostic library only
+        if kern and int(kern) and L.sdp_debug_skip(int(kern)) < 0:
+            raise RuntimeError("SDPNET_DEBUG_SKIP needs the diagnostic library (make -C sdp-net_amd/csrc stamps, "
+                               "SDPNET_HIP_LIB=sdp-net_amd/lib_stamps/libsdpnet_hip.so); the product library "
+                               "has no kernel-skip paths")
         kern = os.environ.get("SDPNET_GEMM_GROUP_M")  # tile raster of the 8-phase GEMM (-1 auto, 1 row-major)
         if kern:
             L.sdp_gemm_set_group_m(int(kern))
-        kern = os.environ.get("SDPNET_GEMM_SCHEDULE")  # 0 data-parallel tiles (default), 1 stream-K
-        if kern:
-            L.sdp_gemm_set_schedule(int(kern))
         kern = os.environ.get("SDPNET_DW_KERNEL")  # A/B switch for the depthwise conv
         if kern:
             L.sdp_dwconv_set_kernel(int(kern))
@@ -284,8 +280,6 @@ def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Option
         r = [resid.t.data_ptr(), resid.ld, *resid.map()]
     else:
         r = [None, 0, 0, 0, 0]
-    if dt == BF16:
-        _ensure_workspace(y.t, M, N, K)
     tl = _TL
     if tl is not None:
         slot0 = lib().sdp_gemm_timeline_count()
@@ -304,34 +298,6 @@ def gemm(x: Rows, w: torch.Tensor, y: Rows, M: int, N: int, K: int, bias: Option
         es = x.t.element_size()
         nbytes = es * (M * K + N * K + M * N * (2 if resid is not None else 1)) + (4 * N if bias is not None else 0)
         tl.append((slot0, M, N, K, 2.0 * M * N * K, nbytes))
-
-
-# Stream-K workspaces, one per HIP stream that has run a GEMM (caller-owned memory the
-# library only borrows; see sdp_gemm_set_workspace).  A stream first seen while a graph
-# is being captured gets none, and its GEMMs keep the data-parallel tile schedule.
-_WS = {}
-
-
-def _ensure_workspace(t: torch.Tensor, M: int, N: int, K: int):
-    s = torch.cuda.current_stream(t.device)
-    key = (t.device.index, s.cuda_stream)
-    if key in _WS or not lib().sdp_gemm_sk_applies(M, N, K) or torch.cuda.is_current_stream_capturing():
-        return
-    ws = torch.zeros(int(lib().sdp_gemm_workspace_bytes()), dtype=torch.uint8, device=t.device)
-    rc = lib().sdp_gemm_set_workspace(s.cuda_stream, ws.data_ptr(), ws.numel())
-    # every registration slot taken (more streams than the library tracks): this stream keeps
-    # the data-parallel schedule (remembered, so it is not retried per launch)
-    _WS[key] = ws if rc == 0 else None
-
-
-def gemm_sk_status(t: torch.Tensor) -> int:
-    """Give-up count of the stream-K waits on the current stream's workspace (0 expected)."""
-    key = (t.device.index, torch.cuda.current_stream(t.device).cuda_stream)
-    if _WS.get(key) is None:
-        return 0
-    out = ctypes.c_uint(0)
-    _check(lib().sdp_gemm_sk_status(key[1], ctypes.byref(out)), "gemm_sk_status")
-    return int(out.value)
 
 
 def layernorm(x: Rows, gamma: torch.Tensor, beta: torch.Tensor, eps: float, y: Rows, M: int, C: int):
@@ -851,10 +817,13 @@ def ce_loss(logits: torch.Tensor, labels: torch.Tensor, eps: float, grad_scale: 
     _req(labels.dtype == torch.int64 and loss.dtype == torch.float32, "ce_loss dtypes")
     B, K = logits.shape
     _req(labels.numel() == B, "ce_loss: one label per row")
-    rc = lib().sdp_ce_loss_ignore(dcode(logits.dtype), logits.data_ptr(), logits.stride(0),
-                                  labels.contiguous().data_ptr(), B, K, float(eps), float(grad_scale),
-                                  int(ignore_index), _ptr(dlogits), dlogits.stride(0) if dlogits is not None else 0,
-                                  loss.data_ptr(), _stream(loss))
+    labels = labels.contiguous()
+    nrows = torch.empty(1, dtype=torch.float32, device=loss.device)
+    _check(lib().sdp_ce_count(labels.data_ptr(), B, int(ignore_index), nrows.data_ptr(), _stream(loss)), "ce_count")
+    rc = lib().sdp_ce_loss_counted(dcode(logits.dtype), logits.data_ptr(), logits.stride(0),
+                                   labels.data_ptr(), B, K, float(eps), float(grad_scale),
+                                   int(ignore_index), nrows.data_ptr(), _ptr(dlogits),
+                                   dlogits.stride(0) if dlogits is not None else 0, loss.data_ptr(), _stream(loss))
     _check(rc, "ce_loss")
 
 

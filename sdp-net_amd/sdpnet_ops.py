@@ -165,7 +165,7 @@ train_forward.register_autograd(_train_backward_formula, setup_context=_train_se
 # head (sdpnet_train.train_layers order), each with an autograd formula that is a second op:
 #
 #   sdpnet::train_layer(t, params, handle, layer, num_registers, dtype_code, batch) -> (out, key)
-#   sdpnet::train_layer_backward(grad_out, key, params, handle, layer) -> (grad_in, grads)
+#   sdpnet::train_layer_backward(grad_out, key, params, handle, layer, in_shape, in_dtype) -> (grad_in, grads)
 #
 # so the compiled backward runs layer by layer and DDP (training_tools.py:36-39 compiles the
 # DDP-wrapped model) all-reduces a bucket while earlier layers' backward ops still run.  The
@@ -199,8 +199,8 @@ def _train_layer_fake(t, params, handle, layer, num_registers, dtype_code, batch
 
 
 @torch.library.custom_op("sdpnet::train_layer_backward", mutates_args=(), device_types="cuda")
-def train_layer_backward(grad_out: Tensor, key: Tensor, t: Tensor, params: List[Tensor], handle: int,
-                         layer: int) -> Tuple[Tensor, List[Tensor]]:
+def train_layer_backward(grad_out: Tensor, key: Tensor, params: List[Tensor], handle: int, layer: int,
+                         in_shape: List[int], in_dtype: int) -> Tuple[Tensor, List[Tensor]]:
     import sdpnet_train
     rec = _TAPES.pop(key.data_ptr(), None)
     if rec is None:
@@ -212,22 +212,26 @@ def train_layer_backward(grad_out: Tensor, key: Tensor, t: Tensor, params: List[
 
 
 @train_layer_backward.register_fake
-def _train_layer_backward_fake(grad_out, key, t, params, handle, layer):
-    # t: the layer's forward input (shape / dtype of its gradient; the image for layer 0)
-    gin = grad_out.new_empty((0,)) if layer == 0 else torch.empty_like(t)
+def _train_layer_backward_fake(grad_out, key, params, handle, layer, in_shape, in_dtype):
+    # (in_shape, in_dtype): the layer's forward input, i.e. its gradient's shape / dtype; the input
+    # itself is not kept alive for the backward (eager frees it once the layer's ctx is done with it)
+    gin = grad_out.new_empty((0,)) if layer == 0 else grad_out.new_empty(in_shape, dtype=_DTYPES[in_dtype])
     return gin, [torch.empty_like(p) for p in params]
 
 
 def _layer_setup_context(ctx, inputs, output):
     t, params, handle, layer, num_registers, dtype_code, batch = inputs
-    ctx.save_for_backward(output[1], t, *params)
+    ctx.save_for_backward(output[1], *params)
     ctx.handle = handle
     ctx.layer = layer
+    ctx.in_shape = list(t.shape)
+    ctx.in_dtype = DTYPE_CODES[t.dtype]
 
 
 def _layer_backward_formula(ctx, grad_out, grad_key):
-    key, t, *params = ctx.saved_tensors
-    gin, grads = torch.ops.sdpnet.train_layer_backward(grad_out, key, t, params, ctx.handle, ctx.layer)
+    key, *params = ctx.saved_tensors
+    gin, grads = torch.ops.sdpnet.train_layer_backward(grad_out, key, params, ctx.handle, ctx.layer, ctx.in_shape,
+                                                       ctx.in_dtype)
     return (None if ctx.layer == 0 else gin), list(grads), None, None, None, None, None
 
 

@@ -1049,7 +1049,9 @@ def train_layernorm(ln, x: torch.Tensor) -> torch.Tensor:
 
 class _PatchFn(torch.autograd.Function):
     """ConvPatcher (layers.py:28-42): stride-p convolution as patchify + GEMM; weight gradient
-    dW = dY^T patches.  The input image takes no gradient (it is data)."""
+    dW = dY^T patches.  When the image requires grad (eager training), its gradient is the
+    convolution's input gradient: dpatches = dY W on the GEMM, then sp.unpatchify (the adjoint of
+    patchify); otherwise none is computed."""
 
     @staticmethod
     def forward(ctx, x, w, pat, dt):
@@ -1372,14 +1374,24 @@ def layer_forward(model, layer: int, t: torch.Tensor, num_registers: int, dt):
                 raise RuntimeError(f"image grid {Hp}x{Wp} exceeds max_image_size {[ew.shape[0], eh.shape[0]]}")
         S.geo = (B, R, Hp, Wp, Hp * Wp + R, model.conv_init.conv.out_channels)
         S.dt = dt
-        _WPREP = _prep_weights(model, dt)
-        S.wprep = _WPREP
-        S.rng = _RNG()
-        model._sdp_session = S
-        C = S.geo[5]
-        xin = t if t.dtype == dt else as_dtype(t, dt)
-        with torch.no_grad():
-            out = _EmbedFn.forward(ctx, xin, (B, R, Hp, Wp, num_registers, stream_dtype(dt, C)), model, dt, *params)
+        # _WPREP is valid only inside one layer op (cleared on every exit, as for the other layers);
+        # the session keeps the prepared weights for the later layers, and a failed layer 0 leaves
+        # no session behind
+        try:
+            _WPREP = _prep_weights(model, dt)
+            S.wprep = _WPREP
+            S.rng = _RNG()
+            model._sdp_session = S
+            C = S.geo[5]
+            xin = t if t.dtype == dt else as_dtype(t, dt)
+            with torch.no_grad():
+                out = _EmbedFn.forward(ctx, xin, (B, R, Hp, Wp, num_registers, stream_dtype(dt, C)), model, dt,
+                                       *params)
+        except BaseException:
+            model._sdp_session = None
+            raise
+        finally:
+            _WPREP = None
         return out, (_EmbedFn, ctx, 4, params)
     S = getattr(model, "_sdp_session", None)
     if S is None:
@@ -1397,6 +1409,9 @@ def layer_forward(model, layer: int, t: torch.Tensor, num_registers: int, dt):
             else:
                 out = _HeadFn.forward(ctx, t, (B, R, Hp * Wp, N, C), mod, S.dt, S.rng, *params)
                 rec = (_HeadFn, ctx, 5, params)
+    except BaseException:
+        model._sdp_session = None  # an aborted forward closes the session (no stale weight copies)
+        raise
     finally:
         _WPREP = None
     if kind == "head":

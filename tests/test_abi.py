@@ -66,3 +66,42 @@ def test_wrapper_rejects_cpu_tensors():
     x = torch.zeros(4, 8)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         sp.layernorm(sp.dense(x), torch.ones(8), torch.zeros(8), 1e-5, sp.dense(x), 4, 8)
+
+
+def test_product_library_has_no_kernel_skip_paths():
+    """The product library compiles the timing-experiment skips out (SDP_DIAG only): a
+    non-zero request is refused and the mask stays 0, and sdp_build_info() reports 0."""
+    L = sp.lib()
+    assert L.sdp_build_info() == 0
+    assert L.sdp_debug_skip(3) == -1
+    assert L.sdp_debug_skip(0) == 0
+
+
+class _FakeLib:
+    def __init__(self, info=0, mask=0):
+        self.info, self.mask = info, mask
+
+    def sdp_build_info(self):
+        return self.info
+
+    def sdp_debug_skip(self, m):
+        old, self.mask = self.mask, m
+        return old
+
+
+def test_bench_refuses_skip_masks_and_diagnostic_builds():
+    """bench.py's integrity gate: a diagnostic library, a non-zero skip mask or SDPNET_DEBUG_SKIP
+    make it exit before timing; otherwise it returns the SDPNET_* knobs it records."""
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    assert bench.check_library(_FakeLib(), {"PATH": "/bin"}) == {}
+    assert bench.check_library(_FakeLib(), {"SDPNET_STREAMS": "2", "X": "1"}) == {"SDPNET_STREAMS": "2"}
+    with pytest.raises(SystemExit, match="diagnostic"):
+        bench.check_library(_FakeLib(info=1), {})
+    with pytest.raises(SystemExit, match="skip"):
+        bench.check_library(_FakeLib(mask=2), {})
+    with pytest.raises(SystemExit, match="skip"):
+        bench.check_library(_FakeLib(), {"SDPNET_DEBUG_SKIP": "1"})
+    # the real product library passes the gate
+    assert bench.check_library(sp.lib(), {}) == {}

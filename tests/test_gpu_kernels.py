@@ -518,6 +518,37 @@ def test_gemm_specialised_epilogue_bit_identical(act, combo, M, N, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("offset,spread", [(100.0, 0.3), (-40.0, 0.05), (2000.0, 4.0)])
+def test_gemm_partials_large_common_offset(offset, spread):
+    """LN partials of rows whose mean is far above their spread: the specialised
+    epilogue's two-pass {mean, M2} equal the run-time epilogue's and an fp64 two-pass over the
+    stored bf16 rows (a one-pass sumsq - sum * mean loses most of M2 here)."""
+    M, N, K = 1003, 768, 768
+    x = rnd(M, K, dtype=BF, seed=95)
+    w = rnd(N, K, dtype=BF, seed=96, scale=0.001)
+    r = (offset + spread * torch.randn(M, N, device=DEV, generator=torch.Generator(DEV).manual_seed(97))).to(BF)
+    nch = N // 64
+    outs = []
+    for spec in (0, 1):
+        old = sp.lib().sdp_gemm_set_epi_spec(spec)
+        try:
+            y = r.clone()
+            part = torch.full((M, nch, 2), float("nan"), device=DEV)
+            sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, resid=sp.dense(y), part=part)
+            torch.cuda.synchronize()
+            outs.append((y, part))
+        finally:
+            sp.lib().sdp_gemm_set_epi_spec(old)
+    assert torch.equal(outs[0][0], outs[1][0])
+    yc = outs[1][0].double().view(M, nch, 64)
+    mean = yc.mean(-1)
+    m2 = ((yc - mean[..., None]) ** 2).sum(-1)
+    for _, part in outs:
+        close(part[..., 0].double(), mean, torch.float32, rel=1e-6, what="partial mean")
+        assert ((part[..., 1].double() - m2).abs() <= 1e-4 * m2 + 1e-3 * spread ** 2).all(), "partial M2"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("spec", [0, 1])
 @pytest.mark.parametrize("M,N,K", [(512, 256, 64), (700, 320, 128), (1536, 768, 192), (2048, 512, 768),
                                    (1000, 2304, 3072)])
@@ -551,107 +582,19 @@ def test_gemm_kloop_phases_bit_identical(spec, M, N, K):
     close(outs[1][0], ref, BF, what="2-phase GEMM vs fp32")
 
 
-# ------------------------------------------------- stream-K schedule of the 8-phase GEMM
-def _gemm_both_schedules(run):
-    """run() -> output tensor; returns (data-parallel result, stream-K result)."""
-    old = sp.lib().sdp_gemm_set_schedule(0)
-    try:
-        dp = run().clone()
-        sp.lib().sdp_gemm_set_schedule(1)
-        sk = run().clone()
-    finally:
-        sp.lib().sdp_gemm_set_schedule(old)
-    return dp, sk
-
-
-@pytest.mark.parametrize("kern", [9, 14])
-@pytest.mark.parametrize("M,N,K,act,res,has_b", [
-    (50176, 768, 768, 1, True, False),    # SdP-Net-M mixer 1x1 conv (T = 588)
-    (25088, 3072, 768, 1, False, False),  # half-batch up projection (T = 1176)
-    (25088, 768, 3072, 0, True, False),   # half-batch down projection (48 k-tiles per tile)
-    (25600, 2304, 768, 0, False, True),   # QKV (T = 900)
-    (65601, 200, 64, 0, True, True),      # one k-tile per tile, ragged M and N
-    (25000, 768, 128, 3, True, False),    # two k-tiles, ragged M
-    (70001, 640, 192, 1, False, True)])   # ragged N tile
-def test_gemm_stream_k_bit_identical(kern, M, N, K, act, res, has_b):
-    """Stream-K finishes split tiles from the earlier range's fp32 accumulators, so every
-    output must equal the data-parallel tile schedule bit for bit (and torch within bf16)."""
-    old = sp.lib().sdp_gemm_set_schedule(1)
-    try:
-        assert sp.lib().sdp_gemm_sk_applies(M, N, K) == 1
-    finally:
-        sp.lib().sdp_gemm_set_schedule(old)
-    x = rnd(M, K, dtype=BF, seed=80)
-    w = rnd(N, K, dtype=BF, seed=81, scale=0.05)
-    b = rnd(N, seed=82) if has_b else None
-    r = rnd(M, N, dtype=BF, seed=83) if res else None
-    y = torch.empty(M, N, dtype=BF, device=DEV)
-
-    def run():
-        y.fill_(float("nan"))
-        sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, bias=b, resid=None if r is None else sp.dense(r), act=act)
-        return y
-
-    old = sp.lib().sdp_gemm_set_fast_kernel(kern)
-    try:
-        dp, sk = _gemm_both_schedules(run)
-    finally:
-        sp.lib().sdp_gemm_set_fast_kernel(old)
-    assert sp.gemm_sk_status(y) == 0
-    assert torch.equal(dp, sk), f"stream-K differs from data-parallel: {(dp.float() - sk.float()).abs().max()}"
-    ref = ACTS[act](x.float() @ w.float().t() + (b if b is not None else 0)) + (r.float() if res else 0)
-    close(sk, ref, BF, what="stream-K vs torch")
-
-
-def test_gemm_stream_k_ln_fold_row_maps_partials():
-    """The ConvMixer call form: LN folded into the GEMM, row-mapped output into the token
-    buffer with an in-place residual, LN partials emitted -- identical under both schedules."""
-    B_, R, P, C, N = 128, 4, 196, 768, 768
-    Mt, Nt = B_ * P, R + P
-    x = (rnd(Mt, C, seed=84, scale=1.3) + rnd(Mt, 1, seed=85, scale=2.0)).to(BF)
-    w = rnd(N, C, seed=86, scale=0.05)
-    g, be = rnd(C, seed=87) * 0.2 + 1, rnd(C, seed=88) * 0.2
-    part_x = torch.empty(Mt, C // 64, 2, device=DEV)
-    sp.row_partials(sp.dense(x), Mt, C, part_x)
-    st = torch.empty(Mt, 2, device=DEV)
-    sp.ln_stats(part_x, sp.dense(x), Mt, C, 1e-5, st)
-    wf, colsum, cvec = sp.fold_ln_weight(w, g, be, None, BF)
-    tok0 = rnd(B_ * Nt, N, dtype=BF, seed=89)
-    tok = tok0.clone()
-    part = torch.empty(B_ * Nt, N // 64, 2, device=DEV)
-    outs = []
-
-    def run():
-        tok.copy_(tok0)
-        part.fill_(float("nan"))
-        img = sp.Rows(tok, N, P, Nt, R)
-        sp.gemm(sp.dense(x), wf, img, Mt, N, C, bias=cvec, act=1, resid=img, ln=(st, colsum), part=part)
-        outs.append(part.clone())
-        return tok
-
-    dp, sk = _gemm_both_schedules(run)
-    assert torch.equal(dp, sk)
-    assert torch.equal(outs[0].nan_to_num(7.0), outs[1].nan_to_num(7.0))
-    assert sp.gemm_sk_status(tok) == 0
-
-
-def test_gemm_stream_k_two_streams_and_graph_replay():
-    """Two stream-K GEMMs running concurrently on two streams (separate workspaces), then
-    the same pair captured in a HIP graph and replayed: all equal the data-parallel result."""
+# ------------------------------------------------- the 8-phase GEMM on concurrent streams
+def test_gemm_two_streams_and_graph_replay():
+    """Two GEMMs running concurrently on two streams (the model's sub-batch streams), then the
+    same pair captured in a HIP graph and replayed: all equal the single-stream result."""
     M, N, K = 25088, 3072, 768
-    sched = sp.lib().sdp_gemm_set_schedule(1)
     xs = [rnd(M, K, dtype=BF, seed=90 + i) for i in range(2)]
     w = rnd(N, K, dtype=BF, seed=92, scale=0.05)
     ys = [torch.empty(M, N, dtype=BF, device=DEV) for _ in range(2)]
-    old = sp.lib().sdp_gemm_set_schedule(0)
-    try:
-        ref = []
-        for x in xs:
-            y = torch.empty(M, N, dtype=BF, device=DEV)
-            sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, act=1)
-            ref.append(y)
-    finally:
-        sp.lib().sdp_gemm_set_schedule(old)
+    ref = []
+    for x in xs:
+        y = torch.empty(M, N, dtype=BF, device=DEV)
+        sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, act=1)
+        ref.append(y)
     streams = [torch.cuda.Stream() for _ in range(2)]
 
     def pair():
@@ -665,7 +608,7 @@ def test_gemm_stream_k_two_streams_and_graph_replay():
         for s in streams:
             cur.wait_stream(s)
 
-    pair()  # eager: registers the workspaces
+    pair()
     torch.cuda.synchronize()
     for y, r in zip(ys, ref):
         assert torch.equal(y, r)
@@ -679,7 +622,3 @@ def test_gemm_stream_k_two_streams_and_graph_replay():
     torch.cuda.synchronize()
     for y, r in zip(ys, ref):
         assert torch.equal(y, r)
-    for s in streams:
-        with torch.cuda.stream(s):
-            assert sp.gemm_sk_status(ys[0]) == 0
-    sp.lib().sdp_gemm_set_schedule(sched)

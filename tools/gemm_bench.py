@@ -39,7 +39,6 @@ def main():
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--kernels", default="14", help="bf16 fast kernel ids to A/B (9, 14)")
     ap.add_argument("--exact-gelu", default="0", help="GELU forms to A/B (0 tanh form, 1 exact erf)")
-    ap.add_argument("--schedules", default="0", help="tile schedules to A/B (0 data-parallel, 1 stream-K)")
     ap.add_argument("--epi-spec", default="1", help="epilogue specialisation A/B (0 run-time flags, 1 compile-time)")
     ap.add_argument("--kloop", default="2", help="main-loop phases per K-tile A/B (4, 2)")
     ap.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) as a yardstick")
@@ -48,7 +47,7 @@ def main():
     def combos():
         return [(kk, int(s_), int(d), int(c), int(e), int(kl)) for kk in args.kernels.split(",")
                 for s_ in args.streams.split(",") for d in args.exact_gelu.split(",")
-                for c in args.schedules.split(",") for e in args.epi_spec.split(",") for kl in args.kloop.split(",")]
+                for c in ["0"] for e in args.epi_spec.split(",") for kl in args.kloop.split(",")]
     dev = torch.device("cuda")
     bf = torch.bfloat16
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -65,7 +64,6 @@ def main():
             sp.lib().sdp_gemm_set_epi_spec(spc)
             sp.lib().sdp_gemm_set_kloop_phases(kl)
             sp.lib().sdp_gemm_set_fast_kernel(int(kern))
-            sp.lib().sdp_gemm_set_schedule(sch)
             sp.lib().sdp_gemm_set_exact_gelu(dsy)
             streams = [torch.cuda.Stream() for _ in range(ns)]
             parts = []
@@ -104,8 +102,7 @@ def main():
             diff = float((y.float() - ref_y.float()).abs().max())
             tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
             total_us[(name, kern, ns, dsy, sch, spc, kl)] = us
-            print(f"{name:11s} M={M:6d} N={N:5d} K={K:5d} kern={kern} sched={sch} streams={ns} exact_gelu={dsy} spec={spc} kloop={kl} "
-                  f"sk={sp.lib().sdp_gemm_sk_applies(M, N, K) if sch else 0} "
+            print(f"{name:11s} M={M:6d} N={N:5d} K={K:5d} kern={kern} streams={ns} exact_gelu={dsy} spec={spc} kloop={kl} "
                   f"{us:9.1f} us  {tf:7.1f} TF/s  ({100 * tf / 2516.6:4.1f}% of bf16 peak)  max|diff vs first| {diff:.3g}", flush=True)
         if args.torch:  # vendor-library yardstick (plain GEMM, no epilogue) -- not used by the product
             import torch.nn.functional as F
@@ -127,7 +124,7 @@ def main():
     for key in combos():
         if all((n, *key) in total_us for n in counts):
             t = sum(total_us[(n, *key)] * c for n, c in counts.items())
-            print(f"GEMM time per M forward (kernel, streams, exact_gelu, schedule, spec, kloop = {key}): {t / 1e3:.2f} ms")
+            print(f"GEMM time per M forward (kernel, streams, exact_gelu, unused, spec, kloop = {key}): {t / 1e3:.2f} ms")
 
 
 if __name__ == "__main__":

@@ -88,7 +88,7 @@ def analyse(st, label):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="mixer_cc,mixer_up,mixer_down,enc_qkv")
-    ap.add_argument("--schedules", default="0,1")
+    ap.add_argument("--schedules", default="0")
     ap.add_argument("--dephase", default="0", help="first-round start offsets per group of 8 workgroups per XCD, "
                     "in 10-ns ticks (experiment: group g = (b >> 3) & 3 waits g * value)")
     args = ap.parse_args()
@@ -106,7 +106,6 @@ def main():
         y = torch.empty(M, N, dtype=bf, device=dev)
         print(f"{name} M={M} N={N} K={K}")
         for sch, dph in [(int(c), int(d)) for c in args.schedules.split(",") for d in args.dephase.split(",")]:
-            sp.lib().sdp_gemm_set_schedule(sch)
             assert L.sdp_gemm_set_dephase(dph) == 0
             run = lambda: sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, bias=b,  # noqa: E731
                                   resid=None if r is None else sp.dense(r), act=act)
@@ -121,7 +120,7 @@ def main():
             print(f"  dephase {dph} ticks: {1e3 * e0.elapsed_time(e1) / 20:.1f} us per launch (events)")
             read_stamps(1)
             run()
-            sk = sch and sp.lib().sdp_gemm_sk_applies(M, N, K)
+            sk = 0
             nwg = 256 if sk else ((M + 255) // 256) * ((N + 255) // 256)
             analyse(read_stamps(nwg), f"schedule {sch} ({'stream-K' if sk else 'data-parallel'})")
 
