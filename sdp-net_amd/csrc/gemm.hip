@@ -666,12 +666,10 @@ SDP_DEV void tile_epilogue_fl(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0
     prs = __builtin_amdgcn_make_buffer_rsrc(epi.part, 0, (int)epi.part_bytes, 0x00020000);
     pcolb = (uint32_t)((n0 + wn * 64) >> 6) * 8u;
   }
-  auto drain = [&](int j, const u32x4(&rr)[2]) {
-    const char* sl = stg + j * 2048;
+  auto drain = [&](int j, const u32x4(&rr)[2], const u32x4(&ov)[2]) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int r = rlo + 8 * q;
-      u32x4 o = *(const u32x4*)(sl + r * 128 + ((ch ^ (r & 7)) << 4));
+      u32x4 o = ov[q];
       const int m = mb + j * 16 + 8 * q;
       if constexpr (HR) o = add_bf16x8(o, rr[q]);
       const bool ok = m < M && col_ok;
@@ -708,9 +706,9 @@ SDP_DEV void tile_epilogue_fl(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0
         // the partials are addressed by the output's physical row (walk pw, nch * 8 B per row)
         const uint32_t poff = pw.off;
         pw.step8();
-        if (ch == 0)
-          __builtin_amdgcn_raw_buffer_store_b64(i32x2v{__float_as_int(mean), __float_as_int(m2)}, prs,
-                                                ok ? poff + pcolb : OFF_DROP, 0, 0);
+        // every lane stores (no divergent branch); only the row's first lane has an in-range offset
+        __builtin_amdgcn_raw_buffer_store_b64(i32x2v{__float_as_int(mean), __float_as_int(m2)}, prs,
+                                              (ok && ch == 0) ? poff + pcolb : OFF_DROP, 0, 0);
       }
     }
   };
@@ -729,7 +727,18 @@ SDP_DEV void tile_epilogue_fl(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0
     });
   }
   static_for<0, 8>([&](auto j) { stage(j); });
-  static_for<0, 8>([&](auto j) { drain(j, rres[j]); });
+  // read every staged row back before the first store: one LDS round trip per wave instead of one
+  // per row (hipcc keeps an LDS read below any earlier buffer store, which it cannot prove
+  // disjoint, so reads placed inside the drain loop wait for the previous row's store)
+  u32x4 ov[8][2];
+  static_for<0, 8>([&](auto j) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = rlo + 8 * q;
+      ov[j][q] = *(const u32x4*)(stg + j * 2048 + r * 128 + ((ch ^ (r & 7)) << 4));
+    }
+  });
+  static_for<0, 8>([&](auto j) { drain(j, rres[j], ov[j]); });
 }
 
 // EPI: 0 = 8-B stores, 1 = permlane-paired 16-B stores, 2 = no stores (timing probe only)
