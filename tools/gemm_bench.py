@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--exact-gelu", default="0", help="GELU forms to A/B (0 tanh form, 1 exact erf)")
     ap.add_argument("--epi-spec", default="1", help="epilogue specialisation A/B (0 run-time flags, 1 compile-time)")
     ap.add_argument("--kloop", default="2", help="main-loop phases per K-tile A/B (4, 2)")
+    ap.add_argument("--warm-s", type=float, default=0.5, help="seconds of warm-up launches per variant")
     ap.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) as a yardstick")
     args = ap.parse_args()
 
@@ -86,7 +87,7 @@ def main():
             # warm up for ~0.5 s of GPU time so every variant is timed at the loaded clock
             # (the host-side tensor set-up leaves the GPU idle and down-clocked)
             import time
-            t_end = time.time() + 0.5
+            t_end = time.time() + args.warm_s
             while time.time() < t_end:
                 for _ in range(5):
                     run()

@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/gpmc}
 rm -rf "$OUT"; mkdir -p "$OUT"
-GB="python tools/gemm_bench.py --reps 4 --shapes mixer_cc,mixer_up,mixer_down,enc_qkv,enc_o,enc_ff1,enc_ff2"
+GB="python tools/gemm_bench.py --reps 4 --warm-s 0.05 --shapes mixer_cc,mixer_up,mixer_down,enc_qkv,enc_o,enc_ff1,enc_ff2"
 run() {  # name counters...
   local n=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" -d "$OUT/$n" -o run --output-format csv -- $GB > "$OUT/$n.log" 2>&1 || { echo "pass $n failed"; tail -5 "$OUT/$n.log"; exit 1; }
@@ -16,4 +16,6 @@ run B SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_IN
 run F FETCH_SIZE
 run W WRITE_SIZE
 run H TCC_HIT_sum TCC_MISS_sum
+python tools/gemm_pmc_summary.py "$OUT" --json "$OUT.json" > "$OUT.md" 2>&1; cat "$OUT.md"
+rm -rf "$OUT"   # raw CSVs stay on the box (gpurun_out is capped at 64 MiB)
 echo done

@@ -19,34 +19,51 @@ WARM = 3
 NCU, PEAK = 256, 2516.6e12
 
 
-def gemm_rows(path, key):
-    rows = [r for r in csv.DictReader(open(path)) if "gemm_bf16_8ph" in r["Kernel_Name"]]
-    return rows
+def gemm_rows(path):
+    return [r for r in csv.DictReader(open(path)) if "gemm_bf16_8ph" in r["Kernel_Name"]]
+
+
+def blocks(rows):
+    """Consecutive dispatches of one (kernel, grid) = one shape of gemm_bench (run in SHAPES order);
+    the first WARM of each block are dropped."""
+    rows = sorted(rows, key=lambda r: int(r["Dispatch_Id"]))
+    out, key = [], None
+    for r in rows:
+        k = (r["Kernel_Name"], r.get("Grid_Size", r.get("Grid_Size_X", "")))
+        if k != key:
+            out.append([])
+            key = k
+        out[-1].append(r)
+    return [b[WARM:] if len(b) > WARM else b for b in out]
 
 
 def main():
     d = sys.argv[1]
-    tr = gemm_rows(f"{d}/trace/run_kernel_trace.csv", None)
-    per = len(tr) // len(SHAPES)
-    dur = defaultdict(list)
-    for i, r in enumerate(tr):
-        s = i // per
-        if i % per >= WARM:
-            dur[s].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    bl = blocks(gemm_rows(f"{d}/trace/run_kernel_trace.csv"))
+    if len(bl) != len(SHAPES):
+        raise SystemExit(f"expected {len(SHAPES)} shape blocks in the kernel trace, found {len(bl)}")
+    dur = {s: [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in b] for s, b in enumerate(bl)}
     ctr = defaultdict(lambda: defaultdict(list))
     for p in "ABFWH":
         try:
-            rows = gemm_rows(f"{d}/{p}/run_counter_collection.csv", None)
+            rows = gemm_rows(f"{d}/{p}/run_counter_collection.csv")
         except FileNotFoundError:
             continue
-        disp = sorted({int(r["Dispatch_Id"]) for r in rows})
-        idx = {x: i for i, x in enumerate(disp)}
+        # counter rows: one per (dispatch, counter); group dispatches into shape blocks the same way
+        disp = {}
         for r in rows:
-            i = idx[int(r["Dispatch_Id"])]
-            s, j = i // per, i % per
-            if j >= WARM:
-                ctr[s][r["Counter_Name"]].append((float(r["Counter_Value"]),
-                                                   (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9))
+            disp.setdefault(int(r["Dispatch_Id"]), []).append(r)
+        order = sorted(disp)
+        seq = [disp[i][0] for i in order]
+        bks = blocks(seq)
+        if len(bks) != len(SHAPES):
+            print(f"pass {p}: {len(bks)} shape blocks, skipped")
+            continue
+        for s, b in enumerate(bks):
+            for r0 in b:
+                for r in disp[int(r0["Dispatch_Id"])]:
+                    ctr[s][r["Counter_Name"]].append((float(r["Counter_Value"]),
+                                                       (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9))
     out = []
     hdr = ("shape", "us", "TF/s", "%pk", "clk GHz", "%pk@clk", "MFMA busy", "wait", "issue-stall", "active",
            "LDS cf/act", "HBM MB", "alg MB", "x alg", "L2 hit")
