@@ -189,8 +189,9 @@ int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstri
                const float* stats, const float* ln_gamma, const float* ln_beta,
                const float* weight, const float* bias, void* Y, int64_t ldy, int y_grp,
                int64_t y_gstride, int y_off, int B, int H, int W, int C, int k, void* stream);
-/* Select the depthwise kernel: 3 (default) = MFMA Toeplitz form (bf16, C % 32 == 0,
- * H, W <= 16, k in {3,5,7}), 2 = 64-channel x band blocks with an fp32 LDS tile
+/* Select the depthwise kernel: 4 = tier 3 with the tap-row A fragments moved between lanes by DPP
+ * (two LDS reads per channel instead of k; bit-identical to 3), 3 (default) = MFMA Toeplitz form
+ * (bf16, C % 32 == 0, H, W <= 16, k in {3,5,7}), 2 = 64-channel x band blocks with an fp32 LDS tile
  * (C % 8 == 0, k in {3,5,7}, 16-B aligned rows), 1 = 32-channel blocks with a
  * bf16 tile (any shape); each falls back to the next where it does not apply.  Other values leave the selection unchanged.
  * Returns the previous selection. */

@@ -14,6 +14,7 @@
 //    zeros, optional bias) on image rows of a token-major buffer, optionally on
 //    LN(x) computed while staging (ConvMixer layer_norm_1, layers.py:102).
 #include "common.h"
+#include <type_traits>
 
 // ---------------------------------------------------------------------------
 // Row LayerNorm
@@ -805,10 +806,22 @@ SDP_DEV uint32_t pack_bf16x2(float a, float b) {
 // ds_read_b128 lane group (16 rows of one 16-B chunk) hit every bank twice
 // (SQ_LDS_BANK_CONFLICT was 42 % of the kernel's LDS cycles)
 constexpr int DW3_CB = 32, DW3_ROWS = 22, DW3_RS = 48;
+// f(integral_constant<int, I>) for I = B .. E-1 (compile-time indices, e.g. DPP controls)
+template <int B, int E, typename F>
+SDP_DEV void dw_static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    dw_static_for<B + 1, E>(f);
+  }
+}
 constexpr int DW3_PLANE = DW3_ROWS * DW3_RS;  // elements per channel plane
 
 
-template <int KS, int NT, bool LN, int PF>
+// DPPA: the A fragment of tap row ky + 1 is the fragment of ky moved up one row: lanes h = 0..14 take
+// lane h + 1's registers (DPP row_shl:1, within each 16-lane row) and lane 15 takes plane row 16 + ky,
+// read once per channel into the lanes h < KS - 1 and moved across by DPP row_shr -- two LDS reads per
+// channel and image instead of KS.  Same MFMA operands: bit-identical.
+template <int KS, int NT, bool LN, int PF, bool DPPA = false>
 __global__ __launch_bounds__(NT) void dwconv3_mfma(
     const bf16_t* __restrict__ X, int64_t ldx, RowMap xm, const float* __restrict__ stats,
     const float* __restrict__ lg, const float* __restrict__ lb, const float* __restrict__ Wt,
@@ -930,10 +943,27 @@ __global__ __launch_bounds__(NT) void dwconv3_mfma(
           const int cc = 2 * pp + c2, cl = CPW * wave + cc;
           const bf16_t* pl = planes + (size_t)cl * DW3_PLANE + 16 * (cl >> 3);
           d[c2] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (DPPA) {
+            u32x4 a = __builtin_bit_cast(u32x4, *(const bf16x8*)(pl + n * DW3_RS + 8 * j));  // A_0
+            const u32x4 ex = __builtin_bit_cast(u32x4, *(const bf16x8*)(pl + (16 + min(n, KS - 2)) * DW3_RS + 8 * j));
+            dw_static_for<0, KS>([&](auto kyc) {
+              constexpr int ky = decltype(kyc)::value;
+              d[c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), bfr[cc][ky], d[c2], 0, 0, 0);
+              if constexpr (ky + 1 < KS) {
 #pragma unroll
-          for (int ky = 0; ky < KS; ++ky) {
-            const bf16x8 a = *(const bf16x8*)(pl + (n + ky) * DW3_RS + 8 * j);  // A_ky[h = n][8j ..]
-            d[c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[cc][ky], d[c2], 0, 0, 0);
+                for (int e = 0; e < 4; ++e) {
+                  // lane 15 <- lane ky of ex (row_shr:(15 - ky)); lanes 0..14 <- lane + 1 of a (row_shl:1)
+                  const int t = __builtin_amdgcn_update_dpp(0, (int)ex[e], 0x110 + (15 - ky), 0xF, 0xF, false);
+                  a[e] = (uint32_t)__builtin_amdgcn_update_dpp(t, (int)a[e], 0x101, 0xF, 0xF, false);
+                }
+              }
+            });
+          } else {
+#pragma unroll
+            for (int ky = 0; ky < KS; ++ky) {
+              const bf16x8 a = *(const bf16x8*)(pl + (n + ky) * DW3_RS + 8 * j);  // A_ky[h = n][8j ..]
+              d[c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[cc][ky], d[c2], 0, 0, 0);
+            }
           }
         }
         // D[h = 4j + i][w = n] -> outs[pixel][32], 16-B chunk c of pixel p at c ^ ((p >> 2) & 3)
@@ -985,17 +1015,24 @@ static int launch_dw3(int variant, int k, const void* X, int64_t ldx, RowMap xm,
   nchunk = (B + ipb - 1) / ipb;
   const int nunits = npairs * nchunk;
   const int grid = ((nunits + 7) / 8) * 16;
-#define SDP_DW3(KS, NT, PF)                                                                                    \
-  if (stats)                                                                                                     \
-    hipLaunchKernelGGL((dwconv3_mfma<KS, NT, true, PF>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx, xm,  \
-                       stats, lg, lb, Wt, bias, (bf16_t*)Y, ldy, ym, B, H, W, C, ncg, ipb, nunits);             \
-  else                                                                                                           \
-    hipLaunchKernelGGL((dwconv3_mfma<KS, NT, false, PF>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx, xm, \
-                       stats, lg, lb, Wt, bias, (bf16_t*)Y, ldy, ym, B, H, W, C, ncg, ipb, nunits)
+#define SDP_DW3V(KS, NT, PF, DP)                                                                                  \
+  if (stats)                                                                                                        \
+    hipLaunchKernelGGL((dwconv3_mfma<KS, NT, true, PF, DP>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx, xm, \
+                       stats, lg, lb, Wt, bias, (bf16_t*)Y, ldy, ym, B, H, W, C, ncg, ipb, nunits);                \
+  else                                                                                                              \
+    hipLaunchKernelGGL((dwconv3_mfma<KS, NT, false, PF, DP>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx,    \
+                       xm, stats, lg, lb, Wt, bias, (bf16_t*)Y, ldy, ym, B, H, W, C, ncg, ipb, nunits)
+#define SDP_DW3(KS, NT, PF)                  \
+  do {                                       \
+    if (variant >= 4) {                      \
+      SDP_DW3V(KS, NT, PF, true);            \
+    } else {                                 \
+      SDP_DW3V(KS, NT, PF, false);           \
+    }                                        \
+  } while (0)
   // 16 waves x 2 channels, 2 images in flight (k = 7 at the M shape: 1 / 2 / 3 / 4 images give
   // 53.4 / 51.2-51.5 / 54.4 / 55.2 us alone and M forward 10,212 / 10,255 / 10,213 / 10,201 img/s,
   // interleaved means, tools/r4_pf.sh)
-  (void)variant;
   switch (k) {
     case 3: SDP_DW3(3, 1024, 2); break;
     case 5: SDP_DW3(5, 1024, 2); break;
@@ -1003,16 +1040,18 @@ static int launch_dw3(int variant, int k, const void* X, int64_t ldx, RowMap xm,
     default: return -1;
   }
 #undef SDP_DW3
+#undef SDP_DW3V
   return SDP_CHECK_LAUNCH();
 }
 
 // Highest kernel tier allowed (each tier falls back to the next lower one per shape):
-// 3 (default) = dwconv3_mfma where it applies (bf16, H, W <= 16, C % 32 == 0, k in {3,5,7}),
+// 4 = dwconv3_mfma with the tap-row A fragments moved by DPP (two LDS reads per channel instead of
+// KS), 3 (default) = dwconv3_mfma where it applies (bf16, H, W <= 16, C % 32 == 0, k in {3,5,7}),
 // 2 = dwconv2_nhwc (C % 8 == 0, 16-B rows), 1 = dwconv_ln_nhwc (any shape)
 static int g_dw_kernel = 3;
 extern "C" int sdp_dwconv_set_kernel(int k) {
   const int old = g_dw_kernel;
-  if (k >= 1 && k <= 3) g_dw_kernel = k;
+  if (k >= 1 && k <= 4) g_dw_kernel = k;
   return old;
 }
 

@@ -178,7 +178,7 @@ def test_qk_headnorm(dtype, H, hd):
                                        (1, 20, 37, 36, 9), (2, 3, 3, 8, 1)])
 @pytest.mark.parametrize("bias", [False, True])
 @pytest.mark.parametrize("ln", [False, True])
-@pytest.mark.parametrize("kern", [1, 2, 3])
+@pytest.mark.parametrize("kern", [1, 2, 3, 4])
 def test_dwconv(dtype, B, H, W, C, k, bias, ln, kern):
     x = rnd(B, C, H, W, dtype=dtype, seed=30, scale=2.0) + 0.5
     w = rnd(C, 1, k, k, seed=31, scale=0.2)
@@ -202,6 +202,33 @@ def test_dwconv(dtype, B, H, W, C, k, bias, ln, kern):
         sp.lib().sdp_dwconv_set_kernel(old)
     ref = F.conv2d(xin, w, b, padding="same", groups=C).permute(0, 2, 3, 1).reshape(B * H * W, C)
     close(y, ref, dtype, what="dwconv")
+
+
+@pytest.mark.parametrize("B,H,W,C,k", [(4, 14, 14, 768, 7), (2, 16, 16, 768, 7), (3, 7, 7, 64, 3), (2, 8, 8, 96, 5),
+                                       (2, 16, 16, 128, 5), (1, 12, 13, 64, 3)])
+@pytest.mark.parametrize("ln", [False, True])
+def test_dwconv_dpp_tap_rows_bit_identical(B, H, W, C, k, ln):
+    """Kernel tier 4 (the A fragments of successive tap rows moved by DPP instead of re-read from LDS)
+    feeds the MFMAs the same operands as tier 3: outputs bit-identical."""
+    x = rnd(B * H * W, C, dtype=BF, seed=35, scale=2.0)
+    w = rnd(C, k * k, seed=36, scale=0.2)
+    b = rnd(C, seed=37)
+    kw = {}
+    if ln:
+        stats = torch.empty(B * H * W, 2, device=DEV)
+        sp.rowstats(sp.dense(x), 1e-6, stats, B * H * W, C)
+        kw = dict(stats=stats, ln_gamma=rnd(C, seed=38) * 0.1 + 1, ln_beta=rnd(C, seed=39) * 0.1)
+    ys = []
+    for kern in (3, 4):
+        y = torch.full_like(x, float("nan"))
+        old = sp.lib().sdp_dwconv_set_kernel(kern)
+        try:
+            sp.dwconv(sp.dense(x), w, b, sp.dense(y), B, H, W, C, k, **kw)
+            torch.cuda.synchronize()
+        finally:
+            sp.lib().sdp_dwconv_set_kernel(old)
+        ys.append(y)
+    assert torch.equal(ys[0], ys[1])
 
 
 # ---------------------------------------------------------------------- attention
