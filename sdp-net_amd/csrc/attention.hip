@@ -304,6 +304,43 @@ __global__ __launch_bounds__(640) void attn_fa_bf16(const bf16_t* __restrict__ Q
 // shape with 4 (tools/r4_ch.sh).  hd = 128 keeps 4 (register budget).
 #define ATTN_CH 7
 #endif
+
+// K and V of one (image, head) pair -> LDS by buffer LDS-DMA (K chunk c of row r at c ^ ((r >> 2) & 3),
+// V row-major, NP16 rows each), in units of 16 rows = HDT instructions of 64 x 16 B.  A 16-row unit
+// keeps the K swizzle phase, so the per-lane byte offsets within a unit are the same for every unit
+// and pair: computed once (2 HDT registers); a unit's loads differ only by the scalar offset, and
+// no per-load address arithmetic is left (it was ~40 VALU per load, a quarter of the kernel's VALU).
+// The buffer resource ends at row N-1 of the pair's image, so rows N .. NP16-1 read as 0 (the
+// hardware's range check): finite, masked scores, P = 0, and nothing read from another image.
+template <int HDT>
+struct AttnKV {
+  uint32_t ko[HDT], vo[HDT];
+  SDP_DEV AttnKV(int lane, int64_t ldq, int C) {
+    constexpr int CPR = 4 * HDT;
+#pragma unroll
+    for (int r = 0; r < HDT; ++r) {
+      const int g = r * 64 + lane, row = g / CPR, pc = g - (g / CPR) * CPR;
+      ko[r] = (uint32_t)(((int64_t)row * ldq + C + 8 * (pc ^ ((row >> 2) & 3))) * 2);
+      vo[r] = (uint32_t)(((int64_t)row * ldq + 2 * C + 8 * pc) * 2);
+    }
+  }
+  // base: row 0 / column hh * HD of the pair; bytes: extent of the image's QKV rows from base
+  SDP_DEV void issue(const bf16_t* base, uint64_t bytes, char* Ks, char* Vs, int NP16, int64_t ldq, int wave,
+                     int nwaves) const {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)base, 0, (int)(bytes < 0xffffffffull ? bytes : 0xffffffffull), 0x00020000);
+    const int U = NP16 >> 4, w0 = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform unit index
+    const uint32_t ustep = (uint32_t)(16 * ldq * 2);
+    for (int u = w0; u < U; u += nwaves)
+#pragma unroll
+      for (int r = 0; r < HDT; ++r)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (AS3 void*)(Ks + (u * HDT + r) * 1024), 16, (int)ko[r], (int)(u * ustep), 0, 0);
+    for (int u = w0; u < U; u += nwaves)
+#pragma unroll
+      for (int r = 0; r < HDT; ++r)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (AS3 void*)(Vs + (u * HDT + r) * 1024), 16, (int)vo[r], (int)(u * ustep), 0, 0);
+  }
+};
 // ---------------------------------------------------------------------------
 // Per-wave pieces of the two-workgroup / persistent flash kernels (hd = 32*HDT).
 // Lane (r = lane & 31, hf = lane >> 5) owns query r of a 32-query tile and, in
@@ -802,22 +839,11 @@ __global__ __launch_bounds__(576) __attribute__((amdgpu_waves_per_eu(HDT <= 3 ? 
   const int nwaves = blockDim.x >> 6;
   const bf16_t* base = QKV + (int64_t)b * N * ldq + hh * HD;
 
-  // ---- K and V -> LDS by DMA: instruction i of the block moves chunks 64i..64i+63
-  // (lane-linear destination); source rows >= N are clamped to N-1 ----
+  // ---- K and V -> LDS by DMA ----
   {
-    const int nchunk = NP16 * CPR;
-    const int ninst = (nchunk + 63) / 64;
-    for (int i = wave; i < 2 * ninst; i += nwaves) {
-      const bool isv = i >= ninst;
-      const int ii = isv ? i - ninst : i;
-      const int g = ii * 64 + lane;
-      const int row = g / CPR, pc = g - row * CPR;
-      const int srow = row < N ? row : N - 1;
-      const int c = isv ? pc : (pc ^ ((row >> 2) & 3));
-      const bf16_t* src = base + (int64_t)srow * ldq + (isv ? 2 * C : C) + c * 8;
-      char* dst = (char*)(isv ? Vs : Ks) + ii * 1024;
-      if (g < nchunk) __builtin_amdgcn_global_load_lds((const AS1 void*)src, (AS3 void*)dst, 16, 0, 0);
-    }
+    const AttnKV<HDT> kv(lane, ldq, C);
+    kv.issue(base, (uint64_t)((int64_t)(N - 1) * ldq + 3 * C - hh * HD) * 2, (char*)Ks, (char*)Vs, NP16, ldq,
+             wave, nwaves);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -940,7 +966,7 @@ __global__ __launch_bounds__(256, 2) void attn_fa4_bf16(const bf16_t* __restrict
                                                      const float* __restrict__ gk, const float* __restrict__ bk,
                                                      float eps, float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) char sm[];
-  constexpr int HD = 32 * HDT, CPR = HD / 8;
+  constexpr int HD = 32 * HDT;
   const int NP16 = (N + 15) / 16 * 16;
   bf16_t* const Ks = (bf16_t*)sm;
   bf16_t* const Vs = Ks + (size_t)NP16 * HD;
@@ -967,20 +993,11 @@ __global__ __launch_bounds__(256, 2) void attn_fa4_bf16(const bf16_t* __restrict
     const int b = pair / H, hh = pair - (pair / H) * H;
     return QKV + (int64_t)b * N * ldq + hh * HD;
   };
-  const int nchunk = NP16 * CPR, ninst = (nchunk + 63) / 64;
+  const AttnKV<HDT> kv(lane, ldq, C);
   auto stage = [&](int pair) {
-    const bf16_t* base = qkv_base(pair);
-    for (int i = wave; i < 2 * ninst; i += 4) {
-      const bool isv = i >= ninst;
-      const int ii = isv ? i - ninst : i;
-      const int g = ii * 64 + lane;
-      const int row = g / CPR, pc = g - row * CPR;
-      const int srow = row < N ? row : N - 1;
-      const int c = isv ? pc : (pc ^ ((row >> 2) & 3));
-      const bf16_t* src = base + (int64_t)srow * ldq + (isv ? 2 * C : C) + c * 8;
-      char* dst = (char*)(isv ? Vs : Ks) + ii * 1024;
-      if (g < nchunk) __builtin_amdgcn_global_load_lds((const AS1 void*)src, (AS3 void*)dst, 16, 0, 0);
-    }
+    const int hh = pair - (pair / H) * H;
+    kv.issue(qkv_base(pair), (uint64_t)((int64_t)(N - 1) * ldq + 3 * C - hh * HD) * 2, (char*)Ks, (char*)Vs, NP16,
+             ldq, wave, 4);
   };
   const int r = lane & 31, hf = lane >> 5;
   // Every wave computes two query-tile slots per pair; a slot past the last tile

@@ -568,6 +568,35 @@ SDP_DEV u32x4 add_bf16x8(u32x4 ou, u32x4 ru) {
   return res;
 }
 
+#ifdef SDP_GEMM_STAMPS
+// Diagnostic build only (tools/gemm_stamps.py, a separate library): wall-clock stamps of
+// workgroup events, 64 per workgroup; stamp = event code << 56 | s_memrealtime (100 MHz).
+__device__ unsigned long long g_gemm_stamps[8192 * 64];
+__device__ int g_gemm_dephase;  // experiment: first-round workgroup b waits ((b >> 3) & 3) * this many 10-ns ticks
+// phase timeline of workgroup 0: waves 0 (group 0) and 4 (group 1), s_memtime (shader clock) at
+// each MFMA section's start (after its barrier + lgkmcnt wait) and after its last MFMA issue
+__device__ unsigned long long g_phase_stamps[2 * 2 * 64];  // [s_memtime x 2 groups][s_memrealtime x 2 groups]
+#define SDP_STAMP(code)                                                                            \
+  do {                                                                                             \
+    if (tid == 0 && nstamp < 64)                                                                   \
+      g_gemm_stamps[(int64_t)b * 64 + nstamp++] =                                                  \
+          ((unsigned long long)(code) << 56) | (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffffull); \
+  } while (0)
+// epilogue sub-phases: slots 40 + code of the workgroup's row, wave 0 only; g_epi_wait = 1 drains
+// the wave's memory counters before each stamp (serialises the parts so each one is timed alone)
+__device__ int g_epi_wait;
+#define SDP_ESTAMP(code)                                                                               \
+  do {                                                                                                 \
+    if (g_epi_wait) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                        \
+    if (threadIdx.x == 0)                                                                              \
+      g_gemm_stamps[(int64_t)blockIdx.x * 64 + 40 + (code)] =                                          \
+          ((unsigned long long)(0x20 + (code)) << 56) | (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffffull); \
+  } while (0)
+#else
+#define SDP_STAMP(code) do {} while (0)
+#define SDP_ESTAMP(code) do {} while (0)
+#endif
+
 // byte offset of a lane's rows m, m + 8, m + 16, ... through a RowMap (see RowWalk), 32-bit
 struct RowOff {
   uint32_t off, step, wrap;
@@ -712,6 +741,7 @@ SDP_DEV void tile_epilogue_fl(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0
       }
     }
   };
+  SDP_ESTAMP(0);
   u32x4 rres[8][2];
   if constexpr (HR) {
     const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc((void*)epi.resid, 0, (int)epi.res_bytes, 0x00020000);
@@ -726,7 +756,9 @@ SDP_DEV void tile_epilogue_fl(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0
       }
     });
   }
+  SDP_ESTAMP(1);
   static_for<0, 8>([&](auto j) { stage(j); });
+  SDP_ESTAMP(2);
   // read every staged row back before the first store: one LDS round trip per wave instead of one
   // per row (hipcc keeps an LDS read below any earlier buffer store, which it cannot prove
   // disjoint, so reads placed inside the drain loop wait for the previous row's store)
@@ -738,7 +770,12 @@ SDP_DEV void tile_epilogue_fl(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0
       ov[j][q] = *(const u32x4*)(stg + j * 2048 + r * 128 + ((ch ^ (r & 7)) << 4));
     }
   });
+  SDP_ESTAMP(3);
   static_for<0, 8>([&](auto j) { drain(j, rres[j], ov[j]); });
+#ifdef SDP_GEMM_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  SDP_ESTAMP(4);
 }
 
 // EPI: 0 = 8-B stores, 1 = permlane-paired 16-B stores, 2 = no stores (timing probe only)
@@ -787,23 +824,6 @@ SDP_DEV void tile_coords(int t, int tiles_m, int tiles_n, int group_m, int& tm, 
   }
 }
 
-#ifdef SDP_GEMM_STAMPS
-// Diagnostic build only (tools/gemm_stamps.py, a separate library): wall-clock stamps of
-// workgroup events, 64 per workgroup; stamp = event code << 56 | s_memrealtime (100 MHz).
-__device__ unsigned long long g_gemm_stamps[8192 * 64];
-__device__ int g_gemm_dephase;  // experiment: first-round workgroup b waits ((b >> 3) & 3) * this many 10-ns ticks
-// phase timeline of workgroup 0: waves 0 (group 0) and 4 (group 1), s_memtime (shader clock) at
-// each MFMA section's start (after its barrier + lgkmcnt wait) and after its last MFMA issue
-__device__ unsigned long long g_phase_stamps[2 * 2 * 64];  // [s_memtime x 2 groups][s_memrealtime x 2 groups]
-#define SDP_STAMP(code)                                                                            \
-  do {                                                                                             \
-    if (tid == 0 && nstamp < 64)                                                                   \
-      g_gemm_stamps[(int64_t)b * 64 + nstamp++] =                                                  \
-          ((unsigned long long)(code) << 56) | (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffffull); \
-  } while (0)
-#else
-#define SDP_STAMP(code) do {} while (0)
-#endif
 
 // EPI: 1 = permlane-paired register epilogue, 4 = whole-line LDS-staged epilogue.
 // PH2 = true: the same K-tile in 2 phases of 32 MFMAs per wave group instead of 4 of 16 (half the
@@ -1230,6 +1250,9 @@ extern "C" int sdp_gemm_phase_stamps(void* dst) {
   hipError_t rc = hipDeviceSynchronize();
   if (rc == hipSuccess) rc = hipMemcpyFromSymbol(dst, HIP_SYMBOL(fast::g_phase_stamps), sizeof(fast::g_phase_stamps));
   return (int)rc;
+}
+extern "C" int sdp_gemm_set_epi_wait(int on) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(fast::g_epi_wait), &on, sizeof(int));
 }
 extern "C" int sdp_gemm_set_dephase(int ticks) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(fast::g_gemm_dephase), &ticks, sizeof(int));

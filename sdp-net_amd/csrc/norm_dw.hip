@@ -806,22 +806,10 @@ SDP_DEV uint32_t pack_bf16x2(float a, float b) {
 // ds_read_b128 lane group (16 rows of one 16-B chunk) hit every bank twice
 // (SQ_LDS_BANK_CONFLICT was 42 % of the kernel's LDS cycles)
 constexpr int DW3_CB = 32, DW3_ROWS = 22, DW3_RS = 48;
-// f(integral_constant<int, I>) for I = B .. E-1 (compile-time indices, e.g. DPP controls)
-template <int B, int E, typename F>
-SDP_DEV void dw_static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    dw_static_for<B + 1, E>(f);
-  }
-}
 constexpr int DW3_PLANE = DW3_ROWS * DW3_RS;  // elements per channel plane
 
 
-// DPPA: the A fragment of tap row ky + 1 is the fragment of ky moved up one row: lanes h = 0..14 take
-// lane h + 1's registers (DPP row_shl:1, within each 16-lane row) and lane 15 takes plane row 16 + ky,
-// read once per channel into the lanes h < KS - 1 and moved across by DPP row_shr -- two LDS reads per
-// channel and image instead of KS.  Same MFMA operands: bit-identical.
-template <int KS, int NT, bool LN, int PF, bool DPPA = false>
+template <int KS, int NT, bool LN, int PF>
 __global__ __launch_bounds__(NT) void dwconv3_mfma(
     const bf16_t* __restrict__ X, int64_t ldx, RowMap xm, const float* __restrict__ stats,
     const float* __restrict__ lg, const float* __restrict__ lb, const float* __restrict__ Wt,
@@ -885,21 +873,30 @@ __global__ __launch_bounds__(NT) void dwconv3_mfma(
   }
   __syncthreads();  // weights consumed before outs is reused
 
-  // staging role: item t (2 per thread) -> pixel t / 4 (of up to 256), channels 8 * (t & 3) .. +7
-  auto load = [&](int b, int it, bf16x8& v, float2& st) {
+  // staging role: item t (NIT per thread) -> pixel t / 4 (of up to 256), channels 8 * (t & 3) .. +7.
+  // Pixel / plane offsets are image-independent (computed once); a group of the row maps holds whole
+  // images (host check), so image b's rows are xm(b P) + pixel: one row-map evaluation per image.
+  int pixo[NIT], dsto[NIT], outo[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
     const int t = tid + NT * it, pix = t >> 2, q = t & 3;
-    const int64_t local = (int64_t)b * P + (pix < P ? pix : 0);
-    v = *(const bf16x8*)(X + xm(local) * ldx + c0 + 8 * q);
-    if constexpr (LN) st = *(const float2*)(stats + 2 * local);
+    const int h = pix / W, w = pix - (pix / W) * W;
+    pixo[it] = pix < P ? pix : 0;
+    dsto[it] = pix < P ? (8 * q) * DW3_PLANE + 16 * q + (h + PAD) * DW3_RS + (w + PAD) : -1;
+    outo[it] = pix * DW3_CB + ((q ^ ((pix >> 2) & 3)) << 3);
+  }
+  const int q8 = 8 * (tid & 3);  // NT % 4 == 0: the same channel octet for every item
+  auto load = [&](int b, int it, bf16x8& v, float2& st) {
+    const int64_t r0 = xm((int64_t)b * P);
+    v = *(const bf16x8*)(X + (r0 + pixo[it]) * ldx + c0 + q8);
+    if constexpr (LN) st = *(const float2*)(stats + 2 * ((int64_t)b * P + pixo[it]));
   };
   auto put = [&](int it, const bf16x8& v, const float2& st) {  // LN + transpose into the planes
-    const int t = tid + NT * it, pix = t >> 2, q = t & 3;
-    if (pix >= P) return;
-    const int h = pix / W, w = pix - (pix / W) * W;
-    bf16_t* dst = planes + (size_t)(8 * q) * DW3_PLANE + 16 * q + (h + PAD) * DW3_RS + (w + PAD);
+    if (dsto[it] < 0) return;
+    bf16_t* dst = planes + dsto[it];
     if constexpr (LN) {  // gamma / beta from LDS (a global load here would drain the prefetch ring)
-      const f32x4 g0 = *(const f32x4*)(lnp + 8 * q), g1 = *(const f32x4*)(lnp + 8 * q + 4);
-      const f32x4 e0 = *(const f32x4*)(lnp + DW3_CB + 8 * q), e1 = *(const f32x4*)(lnp + DW3_CB + 8 * q + 4);
+      const f32x4 g0 = *(const f32x4*)(lnp + q8), g1 = *(const f32x4*)(lnp + q8 + 4);
+      const f32x4 e0 = *(const f32x4*)(lnp + DW3_CB + q8), e1 = *(const f32x4*)(lnp + DW3_CB + q8 + 4);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float x = (bf2f((bf16_t)v[e]) - st.x) * st.y;
@@ -943,28 +940,11 @@ __global__ __launch_bounds__(NT) void dwconv3_mfma(
           const int cc = 2 * pp + c2, cl = CPW * wave + cc;
           const bf16_t* pl = planes + (size_t)cl * DW3_PLANE + 16 * (cl >> 3);
           d[c2] = f32x4{0.f, 0.f, 0.f, 0.f};
-          if constexpr (DPPA) {
-            u32x4 a = __builtin_bit_cast(u32x4, *(const bf16x8*)(pl + n * DW3_RS + 8 * j));  // A_0
-            const u32x4 ex = __builtin_bit_cast(u32x4, *(const bf16x8*)(pl + (16 + min(n, KS - 2)) * DW3_RS + 8 * j));
-            dw_static_for<0, KS>([&](auto kyc) {
-              constexpr int ky = decltype(kyc)::value;
-              d[c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), bfr[cc][ky], d[c2], 0, 0, 0);
-              if constexpr (ky + 1 < KS) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  // lane 15 <- lane ky of ex (row_shr:(15 - ky)); lanes 0..14 <- lane + 1 of a (row_shl:1)
-                  const int t = __builtin_amdgcn_update_dpp(0, (int)ex[e], 0x110 + (15 - ky), 0xF, 0xF, false);
-                  a[e] = (uint32_t)__builtin_amdgcn_update_dpp(t, (int)a[e], 0x101, 0xF, 0xF, false);
-                }
-              }
-            });
-          } else {
 #pragma unroll
             for (int ky = 0; ky < KS; ++ky) {
               const bf16x8 a = *(const bf16x8*)(pl + (n + ky) * DW3_RS + 8 * j);  // A_ky[h = n][8j ..]
               d[c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[cc][ky], d[c2], 0, 0, 0);
             }
-          }
         }
         // D[h = 4j + i][w = n] -> outs[pixel][32], 16-B chunk c of pixel p at c ^ ((p >> 2) & 3)
         const int cl0 = CPW * wave + 2 * pp;
@@ -980,15 +960,10 @@ __global__ __launch_bounds__(NT) void dwconv3_mfma(
         asm volatile("" ::: "memory");  // one channel pair's A fragments live at a time
       }
       __syncthreads();  // outs complete; everyone done reading the planes
+      const int64_t yr0 = ym((int64_t)b * P);
 #pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        const int t = tid + NT * it, pix = t >> 2, q = t & 3;
-        if (pix < P) {
-          const int64_t local = (int64_t)b * P + pix;
-          *(bf16x8*)(Y + ym(local) * ldy + c0 + 8 * q) =
-              *(const bf16x8*)(outs + pix * DW3_CB + ((q ^ ((pix >> 2) & 3)) << 3));
-        }
-      }
+      for (int it = 0; it < NIT; ++it)
+        if (dsto[it] >= 0) *(bf16x8*)(Y + (yr0 + pixo[it]) * ldy + c0 + q8) = *(const bf16x8*)(outs + outo[it]);
       if (b + 1 < b1) {
         const int un = (u + 1) % PF;  // static after unrolling
 #pragma unroll
@@ -998,7 +973,7 @@ __global__ __launch_bounds__(NT) void dwconv3_mfma(
   }
 }
 
-static int launch_dw3(int variant, int k, const void* X, int64_t ldx, RowMap xm, const float* stats, const float* lg,
+static int launch_dw3(int k, const void* X, int64_t ldx, RowMap xm, const float* stats, const float* lg,
                       const float* lb, const float* Wt, const float* bias, void* Y, int64_t ldy, RowMap ym, int B,
                       int H, int W, int C, hipStream_t s) {
   const int ncg = C / DW3_CB;
@@ -1015,21 +990,13 @@ static int launch_dw3(int variant, int k, const void* X, int64_t ldx, RowMap xm,
   nchunk = (B + ipb - 1) / ipb;
   const int nunits = npairs * nchunk;
   const int grid = ((nunits + 7) / 8) * 16;
-#define SDP_DW3V(KS, NT, PF, DP)                                                                                  \
+#define SDP_DW3(KS, NT, PF)                                                                                    \
   if (stats)                                                                                                        \
-    hipLaunchKernelGGL((dwconv3_mfma<KS, NT, true, PF, DP>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx, xm, \
+    hipLaunchKernelGGL((dwconv3_mfma<KS, NT, true, PF>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx, xm,     \
                        stats, lg, lb, Wt, bias, (bf16_t*)Y, ldy, ym, B, H, W, C, ncg, ipb, nunits);                \
   else                                                                                                              \
-    hipLaunchKernelGGL((dwconv3_mfma<KS, NT, false, PF, DP>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx,    \
-                       xm, stats, lg, lb, Wt, bias, (bf16_t*)Y, ldy, ym, B, H, W, C, ncg, ipb, nunits)
-#define SDP_DW3(KS, NT, PF)                  \
-  do {                                       \
-    if (variant >= 4) {                      \
-      SDP_DW3V(KS, NT, PF, true);            \
-    } else {                                 \
-      SDP_DW3V(KS, NT, PF, false);           \
-    }                                        \
-  } while (0)
+    hipLaunchKernelGGL((dwconv3_mfma<KS, NT, false, PF>), dim3(grid), dim3(NT), 0, s, (const bf16_t*)X, ldx, xm,    \
+                       stats, lg, lb, Wt, bias, (bf16_t*)Y, ldy, ym, B, H, W, C, ncg, ipb, nunits)
   // 16 waves x 2 channels, 2 images in flight (k = 7 at the M shape: 1 / 2 / 3 / 4 images give
   // 53.4 / 51.2-51.5 / 54.4 / 55.2 us alone and M forward 10,212 / 10,255 / 10,213 / 10,201 img/s,
   // interleaved means, tools/r4_pf.sh)
@@ -1040,18 +1007,16 @@ static int launch_dw3(int variant, int k, const void* X, int64_t ldx, RowMap xm,
     default: return -1;
   }
 #undef SDP_DW3
-#undef SDP_DW3V
   return SDP_CHECK_LAUNCH();
 }
 
 // Highest kernel tier allowed (each tier falls back to the next lower one per shape):
-// 4 = dwconv3_mfma with the tap-row A fragments moved by DPP (two LDS reads per channel instead of
-// KS), 3 (default) = dwconv3_mfma where it applies (bf16, H, W <= 16, C % 32 == 0, k in {3,5,7}),
+// 3 (default) = dwconv3_mfma where it applies (bf16, H, W <= 16, C % 32 == 0, k in {3,5,7}),
 // 2 = dwconv2_nhwc (C % 8 == 0, 16-B rows), 1 = dwconv_ln_nhwc (any shape)
 static int g_dw_kernel = 3;
 extern "C" int sdp_dwconv_set_kernel(int k) {
   const int old = g_dw_kernel;
-  if (k >= 1 && k <= 4) g_dw_kernel = k;
+  if (k >= 1 && k <= 3) g_dw_kernel = k;
   return old;
 }
 
@@ -1074,7 +1039,7 @@ extern "C" int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int6
                    ((uintptr_t)Y % 16 == 0) && (!stats || ((uintptr_t)stats % 8 == 0));
   if (g_dw_kernel >= 3 && dtype == 1 && C % 32 == 0 && H <= 16 && W <= 16 && v16 && (k == 3 || k == 5 || k == 7) &&
       ((uintptr_t)weight % 4 == 0)) {
-    const int rc = launch_dw3(g_dw_kernel, k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s);
+    const int rc = launch_dw3(k, X, ldx, xm, stats, ln_gamma, ln_beta, weight, bias, Y, ldy, ym, B, H, W, C, s);
     if (rc != -1) return rc;
   }
   if (g_dw_kernel >= 2 && C % 8 == 0 && v16 && (k == 3 || k == 5 || k == 7)) {

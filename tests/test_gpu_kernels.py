@@ -291,6 +291,26 @@ def test_attention_fused_qk_norm(dtype, B, N, H, hd, kern):
     close(o, ref, dtype, rel=2e-5 if dtype == torch.float32 else 2e-2, what=f"fused qk-norm attn variant {v}")
 
 
+@pytest.mark.parametrize("N", [200, 260, 77])
+@pytest.mark.parametrize("kern", [2, 3, 4, 5])
+def test_attention_images_isolated(N, kern):
+    # the K / V staging of one (image, head) pair reads nothing of the next image: NaNs there leave
+    # the first image's output bit-identical to a batch of that image alone
+    H, hd = 8, 96
+    C = H * hd
+    qkv = rnd(2 * N, 3 * C, dtype=BF, seed=49)
+    qkv[N:] = float("nan")
+    o2 = torch.empty(2 * N, C, dtype=BF, device=DEV)
+    o1 = torch.empty(N, C, dtype=BF, device=DEV)
+    old = sp.lib().sdp_attention_set_kernel(kern)
+    try:
+        sp.attention(qkv, o2, 2, N, H, hd)
+        sp.attention(qkv[:N].clone(), o1, 1, N, H, hd)
+    finally:
+        sp.lib().sdp_attention_set_kernel(old)
+    assert torch.equal(o2[:N], o1)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
 def test_attention_mask(dtype):
     B, N, H, hd = 2, 40, 4, 16

@@ -16,20 +16,38 @@ sys.path.insert(0, os.path.join(REPO, "sdp-net_amd"))
 import torch  # noqa: E402
 import sdpnet_hip as sp  # noqa: E402
 
-# name: (M, N, K, bias, act, resid)
+# name: (M, N, K, bias, act, resid, ln) -- the model's epilogues (sdp-net_amd/layers.py): a residual GEMM
+# also writes the next LayerNorm's row partials; ln = LayerNorm folded in (row stats + weight column sums)
 SHAPES = {
-    "mixer_cc": (50176, 768, 768, False, 1, True),
-    "mixer_up": (50176, 3072, 768, False, 1, False),
-    "mixer_down": (50176, 768, 3072, False, 0, True),
-    "enc_qkv": (51200, 2304, 768, False, 0, False),
-    "enc_o": (51200, 768, 768, False, 0, True),
-    "enc_ff1": (51200, 3072, 768, True, 1, False),
-    "enc_ff2": (51200, 768, 3072, True, 0, True),
-    "sq8192": (8192, 8192, 8192, False, 0, False),
-    "mixer_up_noact": (50176, 3072, 768, False, 0, False),
-    "mixer_cc_noact": (50176, 768, 768, False, 0, True),
-    "mixer_cc_nores": (50176, 768, 768, False, 1, False),
+    "mixer_cc": (50176, 768, 768, True, 1, True, False),
+    "mixer_up": (50176, 3072, 768, True, 1, False, True),
+    "mixer_down": (50176, 768, 3072, True, 0, True, False),
+    "enc_qkv": (51200, 2304, 768, True, 0, False, True),
+    "enc_o": (51200, 768, 768, True, 0, True, False),
+    "enc_ff1": (51200, 3072, 768, True, 1, False, True),
+    "enc_ff2": (51200, 768, 3072, True, 0, True, False),
+    "sq8192": (8192, 8192, 8192, False, 0, False, False),
+    "mixer_up_noact": (50176, 3072, 768, True, 0, False, True),
+    "mixer_cc_noact": (50176, 768, 768, True, 0, True, False),
+    "mixer_cc_nores": (50176, 768, 768, True, 1, False, False),
 }
+
+
+def operands(name, g, dev):
+    """Synthetic operands of one shape, the epilogue inputs the model passes (SHAPES)."""
+    M, N, K, has_b, act, has_r, has_ln = SHAPES[name]
+    bf = torch.bfloat16
+    x = (torch.rand(M, K, generator=g) * 2 - 1).to(bf).to(dev)
+    w = ((torch.rand(N, K, generator=g) * 2 - 1) * 0.05).to(bf).to(dev)
+    b = torch.randn(N, generator=g).to(dev) if has_b else None
+    r = torch.randn(M, N, generator=g).to(bf).to(dev) if has_r else None
+    part = torch.empty(M, (N + 63) // 64, 2, device=dev) if has_r else None
+    ln = None
+    if has_ln:
+        st = torch.stack([torch.randn(M, generator=g) * 0.1, torch.rand(M, generator=g) + 0.5], 1).to(dev)
+        ln = (st.contiguous(), w.float().sum(1).contiguous())
+    y = torch.empty(M, N, dtype=bf, device=dev)
+    return M, N, K, act, x, w, b, r, part, ln, y
 
 
 def main():
@@ -50,17 +68,11 @@ def main():
                 for s_ in args.streams.split(",") for d in args.exact_gelu.split(",")
                 for c in ["0"] for e in args.epi_spec.split(",") for kl in args.kloop.split(",")]
     dev = torch.device("cuda")
-    bf = torch.bfloat16
     g = torch.Generator(device="cpu").manual_seed(0)
     total_us = {}
     ref_out = {}
     for name in args.shapes.split(","):
-        M, N, K, has_b, act, has_r = SHAPES[name]
-        x = (torch.rand(M, K, generator=g) * 2 - 1).to(bf).to(dev)
-        w = ((torch.rand(N, K, generator=g) * 2 - 1) * 0.05).to(bf).to(dev)
-        b = torch.randn(N, generator=g).to(dev) if has_b else None
-        r = torch.randn(M, N, generator=g).to(bf).to(dev) if has_r else None
-        y = torch.empty(M, N, dtype=bf, device=dev)
+        M, N, K, act, x, w, b, r, part, ln, y = operands(name, g, dev)
         for kern, ns, dsy, sch, spc, kl in combos():
             sp.lib().sdp_gemm_set_epi_spec(spc)
             sp.lib().sdp_gemm_set_kloop_phases(kl)
@@ -80,7 +92,9 @@ def main():
                 for s, (lo, hi) in zip(streams, parts):
                     with torch.cuda.stream(s):
                         sp.gemm(sp.dense(x[lo:hi]), w, sp.dense(y[lo:hi]), hi - lo, N, K, bias=b,
-                                resid=None if r is None else sp.dense(r[lo:hi]), act=act)
+                                resid=None if r is None else sp.dense(r[lo:hi]), act=act,
+                                ln=None if ln is None else (ln[0][lo:hi], ln[1]),
+                                part=None if part is None else part[lo:hi])
                 for s in streams:
                     cur.wait_stream(s)
 

@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import sdpnet_hip as sp  # noqa: E402
-from gemm_bench import SHAPES  # noqa: E402
+from gemm_bench import operands  # noqa: E402
 
 
 def main():
@@ -33,16 +33,11 @@ def main():
     L = sp.lib()
     L.sdp_gemm_phase_stamps.argtypes = [ctypes.c_void_p]
     dev = torch.device("cuda")
-    bf = torch.bfloat16
     g = torch.Generator(device="cpu").manual_seed(0)
     for name in args.shapes.split(","):
-        M, N, K, has_b, act, has_r = SHAPES[name]
-        x = (torch.rand(M, K, generator=g) * 2 - 1).to(bf).to(dev)
-        w = ((torch.rand(N, K, generator=g) * 2 - 1) * 0.05).to(bf).to(dev)
-        r = torch.randn(M, N, generator=g).to(bf).to(dev) if has_r else None
-        y = torch.empty(M, N, dtype=bf, device=dev)
-        run = lambda: sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K,  # noqa: E731
-                              resid=None if r is None else sp.dense(r), act=act)
+        M, N, K, act, x, w, b, r, part, ln, y = operands(name, g, dev)
+        run = lambda: sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, bias=b,  # noqa: E731
+                              resid=None if r is None else sp.dense(r), act=act, ln=ln, part=part)
         for _ in range(30):
             run()
         torch.cuda.synchronize()

@@ -1,12 +1,12 @@
 """Per-workgroup timeline of the 8-phase GEMM from the stamped diagnostic library.
 
   make -C sdp-net_amd/csrc stamps
-  python tools/gemm_stamps.py [--shapes mixer_cc,mixer_up] [--schedules 0,1]
+  python tools/gemm_stamps.py [--shapes mixer_cc,mixer_up] [--epi-wait 0,1]
 
 Loads sdp-net_amd/lib_stamps/libsdpnet_hip.so (built with -DSDP_GEMM_STAMPS: every
 workgroup records s_memrealtime at its start, each segment start, after the prologue
-wait, after the k-loop, after the epilogue / partial store, and around a stream-K wait)
-and prints, per shape and schedule, the mean time of each part per segment and how many
+wait, after the k-loop, after the epilogue; wave 0 also stamps the epilogue's parts)
+and prints, per shape, the mean time of each part per segment and how many
 workgroups are in their epilogue at once (the store bursts).
 """
 import argparse
@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import sdpnet_hip as sp  # noqa: E402
-from gemm_bench import SHAPES  # noqa: E402
+from gemm_bench import operands  # noqa: E402
 
 TICK_US = 0.01  # s_memrealtime runs at 100 MHz
 
@@ -47,7 +47,7 @@ def analyse(st, label):
     epi_iv = []
     nseg = []
     for w in range(st.shape[0]):
-        ev = [(int(c), int(x) - t0) for c, x, v in zip(codes[w], t[w], valid[w]) if v]
+        ev = [(int(c), int(x) - t0) for c, x, v in zip(codes[w][:40], t[w][:40], valid[w][:40]) if v]
         if not ev:
             continue
         nseg.append(sum(1 for c, _ in ev if c >= 0x10))
@@ -70,6 +70,14 @@ def analyse(st, label):
                 (parts["head_store"] if mode == 1 else parts["epilogue"]).append(x - last["e"])
                 if mode != 1:
                     epi_iv.append((last["e"], x))
+    # epilogue sub-phases (fast epilogue only): slots 40.. hold codes 0x20 + k
+    es = st[:, 40:45]
+    if (es != 0).all(axis=1).any():
+        ok = (es != 0).all(axis=1)
+        et = (es[ok] & np.uint64((1 << 56) - 1)).astype(np.int64)
+        names = ["resid loads", "stage", "LDS read-back", "drain + stores"]
+        print("    epilogue parts (wave 0): " + ", ".join(
+            f"{n} {np.mean(et[:, k + 1] - et[:, k]) * TICK_US:.2f}" for k, n in enumerate(names)) + " us")
     span = (tend - t0) * TICK_US
     print(f"  {label}: span {span:.1f} us over {st.shape[0]} workgroups, segments/wg {np.mean(nseg):.2f}")
     for k, v in parts.items():
@@ -88,27 +96,23 @@ def analyse(st, label):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="mixer_cc,mixer_up,mixer_down,enc_qkv")
-    ap.add_argument("--schedules", default="0")
+    ap.add_argument("--epi-wait", default="0", help="1: drain memory counters before each epilogue stamp")
     ap.add_argument("--dephase", default="0", help="first-round start offsets per group of 8 workgroups per XCD, "
                     "in 10-ns ticks (experiment: group g = (b >> 3) & 3 waits g * value)")
     args = ap.parse_args()
     L = sp.lib()
     L.sdp_gemm_set_dephase.argtypes = [ctypes.c_int]
+    L.sdp_gemm_set_epi_wait.argtypes = [ctypes.c_int]
     dev = torch.device("cuda")
-    bf = torch.bfloat16
     g = torch.Generator(device="cpu").manual_seed(0)
     for name in args.shapes.split(","):
-        M, N, K, has_b, act, has_r = SHAPES[name]
-        x = (torch.rand(M, K, generator=g) * 2 - 1).to(bf).to(dev)
-        w = ((torch.rand(N, K, generator=g) * 2 - 1) * 0.05).to(bf).to(dev)
-        b = torch.randn(N, generator=g).to(dev) if has_b else None
-        r = torch.randn(M, N, generator=g).to(bf).to(dev) if has_r else None
-        y = torch.empty(M, N, dtype=bf, device=dev)
+        M, N, K, act, x, w, b, r, part, ln, y = operands(name, g, dev)
         print(f"{name} M={M} N={N} K={K}")
-        for sch, dph in [(int(c), int(d)) for c in args.schedules.split(",") for d in args.dephase.split(",")]:
+        for ew, dph in [(int(c), int(d)) for c in args.epi_wait.split(",") for d in args.dephase.split(",")]:
             assert L.sdp_gemm_set_dephase(dph) == 0
+            assert L.sdp_gemm_set_epi_wait(ew) == 0
             run = lambda: sp.gemm(sp.dense(x), w, sp.dense(y), M, N, K, bias=b,  # noqa: E731
-                                  resid=None if r is None else sp.dense(r), act=act)
+                                  resid=None if r is None else sp.dense(r), act=act, ln=ln, part=part)
             for _ in range(30):
                 run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -117,12 +121,11 @@ def main():
                 run()
             e1.record()
             torch.cuda.synchronize()
-            print(f"  dephase {dph} ticks: {1e3 * e0.elapsed_time(e1) / 20:.1f} us per launch (events)")
+            print(f"  epi_wait {ew} dephase {dph} ticks: {1e3 * e0.elapsed_time(e1) / 20:.1f} us per launch (events)")
             read_stamps(1)
             run()
-            sk = 0
-            nwg = 256 if sk else ((M + 255) // 256) * ((N + 255) // 256)
-            analyse(read_stamps(nwg), f"schedule {sch} ({'stream-K' if sk else 'data-parallel'})")
+            nwg = ((M + 255) // 256) * ((N + 255) // 256)
+            analyse(read_stamps(nwg), f"epi_wait {ew}")
 
 
 if __name__ == "__main__":
