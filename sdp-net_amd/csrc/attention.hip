@@ -959,6 +959,26 @@ SDP_DEV void attn_knorm32(bf16_t* Kd, int row0, int NP16, int lane, const float*
 // next slot's Q fragments (the next pair's slot 0 after slot 1).
 // LDS: (K + V) x NP16 x HD x 2 B + 4 x HD x 4 B  (N = 200, hd = 96: 81,408 B).
 // ---------------------------------------------------------------------------
+#ifdef SDP_GEMM_STAMPS
+// Diagnostic build only (tools/attn_stamps.py): per workgroup, per pair j < 8, the shader clock
+// (s_memtime) of waves 0 and 3 at: pair start, K/V landed (after the barrier), k-norm done,
+// slot 0 done, slot 1 done.  [wg][wave 0|3][j][5]
+__device__ unsigned long long g_attn_stamps[1024 * 2 * 8 * 5];
+#define SDP_ASTAMP(j, k)                                                                               \
+  do {                                                                                                 \
+    if ((wave == 0 || wave == 3) && lane == 0 && (j) < 8 && blockIdx.x < 1024)                         \
+      g_attn_stamps[(((int64_t)blockIdx.x * 2 + (wave == 3)) * 8 + (j)) * 5 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+// attn_fa5: waves 0 (a compute wave) and 7 (the producer) in the same slots
+#define SDP_ASTAMP5(j, k)                                                                              \
+  do {                                                                                                 \
+    if ((wave == 0 || wave == 7) && lane == 0 && (j) < 8 && blockIdx.x < 1024)                         \
+      g_attn_stamps[(((int64_t)blockIdx.x * 2 + (wave == 7)) * 8 + (j)) * 5 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define SDP_ASTAMP(j, k) do {} while (0)
+#define SDP_ASTAMP5(j, k) do {} while (0)
+#endif
 template <int HDT, int NKT>
 __global__ __launch_bounds__(256, 2) void attn_fa4_bf16(const bf16_t* __restrict__ QKV, int64_t ldq,
                                                      bf16_t* __restrict__ O, int64_t ldo, int B, int N, int H,
@@ -1013,27 +1033,139 @@ __global__ __launch_bounds__(256, 2) void attn_fa4_bf16(const bf16_t* __restrict
   attn_load_q<HDT>(qkv_base(pair) + off0, hf, qa);
   for (int j = 0; j < nj; ++j) {
     const int nxt = j + 1 < nj ? pair_of(j + 1) : pair;  // last pair: a harmless re-load
+    SDP_ASTAMP(j, 0);
     stage(pair);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    SDP_ASTAMP(j, 1);
     if (norm) {
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr)
         if (32 * (wave + 4 * rr) < NP16) attn_knorm32<HDT>(Ks, 32 * (wave + 4 * rr), NP16, lane, prm + 2 * HD, prm + 3 * HD, eps);
       __syncthreads();
     }
+    SDP_ASTAMP(j, 2);
     const int b = pair / H, hh = pair - (pair / H) * H;
     bf16_t* obase = O + (int64_t)b * N * ldo + hh * HD;
     // slot 0 (query tile w), prefetching slot 1's Q
     if (norm) attn_norm_q<HDT>(qa, ok0, hf, prm, prm + HD, eps);
     attn_qtile_chunked<HDT, NKT, (HDT <= 3 ? ATTN_CH : 4)>(Ks, Vs, qa, N, scale_log2, lane, ok0 ? obase + q0 * ldo : nullptr,
                                           qkv_base(pair) + off1, qb);
+    SDP_ASTAMP(j, 3);
     // slot 1 (query tile w + 4), prefetching the next pair's slot 0
     if (norm) attn_norm_q<HDT>(qb, ok1, hf, prm, prm + HD, eps);
     attn_qtile_chunked<HDT, NKT, (HDT <= 3 ? ATTN_CH : 4)>(Ks, Vs, qb, N, scale_log2, lane, ok1 ? obase + q1 * ldo : nullptr,
                                           qkv_base(nxt) + off0, qa);
+    SDP_ASTAMP(j, 4);
     pair = nxt;
     __syncthreads();  // every wave is done with K / V before the next pair's DMA
+  }
+}
+
+// ---------------------------------------------------------------------------
+// attn_fa5_bf16 — one persistent 8-wave workgroup per CU with K / V double-buffered in LDS
+// (2 x (K + V) x NP16 x HD x 2 B + gamma / beta; N = 200, hd = 96: 161,280 of 163,840 B).
+// Waves 0..6 own query tiles 0..6 (N <= 224: one 32-row tile each, none of them padding -- fa4
+// computes 8 slots for 7 tiles) and compute pair j out of buffer j & 1 with the chunked
+// whole-tile softmax, prefetching their next Q tile.  Wave 7 is the producer: it stages pair j + 1
+// into the other buffer (buffer LDS-DMA, K then V) while pair j computes, so the staging latency
+// hides behind a whole pair.  After the pair's barrier all eight waves k-normalise the next K (32
+// rows each, ~2.2k cycles) before a second barrier (fa4: stage -> barrier -> k-norm -> barrier ->
+// compute, per pair, two workgroups per CU).  The producer k-normalising alone (one barrier per
+// pair) measured 129 vs 91-97 us: one wave's k-norm of 208 rows outlasts the compute.
+// ---------------------------------------------------------------------------
+template <int HDT, int NKT>
+__global__ __launch_bounds__(512) void attn_fa5_bf16(const bf16_t* __restrict__ QKV, int64_t ldq,
+                                                  bf16_t* __restrict__ O, int64_t ldo, int B, int N, int H,
+                                                  const float* __restrict__ gq, const float* __restrict__ bq,
+                                                  const float* __restrict__ gk, const float* __restrict__ bk,
+                                                  float eps, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  constexpr int HD = 32 * HDT;
+  const int NP16 = (N + 15) / 16 * 16;
+  const size_t kvb = (size_t)NP16 * HD * sizeof(bf16_t);  // bytes of one K (or V) image
+  float* const prm = (float*)(sm + 4 * kvb);              // gq | bq | gk | bk
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int npairs = B * H, G = gridDim.x, x = blockIdx.x;
+  const int nj = (npairs - x + G - 1) / G;
+  if (nj <= 0) return;
+  const int C = H * HD;
+  const bool norm = gq != nullptr;
+  if (norm) {
+    for (int i = tid; i < 4 * HD; i += 512) {
+      const int k = i / HD, d = i - k * HD;
+      prm[i] = (k == 0 ? gq : k == 1 ? bq : k == 2 ? gk : bk)[d];
+    }
+  }
+  auto pair_of = [&](int j) {  // XCD-contiguous pair order, as attn_fa4 (G % 8 == 0)
+    const int v = x + j * G;
+    const int xcd = v & 7, qd = npairs >> 3, rem = npairs & 7;
+    return (xcd < rem ? xcd * (qd + 1) : rem * (qd + 1) + (xcd - rem) * qd) + (v >> 3);
+  };
+  auto qkv_base = [&](int pair) {
+    const int b = pair / H, hh = pair - (pair / H) * H;
+    return QKV + (int64_t)b * N * ldq + hh * HD;
+  };
+  auto kbuf = [&](int i) { return (bf16_t*)(sm + (size_t)(2 * i) * kvb); };
+  auto vbuf = [&](int i) { return (bf16_t*)(sm + (size_t)(2 * i + 1) * kvb); };
+  const bool producer = wave == 7;
+  const AttnKV<HDT> kv(lane, ldq, C);
+  // producer: pair -> buffer i (K units, then V units), all landed before it joins the barrier
+  auto produce = [&](int pair, int i) {
+    const int hh = pair - (pair / H) * H;
+    kv.issue(qkv_base(pair), (uint64_t)((int64_t)(N - 1) * ldq + 3 * C - hh * HD) * 2, (char*)kbuf(i), (char*)vbuf(i),
+             NP16, ldq, 0, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  const int r = lane & 31, hf = lane >> 5;
+  const bool has_tile = !producer && wave * 32 < N;
+  const int q0 = wave * 32 + r;
+  const bool ok0 = q0 < N;
+  const int64_t off0 = (int64_t)(ok0 ? q0 : N - 1) * ldq;
+  bf16x8 qa[2 * HDT], qb[2 * HDT];
+  int pair = pair_of(0);
+  // barrier without the vmcnt(0) of __syncthreads: a compute wave's O stores and Q prefetch
+  // stay in flight across it (the producer has waited for its DMA; LDS accesses are retired)
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // k-norm of buffer i by all eight waves, 32 rows each, between two barriers
+  auto knorm_all = [&](int i) {
+    if (32 * wave < NP16) attn_knorm32<HDT>(kbuf(i), 32 * wave, NP16, lane, prm + 2 * HD, prm + 3 * HD, eps);
+  };
+  if (producer) produce(pair, 0);
+  else if (has_tile) attn_load_q<HDT>(qkv_base(pair) + off0, hf, qa);
+  __syncthreads();
+  if (norm) {
+    knorm_all(0);
+    barrier();
+  }
+  for (int j = 0; j < nj; ++j) {
+    const int nxt = j + 1 < nj ? pair_of(j + 1) : pair;  // last pair: a harmless re-load
+    SDP_ASTAMP5(j, 0);
+    if (producer) {
+      if (j + 1 < nj) produce(nxt, (j + 1) & 1);
+    } else if (has_tile) {
+      const int b = pair / H, hh = pair - (pair / H) * H;
+      bf16_t* obase = O + (int64_t)b * N * ldo + hh * HD;
+      if (norm) attn_norm_q<HDT>(qa, ok0, hf, prm, prm + HD, eps);
+      attn_qtile_chunked<HDT, NKT, (HDT <= 3 ? ATTN_CH : 4)>(kbuf(j & 1), vbuf(j & 1), qa, N, scale_log2, lane,
+                                                             ok0 ? obase + q0 * ldo : nullptr, qkv_base(nxt) + off0, qb);
+#pragma unroll
+      for (int s = 0; s < 2 * HDT; ++s) qa[s] = qb[s];
+    }
+    pair = nxt;
+    SDP_ASTAMP5(j, 1);
+    barrier();  // pair j's buffer free, pair j + 1's staged
+    SDP_ASTAMP5(j, 2);
+    if (norm && j + 1 < nj) {
+      knorm_all((j + 1) & 1);
+      SDP_ASTAMP5(j, 3);
+      barrier();
+    }
+    SDP_ASTAMP5(j, 4);
   }
 }
 
@@ -1213,6 +1345,14 @@ extern "C" int sdp_attn_set_per_cu(int n) {
   return old;
 }
 
+#ifdef SDP_GEMM_STAMPS
+extern "C" int sdp_attn_stamps(void* dst, int64_t bytes) {
+  hipError_t rc = hipDeviceSynchronize();
+  if (rc == hipSuccess && bytes >= (int64_t)sizeof(g_attn_stamps))
+    rc = hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps));
+  return (int)rc;
+}
+#endif
 static size_t attn_fa4_bytes(int N, int hd) { return (size_t)2 * ((N + 15) / 16 * 16) * hd * 2 + 16 * (size_t)hd; }
 
 template <int HDT>
@@ -1260,6 +1400,42 @@ static int launch_attn_fa4(const void* QKV, int64_t ldq, void* O, int64_t ldo, i
   return SDP_CHECK_LAUNCH();
 }
 
+static size_t attn_fa5_bytes(int N, int hd) { return (size_t)4 * ((N + 15) / 16 * 16) * hd * 2 + 16 * (size_t)hd; }
+
+template <int HDT>
+static int launch_attn_fa5(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H,
+                           const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
+                           hipStream_t s) {
+  const size_t bytes = attn_fa5_bytes(N, 32 * HDT);
+  const void* fn = nullptr;
+  switch ((N + 31) / 32) {
+    case 1: fn = (const void*)attn_fa5_bf16<HDT, 1>; break;
+    case 2: fn = (const void*)attn_fa5_bf16<HDT, 2>; break;
+    case 3: fn = (const void*)attn_fa5_bf16<HDT, 3>; break;
+    case 4: fn = (const void*)attn_fa5_bf16<HDT, 4>; break;
+    case 5: fn = (const void*)attn_fa5_bf16<HDT, 5>; break;
+    case 6: fn = (const void*)attn_fa5_bf16<HDT, 6>; break;
+    case 7: fn = (const void*)attn_fa5_bf16<HDT, 7>; break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) return (int)e;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  int grid = ncu / 8 * 8;  // one workgroup per CU (LDS); pair order needs grid % 8 == 0
+  if (grid < 8) grid = 8;
+  if (grid > B * H) grid = B * H;
+  const float sl = scale * 1.4426950408889634f;
+  const bf16_t* q = (const bf16_t*)QKV;
+  bf16_t* o = (bf16_t*)O;
+  void* args[] = {(void*)&q, (void*)&ldq, (void*)&o, (void*)&ldo, (void*)&B, (void*)&N, (void*)&H, (void*)&gq,
+                  (void*)&bq, (void*)&gk, (void*)&bk, (void*)&eps, (void*)&sl};
+  e = hipLaunchKernel(fn, dim3(grid), dim3(512), args, bytes, s);
+  if (e != hipSuccess) return (int)e;
+  return SDP_CHECK_LAUNCH();
+}
+
 template <int HDT>
 static int launch_attn_fa(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H, int hd,
                           const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
@@ -1286,17 +1462,19 @@ static size_t attn_fa_bytes(int N, int hd) {
 }
 
 // bf16 flash kernel selection: 2 = attn_fa_bf16, 3 = attn_fa2_bf16, 4 (default) =
-// attn_fa4_bf16 (each where it applies, else the next lower one), 5 = attn_fs_bf16 (any N)
+// attn_fa4_bf16 (each where it applies, else the next lower one), 5 = attn_fs_bf16 (any N),
+// 6 = attn_fa5_bf16 where it applies (N <= 224, double-buffered K / V within 160 KiB), else 4
 static int g_attn_kernel = 4;
 extern "C" int sdp_attention_set_kernel(int k) {
   const int old = g_attn_kernel;
-  if (k >= 2 && k <= 5) g_attn_kernel = k;
+  if (k >= 2 && k <= 6) g_attn_kernel = k;
   return old;
 }
 
 extern "C" int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask) {
   if (dtype != 1 || has_mask || head_dim > 128 || head_dim % 16 != 0) return 0;
   if (g_attn_kernel == 5 && head_dim % 32 == 0) return 5;
+  if (g_attn_kernel == 6 && head_dim % 32 == 0 && N <= 224 && attn_fa5_bytes(N, head_dim) <= 160 * 1024) return 6;
   if (g_attn_kernel >= 4 && head_dim % 32 == 0 && N <= 256 && attn_fa4_bytes(N, head_dim) <= 160 * 1024) return 4;
   if (g_attn_kernel >= 3 && head_dim % 32 == 0 && attn_fa2_bytes(N, head_dim) <= 160 * 1024) return 3;
   if (attn_fa_bytes(N, head_dim) > 160 * 1024) return 0;
@@ -1328,6 +1506,16 @@ extern "C" int sdp_attention(int dtype, const void* QKV, int64_t ldq, void* O, i
       case 2: return launch_attn_fs<2>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
       case 3: return launch_attn_fs<3>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
       default: return launch_attn_fs<4>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+    }
+  }
+  if (variant == 6) {
+    const float *gq = norm ? q_gamma : nullptr, *bq = norm ? q_beta : nullptr;
+    const float *gk = norm ? k_gamma : nullptr, *bk = norm ? k_beta : nullptr;
+    switch (head_dim / 32) {
+      case 1: return launch_attn_fa5<1>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      case 2: return launch_attn_fa5<2>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      case 3: return launch_attn_fa5<3>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
+      default: return launch_attn_fa5<4>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
     }
   }
   if (variant == 4) {

@@ -742,11 +742,15 @@ SDP_DEV void tile_epilogue_fl(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0
     }
   };
   SDP_ESTAMP(0);
+  // residual rows j loaded just before stage(j): a wave that issues all 16 loads at once stalls at
+  // issue for as long as the memory pipeline takes to accept them (~3.7 us per tile with every CU
+  // in its epilogue, tools/gemm_stamps.py); interleaved, the staging VALU runs in that time
   u32x4 rres[8][2];
-  if constexpr (HR) {
-    const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc((void*)epi.resid, 0, (int)epi.res_bytes, 0x00020000);
-    RowOff rw(epi.rmap, mb, (uint32_t)epi.ldr * 2u);
-    static_for<0, 8>([&](auto j) {
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t rrs;
+  RowOff rw(epi.rmap, mb, (uint32_t)epi.ldr * 2u);
+  if constexpr (HR) rrs = __builtin_amdgcn_make_buffer_rsrc((void*)epi.resid, 0, (int)epi.res_bytes, 0x00020000);
+  static_for<0, 8>([&](auto j) {
+    if constexpr (HR) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int m = mb + j * 16 + 8 * q;
@@ -754,10 +758,11 @@ SDP_DEV void tile_epilogue_fl(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int m0
         rw.step8();
         rres[j][q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, (m < M && col_ok) ? ro + colb : OFF_DROP, 0, 0));
       }
-    });
-  }
+    }
+    stage(j);
+    if constexpr (HR) __builtin_amdgcn_sched_barrier(0);  // keep each row group's loads before its staging
+  });
   SDP_ESTAMP(1);
-  static_for<0, 8>([&](auto j) { stage(j); });
   SDP_ESTAMP(2);
   // read every staged row back before the first store: one LDS round trip per wave instead of one
   // per row (hipcc keeps an LDS read below any earlier buffer store, which it cannot prove

@@ -245,7 +245,7 @@ def attn_ref(qkv, B, N, H, hd, add=None):
 @pytest.mark.parametrize("B,N,H,hd", [(2, 200, 8, 96), (1, 260, 8, 96), (3, 200, 8, 16), (2, 53, 4, 16),
                                       (1, 5, 2, 32), (2, 1, 8, 64), (1, 300, 2, 128), (2, 53, 8, 12),
                                       (1, 384, 8, 96), (1, 500, 4, 32)])
-@pytest.mark.parametrize("kern", [2, 3, 4, 5])
+@pytest.mark.parametrize("kern", [2, 3, 4, 5, 6])
 def test_attention(dtype, B, N, H, hd, kern):
     if dtype == torch.float32 and kern == 2:
         pytest.skip("kernel selection applies to bf16 only")
@@ -270,7 +270,7 @@ def test_attention_mfma_path_is_taken_for_canonical_shapes():
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
 @pytest.mark.parametrize("B,N,H,hd", [(2, 200, 8, 96), (1, 260, 8, 96), (2, 53, 4, 16), (1, 77, 2, 64),
                                       (2, 33, 8, 12), (1, 300, 2, 128)])
-@pytest.mark.parametrize("kern", [2, 3, 4, 5])
+@pytest.mark.parametrize("kern", [2, 3, 4, 5, 6])
 def test_attention_fused_qk_norm(dtype, B, N, H, hd, kern):
     if dtype == torch.float32 and kern == 2:
         pytest.skip("kernel selection applies to bf16 only")
@@ -292,7 +292,7 @@ def test_attention_fused_qk_norm(dtype, B, N, H, hd, kern):
 
 
 @pytest.mark.parametrize("N", [200, 260, 77])
-@pytest.mark.parametrize("kern", [2, 3, 4, 5])
+@pytest.mark.parametrize("kern", [2, 3, 4, 5, 6])
 def test_attention_images_isolated(N, kern):
     # the K / V staging of one (image, head) pair reads nothing of the next image: NaNs there leave
     # the first image's output bit-identical to a batch of that image alone
@@ -324,7 +324,7 @@ def test_attention_mask(dtype):
     close(o, attn_ref(qkv, B, N, H, hd, add), dtype, what="masked attn")
 
 
-@pytest.mark.parametrize("kern", [2, 3, 4, 5])
+@pytest.mark.parametrize("kern", [2, 3, 4, 5, 6])
 def test_attention_spiky_scores(kern):
     # large logits: softmax max-subtraction must hold (no inf/nan), one dominant key
     B, N, H, hd = 1, 200, 8, 96
