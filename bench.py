@@ -240,6 +240,12 @@ def library_record(env=os.environ):
     return {"knobs": knobs, "lib": os.path.relpath(os.path.realpath(sp.LIB_PATH), REPO), "lib_md5": md5}
 
 
+def _progress(rank, msg):
+    """One progress line on stderr (rank 0): long profiled runs print as they go."""
+    if rank == 0:
+        print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
 def train_step_bench(C, B, steps, warmup, dev, world, rank, local, global_batch):
     """BASELINE.json configs[4]: one training step = bf16-autocast forward + label-smoothed CE
     (training_tools.py:85-88) + backward (DDP bucketed gradient all-reduce over RCCL when
@@ -271,9 +277,11 @@ def train_step_bench(C, B, steps, warmup, dev, world, rank, local, global_batch)
         opt.step(grad_scale=None, max_norm=5.0)  # unscale / inf check / clip / AdamW / scale update
         return loss
 
+    _progress(rank, f"{C['name']} training bs {B}: model built, {max(1, warmup)} warmup steps")
     for _ in range(max(1, warmup)):
         loss = step()
     torch.cuda.synchronize()
+    _progress(rank, "warmup done")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -351,9 +359,11 @@ def forward_bench(C, B, steps, warmup, dev, world, rank, streams=0, graph=True, 
         with torch.autocast("cuda", dtype=torch.bfloat16):
             return m(x)
 
+    _progress(rank, f"{C['name']} bs {B}: model built, {max(1, warmup)} warmup forwards")
     for _ in range(max(1, warmup)):
         y = step()
     torch.cuda.synchronize()
+    _progress(rank, "warmup done")
     pgraph = None
     if graph:
         s = torch.cuda.Stream(device=dev)
@@ -396,8 +406,10 @@ def forward_bench(C, B, steps, warmup, dev, world, rank, streams=0, graph=True, 
         "model_flops_per_image_gf": round(gf, 3),
         "model_mfma_frac": round(value * gf * 1e9 / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
     }
+    _progress(rank, f"{steps} timed forwards: {value:.1f} img/s")
     if roofline:
         out["roofline"] = gemm_roofline(step, dev, ms_step, config)
+        _progress(rank, "roofline replays done")
     del pgraph, m, x, y
     return out, cpu_sd
 
