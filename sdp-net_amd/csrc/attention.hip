@@ -1461,10 +1461,14 @@ static size_t attn_fa_bytes(int N, int hd) {
   return ((size_t)NP * (hd + 8) + (size_t)NP * (32 * HDT + 8)) * 2;
 }
 
-// bf16 flash kernel selection: 2 = attn_fa_bf16, 3 = attn_fa2_bf16, 4 (default) =
-// attn_fa4_bf16 (each where it applies, else the next lower one), 5 = attn_fs_bf16 (any N),
-// 6 = attn_fa5_bf16 where it applies (N <= 224, double-buffered K / V within 160 KiB), else 4
-static int g_attn_kernel = 4;
+// bf16 flash kernel selection (highest tier allowed; each applies where it fits, else the next):
+//   6 (default) attn_fa5_bf16: N <= 224, K / V double-buffered within 160 KiB (M: 91-102 vs fa4's
+//     103-109 us alone, model-neutral);
+//   4 attn_fa4_bf16: N <= 256, two workgroups per CU;
+//   3 attn_fa2_bf16: the whole head staged (XL, N = 260);
+//   then attn_fs_bf16 (5), the streaming kernel, for any longer N (hd % 32 == 0), and attn_fa_bf16
+//   (2) for hd % 32 != 0.  Setting 5 forces attn_fs_bf16; 2 allows only attn_fa_bf16.
+static int g_attn_kernel = 6;
 extern "C" int sdp_attention_set_kernel(int k) {
   const int old = g_attn_kernel;
   if (k >= 2 && k <= 6) g_attn_kernel = k;
@@ -1473,10 +1477,13 @@ extern "C" int sdp_attention_set_kernel(int k) {
 
 extern "C" int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask) {
   if (dtype != 1 || has_mask || head_dim > 128 || head_dim % 16 != 0) return 0;
-  if (g_attn_kernel == 5 && head_dim % 32 == 0) return 5;
-  if (g_attn_kernel == 6 && head_dim % 32 == 0 && N <= 224 && attn_fa5_bytes(N, head_dim) <= 160 * 1024) return 6;
-  if (g_attn_kernel >= 4 && head_dim % 32 == 0 && N <= 256 && attn_fa4_bytes(N, head_dim) <= 160 * 1024) return 4;
-  if (g_attn_kernel >= 3 && head_dim % 32 == 0 && attn_fa2_bytes(N, head_dim) <= 160 * 1024) return 3;
+  const bool hd32 = head_dim % 32 == 0;
+  if (g_attn_kernel == 5 && hd32) return 5;
+  if (g_attn_kernel == 6 && hd32 && N <= 224 && attn_fa5_bytes(N, head_dim) <= 160 * 1024) return 6;
+  if (g_attn_kernel >= 4 && g_attn_kernel != 5 && hd32 && N <= 256 && attn_fa4_bytes(N, head_dim) <= 160 * 1024)
+    return 4;
+  if (g_attn_kernel >= 3 && hd32 && attn_fa2_bytes(N, head_dim) <= 160 * 1024) return 3;
+  if (g_attn_kernel >= 3 && hd32) return 5;  // longer heads: streamed K / V tiles, any N
   if (attn_fa_bytes(N, head_dim) > 160 * 1024) return 0;
   return 2;
 }

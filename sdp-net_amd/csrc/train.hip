@@ -349,18 +349,37 @@ __global__ __launch_bounds__(256) void seg_colsum_v4(const T* __restrict__ X, in
   __shared__ f32x4 red[4][64];
   const int c = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4, sl = threadIdx.x >> 6, g = blockIdx.y;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  auto ld = [&](const T* q) -> f32x4 {
+    if constexpr (sizeof(T) == 2) {
+      const bf16x4 t = *(const bf16x4*)q;
+      return f32x4{bf2f((bf16_t)t[0]), bf2f((bf16_t)t[1]), bf2f((bf16_t)t[2]), bf2f((bf16_t)t[3])};
+    } else {
+      return *(const f32x4*)q;
+    }
+  };
   if (c < C) {
     const T* p = X + (int64_t)g * gstride * ldx + c;
-    for (int e = sl; e < len; e += 4) {
-      const T* q = p + (int64_t)e * estride * ldx;
-      if constexpr (sizeof(T) == 2) {
-        const bf16x4 t = *(const bf16x4*)q;
+    const int64_t rs = estride * ldx;
+    int e = sl;
+    // eight of the slice's rows loaded before any is added (the rows are independent; one load in
+    // flight per thread made the long, narrow reductions -- bias / LN-affine sums over token
+    // segments, the second level over 256-row partials -- latency-bound); the adds keep the
+    // row order, so the sums are bit-identical to the one-row loop
+    for (; e + 28 < len; e += 32) {
+      f32x4 v[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[r] += bf2f((bf16_t)t[r]);
-      } else {
-        s += *(const f32x4*)q;
-      }
+      for (int u = 0; u < 8; ++u) v[u] = ld(p + (int64_t)(e + 4 * u) * rs);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
     }
+    for (; e + 12 < len; e += 16) {
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = ld(p + (int64_t)(e + 4 * u) * rs);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; e < len; e += 4) s += ld(p + (int64_t)e * rs);
   }
   red[sl][threadIdx.x & 63] = s;
   __syncthreads();

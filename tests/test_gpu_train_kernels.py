@@ -97,6 +97,25 @@ def test_seg_colsum(dtype):
     close(out2, 1 + 0.5 * X.float().sum(0, keepdim=True), 1e-5, "scaled accumulate")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("G,len_,C", [(3, 77, 1024), (1, 28, 4096), (1, 7, 2048), (122, 256, 768), (1, 122, 3072)])
+def test_seg_colsum_vec4_summation_order(dtype, G, len_, C):
+    # the 4-column kernel (C % 4 == 0): thread slice sl sums rows sl, sl + 4, ... in row order,
+    # slices combined as ((s0 + s1) + s2) + s3 -- reproduced exactly in fp32 on the host
+    X = rnd(G * len_, C, seed=11, dtype=dtype)
+    out = torch.empty(G, C, dtype=torch.float32, device=DEV)
+    sp.seg_colsum(X, out, G, len_, len_, 1, C)
+    Xh = X.float().cpu().view(G, len_, C)
+    sl = []
+    for k in range(4):
+        acc = torch.zeros(G, C, dtype=torch.float32)
+        for e in range(k, len_, 4):
+            acc = acc + Xh[:, e]
+        sl.append(acc)
+    ref = ((sl[0] + sl[1]) + sl[2]) + sl[3]
+    assert torch.equal(out.cpu(), ref)
+
+
 ACT_REF = {0: lambda x: x, 1: F.gelu, 2: F.relu, 3: torch.tanh, 4: torch.sigmoid,
            5: lambda x: F.leaky_relu(x, 0.01), 6: F.selu,
            7: lambda x: torch.where(x < -3.5, torch.zeros_like(x), torch.where(
