@@ -123,12 +123,17 @@ SDP_DEV float act_grad(int act, float x) {
 // Lets one kernel address the image rows of a [B, R+P, C] token buffer (grp=P,
 // gstride=R+P, off=R), a plain dense matrix (grp=huge, gstride=0, off=0), or a
 // table broadcast over the batch (grp=P, gstride=0, off=0).
+// Logical rows are < 2^31 and grp > 0 (every constructor maps "dense" to grp = INT_MAX), so the
+// division runs in 32 bits: a 64-bit division is a ~40-instruction sequence (plus a branch to its
+// 32-bit fast path) per call, which per-row kernels paid once per operand and row.
 struct RowMap {
   int grp;
   int off;
   int64_t gstride;
   SDP_DEV int64_t operator()(int64_t m) const {
-    return (m / grp) * gstride + off + (m % grp);
+    const uint32_t mm = (uint32_t)m, g = (uint32_t)grp;
+    const uint32_t q = mm / g;
+    return (int64_t)q * gstride + off + (int64_t)(mm - q * g);
   }
 };
 

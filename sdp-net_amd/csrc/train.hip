@@ -856,7 +856,9 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
     const float mean = st[2 * m], rstd = st[2 * m + 1];
     const T* xp = X + xm(m) * ldx;
     const TD* dyp = DY + dym(m) * lddy;
-    V8<T> xh[V], gd[V];
+    T* dxp = DX + dxm(m) * lddx;
+    const T* ap = ADD ? ADD + am(m) * ldadd : nullptr;
+    V8<T> xh[V], gd[V], av[V];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
@@ -865,6 +867,7 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
         V8<TD> dy;
         dy.load(dyp + c);
         xh[i].load(xp + c);
+        if (ap) av[i].load(ap + c);  // the addend's loads go out with X / dY, before the row reductions
         const f32x4 g0 = *(const f32x4*)(g + c), g1 = *(const f32x4*)(g + c + 4);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -880,18 +883,15 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
     }
     s1 = wave_sum(s1) / (float)C;
     s2 = wave_sum(s2) / (float)C;
-    T* dxp = DX + dxm(m) * lddx;
-    const T* ap = ADD ? ADD + am(m) * ldadd : nullptr;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       const int c = 8 * lane + 512 * i;
       if (c < C) {
         V8<T> o;
-        if (ap) o.load(ap + c);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float v = rstd * (gd[i].v[q] - s1 - xh[i].v[q] * s2);
-          o.v[q] = ap ? o.v[q] + v : v;
+          o.v[q] = ap ? av[i].v[q] + v : v;
         }
         o.store(dxp + c);
       }

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 5 A/B against sdp-net_amd/lib_base (HEAD build): seg_colsum with eight rows in flight
-# (training) and attn_fa5 as the default attention (M forward).  Tests of the changed kernels first.
+# Round 5 A/B against sdp-net_amd/lib_base (the HEAD build) after the full GPU suite: XL training
+# step and M forward, interleaved.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -12,7 +12,7 @@ step() {  # name limit cmd...
   echo "== $n rc=$rc"; tail -2 "gpurun_out/$n.log"
   if [ $rc -ne 0 ]; then echo "ABORT after $n"; exit $rc; fi
 }
-step r5c_tests 900 python -u -m pytest tests/test_gpu_train_kernels.py tests/test_gpu_kernels.py tests/test_abi.py tests/test_train.py -x -q --timeout 240 --timeout-method thread -p no:cacheprovider
+step r5c_tests 1100 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider
 for v in base new base new; do
   if [ $v = base ]; then export SDPNET_HIP_LIB=$B; else unset SDPNET_HIP_LIB; fi
   step r5c_xlt_$v 400 python bench.py --config xl_train --steps 20 --warmup 3 --no-cpu-baseline --no-secondary
