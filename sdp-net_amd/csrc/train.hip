@@ -390,12 +390,57 @@ __global__ __launch_bounds__(256) void seg_colsum_v4(const T* __restrict__ X, in
   }
 }
 
+// Wide, short sums (the weight-gradient slab reduction: G = 1, len = split count <= 64, C = N x K):
+// each thread owns 8 consecutive columns and walks all len rows itself, eight rows (16 loads) in
+// flight at a time, adding them in row order -- out[c] = ((x_0 + x_1) + x_2) + ... exactly.
+// seg_colsum_v4's 4-row slices give such a sum only len / 4 loads per thread.
+__global__ __launch_bounds__(256) void colsum_wide_f32(const float* __restrict__ X, int64_t rs, int len, int C,
+                                                       float* __restrict__ out, float scale, int accum) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= C) return;
+  const float* p = X + c;
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  int e = 0;
+  for (; e + 8 <= len; e += 8) {
+    f32x4 a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = *(const f32x4*)(p + (int64_t)(e + u) * rs);
+      b[u] = *(const f32x4*)(p + (int64_t)(e + u) * rs + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s0 += a[u];
+      s1 += b[u];
+    }
+  }
+  for (; e < len; ++e) {
+    s0 += *(const f32x4*)(p + (int64_t)e * rs);
+    s1 += *(const f32x4*)(p + (int64_t)e * rs + 4);
+  }
+  f32x4* o = (f32x4*)(out + c);
+  const f32x4 v0 = scale * s0, v1 = scale * s1;
+  if (accum) {
+    o[0] += v0;
+    o[1] += v1;
+  } else {
+    o[0] = v0;
+    o[1] = v1;
+  }
+}
+
 extern "C" int sdp_seg_colsum(int dtype, const void* X, int64_t ldx, int G, int len, int64_t gstride,
                               int64_t estride, int C, float* out, int64_t ldo, float scale, int accum, void* stream) {
   if (!X || !out || G < 0 || len < 0 || C < 0) return (int)hipErrorInvalidValue;
   if (G == 0 || C == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const int es = dtype == 1 ? 2 : 4;
+  if (dtype == 0 && G == 1 && len <= 64 && C >= 65536 && C % 8 == 0 && (estride * ldx) % 4 == 0 &&
+      (uintptr_t)X % 16 == 0 && (uintptr_t)out % 16 == 0) {
+    hipLaunchKernelGGL(colsum_wide_f32, dim3((C / 8 + 255) / 256), dim3(256), 0, s, (const float*)X, estride * ldx, len,
+                       C, out, scale, accum);
+    return SDP_CHECK_LAUNCH();
+  }
   if (C % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && (uintptr_t)X % (4 * es) == 0 && (uintptr_t)out % 16 == 0) {
     dim3 g4((C / 4 + 63) / 64, G);
     if (dtype == 1)

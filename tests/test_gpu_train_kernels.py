@@ -116,6 +116,22 @@ def test_seg_colsum_vec4_summation_order(dtype, G, len_, C):
     assert torch.equal(out.cpu(), ref)
 
 
+@pytest.mark.parametrize("len_,C", [(7, 768 * 3072), (28, 768 * 768), (9, 2304 * 768), (3, 65536), (64, 131072)])
+def test_seg_colsum_wide_slab_sum_in_row_order(len_, C):
+    # the weight-gradient slab reduction (G = 1, few rows, C = N x K): out = ((x0 + x1) + x2) + ...
+    X = rnd(len_, C, seed=12)
+    out = torch.empty(1, C, dtype=torch.float32, device=DEV)
+    sp.seg_colsum(X, out, 1, len_, 0, 1, C)
+    Xh = X.cpu()
+    ref = torch.zeros(C, dtype=torch.float32)
+    for e in range(len_):
+        ref = ref + Xh[e]
+    assert torch.equal(out.cpu()[0], ref)
+    out2 = torch.ones(1, C, device=DEV)
+    sp.seg_colsum(X, out2, 1, len_, 0, 1, C, scale=0.5, accum=True)
+    assert torch.equal(out2.cpu()[0], 1 + 0.5 * ref)
+
+
 ACT_REF = {0: lambda x: x, 1: F.gelu, 2: F.relu, 3: torch.tanh, 4: torch.sigmoid,
            5: lambda x: F.leaky_relu(x, 0.01), 6: F.selu,
            7: lambda x: torch.where(x < -3.5, torch.zeros_like(x), torch.where(
