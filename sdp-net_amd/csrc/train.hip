@@ -500,6 +500,23 @@ struct V8 {
     }
   }
 };
+// 8 consecutive elements as loaded (bf16 stays packed: 4 registers instead of 8 until used)
+template <typename T>
+struct Raw8 {
+  typename std::conditional<sizeof(T) == 2, bf16x8, f32x4[2]>::type r;
+  SDP_DEV void load(const T* p) {
+    if constexpr (sizeof(T) == 2) {
+      r = *(const bf16x8*)p;
+    } else {
+      r[0] = *(const f32x4*)p;
+      r[1] = *(const f32x4*)(p + 4);
+    }
+  }
+  SDP_DEV float operator[](int q) const {
+    if constexpr (sizeof(T) == 2) return bf2f((bf16_t)r[q]);
+    else return r[q >> 2][q & 3];
+  }
+};
 
 template <typename T>
 __global__ __launch_bounds__(256) void act_fwd_v8(const T* __restrict__ Z, int64_t ldz, T* __restrict__ Y,
@@ -897,30 +914,53 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
   for (int i = 0; i < V; ++i)
 #pragma unroll
     for (int q = 0; q < 8; ++q) dg[i][q] = db[i][q] = 0.f;
-  for (int64_t m = (int64_t)blockIdx.x * 4 + w; m < M; m += (int64_t)gridDim.x * 4) {
-    const float mean = st[2 * m], rstd = st[2 * m + 1];
+  // software-pipelined over the wave's rows: row m + stride's X / dY / addend loads are issued
+  // before row m's reductions and stores, so each wave keeps one row of loads in flight while it
+  // computes (one row at a time left every wave waiting a memory round trip per row)
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  struct RowIn {
+    Raw8<T> x[V], a[V];
+    Raw8<TD> dy[V];
+    float mean, rstd;
+  };
+  auto fetch = [&](int64_t m, RowIn& r) {
+    r.mean = st[2 * m];
+    r.rstd = st[2 * m + 1];
     const T* xp = X + xm(m) * ldx;
     const TD* dyp = DY + dym(m) * lddy;
-    T* dxp = DX + dxm(m) * lddx;
     const T* ap = ADD ? ADD + am(m) * ldadd : nullptr;
-    V8<T> xh[V], gd[V], av[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int c = 8 * lane + 512 * i;
+      if (c < C) {
+        r.dy[i].load(dyp + c);
+        r.x[i].load(xp + c);
+        if (ap) r.a[i].load(ap + c);
+      }
+    }
+  };
+  int64_t m = (int64_t)blockIdx.x * 4 + w;
+  RowIn cur, nxt;
+  if (m < M) fetch(m, cur);
+  for (; m < M; m += stride) {
+    if (m + stride < M) fetch(m + stride, nxt);
+    const float mean = cur.mean, rstd = cur.rstd;
+    T* dxp = DX + dxm(m) * lddx;
+    V8<T> xh[V], gd[V];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       const int c = 8 * lane + 512 * i;
       if (c < C) {
-        V8<TD> dy;
-        dy.load(dyp + c);
-        xh[i].load(xp + c);
-        if (ap) av[i].load(ap + c);  // the addend's loads go out with X / dY, before the row reductions
         const f32x4 g0 = *(const f32x4*)(g + c), g1 = *(const f32x4*)(g + c + 4);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          const float x_ = (xh[i].v[q] - mean) * rstd;
+          const float dyq = cur.dy[i][q];
+          const float x_ = (cur.x[i][q] - mean) * rstd;
           xh[i].v[q] = x_;
-          gd[i].v[q] = dy.v[q] * (q < 4 ? g0[q] : g1[q - 4]);
-          dg[i][q] = fmaf(dy.v[q], x_, dg[i][q]);
-          db[i][q] += dy.v[q];
+          gd[i].v[q] = dyq * (q < 4 ? g0[q] : g1[q - 4]);
+          dg[i][q] = fmaf(dyq, x_, dg[i][q]);
+          db[i][q] += dyq;
           s1 += gd[i].v[q];
           s2 = fmaf(gd[i].v[q], x_, s2);
         }
@@ -936,11 +976,12 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float v = rstd * (gd[i].v[q] - s1 - xh[i].v[q] * s2);
-          o.v[q] = ap ? av[i].v[q] + v : v;
+          o.v[q] = ADD ? cur.a[i][q] + v : v;
         }
         o.store(dxp + c);
       }
     }
+    cur = nxt;
   }
   if (!part) return;
 #pragma unroll
