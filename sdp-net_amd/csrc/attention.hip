@@ -670,7 +670,7 @@ SDP_DEV void attn_qtile_pipe(const bf16_t* Ks, const bf16_t* Vs, const bf16x8 (&
 // tile, so the two waves of a SIMD overlap each other's phases.
 // The next Q tile (qnext) is loaded into qn after the last chunk's
 // exponentials, when the S^T registers are free: the loads overlap the P V^T phase.
-template <int HDT, int NKT, int CH>
+template <int HDT, int NKT, int CH, bool PF = true>
 SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8 (&qf)[2 * HDT], int N,
                                 float scale_log2, int lane, bf16_t* orow, const bf16_t* qnext,
                                 bf16x8 (&qn)[2 * HDT]) {
@@ -746,7 +746,7 @@ SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8
         }
         asm volatile("" : "+v"(pb[t][0]), "+v"(pb[t][1]), "+v"(l2));  // one tile's exponentials at a time
       }
-    if (c0 + n == NKT) {
+    if (PF && c0 + n == NKT) {
       asm volatile("" ::: "memory");
       attn_load_q<HDT>(qnext, hf, qn);
     }  // P complete before P V^T (bounds the live registers)
@@ -816,8 +816,14 @@ SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8
 //   * register budget 128 (4 waves / SIMD) for the 7-wave workgroups.
 // Needs hd % 32 == 0 (whole 4-chunk swizzle groups).
 // ---------------------------------------------------------------------------
-template <int HDT>
-__global__ __launch_bounds__(576) __attribute__((amdgpu_waves_per_eu(HDT <= 3 ? 4 : 2))) void attn_fa2_bf16(
+// NKT > 0: each query tile runs the chunked single-max softmax of attn_fa4 over NKT key tiles
+// (N <= 32 NKT; ATTN_CH2 tiles per chunk, no next-tile Q prefetch: one tile per wave) instead of
+// the per-key-tile online softmax (NKT = 0, any N).
+#ifndef ATTN_CH2
+#define ATTN_CH2 3  // at 168 VGPRs (three waves on a SIMD): 4 spills at hd 96
+#endif
+template <int HDT, int NKT = 0>
+__global__ __launch_bounds__(576) __attribute__((amdgpu_waves_per_eu(NKT > 0 ? 3 : (HDT <= 3 ? 4 : 2)))) void attn_fa2_bf16(
     const bf16_t* __restrict__ QKV, int64_t ldq, bf16_t* __restrict__ O, int64_t ldo, int B, int N, int H,
     const float* __restrict__ gq, const float* __restrict__ bq, const float* __restrict__ gk,
     const float* __restrict__ bk, float eps, float scale_log2) {
@@ -892,7 +898,11 @@ __global__ __launch_bounds__(576) __attribute__((amdgpu_waves_per_eu(HDT <= 3 ? 
     bf16x8 qf[2 * HDT];
     attn_load_q<HDT>(base + (int64_t)(qok ? q : N - 1) * ldq, hf, qf);
     if (gq) attn_norm_q<HDT>(qf, qok, hf, gq, bq, eps);
-    attn_qtile<HDT>(Ks, Vs, qf, N, nqt, scale_log2, lane, qok ? O + ((int64_t)b * N + q) * ldo + hh * HD : nullptr);
+    bf16_t* orow = qok ? O + ((int64_t)b * N + q) * ldo + hh * HD : nullptr;
+    if constexpr (NKT > 0)
+      attn_qtile_chunked<HDT, NKT, ATTN_CH2, false>(Ks, Vs, qf, N, scale_log2, lane, orow, nullptr, qf);
+    else
+      attn_qtile<HDT>(Ks, Vs, qf, N, nqt, scale_log2, lane, orow);
   }
 }
 
@@ -903,17 +913,24 @@ static int launch_attn_fa2(const void* QKV, int64_t ldq, void* O, int64_t ldo, i
                            const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
                            hipStream_t s) {
   const size_t bytes = attn_fa2_bytes(N, 32 * HDT);
-  if (bytes > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)attn_fa2_bf16<HDT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)bytes);
-    if (e != hipSuccess) return (int)e;
-  }
   // one query tile per wave up to 9 tiles (N <= 288: XL's 260 tokens are 8 full tiles + 4 rows;
-  // with 8 waves one wave did two tiles and set the block's time), else 8 waves looping
+  // with 8 waves one wave did two tiles and set the block's time), else 8 waves looping; at exactly
+  // 9 key tiles (XL) the chunked single-max softmax (hd <= 96: hd 128 would spill at 168 VGPRs)
   int waves = (N + 31) / 32;
   if (waves > 9) waves = 8;
-  hipLaunchKernelGGL(attn_fa2_bf16<HDT>, dim3(B * H), dim3(64 * waves), bytes, s, (const bf16_t*)QKV, ldq,
-                     (bf16_t*)O, ldo, B, N, H, gq, bq, gk, bk, eps, scale * 1.4426950408889634f);
+  const void* fn = waves == 9 && HDT <= 3 ? (const void*)attn_fa2_bf16<HDT, HDT <= 3 ? 9 : 0>
+                                          : (const void*)attn_fa2_bf16<HDT, 0>;
+  if (bytes > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return (int)e;
+  }
+  const float sl = scale * 1.4426950408889634f;
+  const bf16_t* q = (const bf16_t*)QKV;
+  bf16_t* o = (bf16_t*)O;
+  void* args[] = {(void*)&q, (void*)&ldq, (void*)&o, (void*)&ldo, (void*)&B, (void*)&N, (void*)&H, (void*)&gq,
+                  (void*)&bq, (void*)&gk, (void*)&bk, (void*)&eps, (void*)&sl};
+  const hipError_t e = hipLaunchKernel(fn, dim3(B * H), dim3(64 * waves), args, bytes, s);
+  if (e != hipSuccess) return (int)e;
   return SDP_CHECK_LAUNCH();
 }
 

@@ -5,7 +5,7 @@
 # (build that one from the commit to compare against and copy it there).  With --knob: the product
 # library with VAR=a against VAR=b (an SDPNET_* switch; bench.py records it in config.knobs).
 # WHAT (each run as A, B, A, B): m (M forward), xl (XL forward), xlt (XL bs120 training step),
-# gemm (single-stream GEMM per M forward, tools/gemm_bench.py), attn / dw (tools/kern_bench.py),
+# gemm (single-stream GEMM per M forward, tools/gemm_bench.py), attn / attnxl / dw (tools/kern_bench.py),
 # lnb (LN backward microbenchmark).  Logs: gpurun_out/ab_<what>_<variant>_<i>.log.
 set -o pipefail
 mkdir -p gpurun_out
@@ -48,6 +48,7 @@ for v in $variants; do
       xlt) step $n 400 python bench.py --config xl_train --steps 20 --warmup 3 --no-cpu-baseline --no-secondary ;;
       gemm) step $n 400 python tools/gemm_bench.py --shapes mixer_cc,mixer_up,mixer_down,enc_qkv,enc_o,enc_ff1,enc_ff2 ;;
       attn) step $n 200 python tools/kern_bench.py --only attn --attn-kerns 4,6 ;;
+      attnxl) step $n 200 python tools/kern_bench.py --only attn --attn-kerns 3 --shape xl ;;
       dw) step $n 200 python tools/kern_bench.py --only dw ;;
       lnb) step $n 120 python tools/lnb_bench.py ;;
       *) echo "unknown WHAT $what"; exit 2 ;;
