@@ -39,6 +39,8 @@ def main(path):
     rows = list(csv.DictReader(open(path)))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r["Queue_Id"])
                 for r in rows)
+    grid = {(int(r["Start_Timestamp"]), short(r["Kernel_Name"])):
+            "x".join(r.get(k, "?") for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z")) for r in rows}
     ends = [b for a, b, n, q in ev if n == "adamw_k"]
     if len(ends) < 2:
         sys.exit("need two optimizer launches in the trace")
@@ -57,6 +59,20 @@ def main(path):
         top = ", ".join(f"{n} {t / 1e6:.2f}" for n, t in fam.most_common(8))
         print(f"  queue {q}: {len(ks)} kernels, busy {busy / 1e6:.2f} ms ({100 * busy / wall:.0f} %), "
               f"kernel sum {sum(b - a for a, b, _ in ks) / 1e6:.2f} ms: {top}")
+    # the main queue's kernels by family: calls, total, mean, and the spread of one family (argv[2])
+    mq = max(byq, key=lambda q: sum(b - a for a, b, _ in byq[q]))
+    fam = collections.defaultdict(list)
+    for a, b, n in byq[mq]:
+        fam[n].append(b - a)
+    print(f"  queue {mq} by kernel (calls, total ms, mean us, min / median / max us):")
+    for n, d in sorted(fam.items(), key=lambda kv: -sum(kv[1]))[:16]:
+        d = sorted(d)
+        print(f"    {n:28s} {len(d):5d} {sum(d) / 1e6:7.2f} {sum(d) / len(d) / 1e3:8.1f}   "
+              f"{d[0] / 1e3:7.1f} {d[len(d) // 2] / 1e3:7.1f} {d[-1] / 1e3:7.1f}")
+    if len(sys.argv) > 2:  # the slowest launches of one kernel family on the main queue, with their grids
+        slow = sorted(((b - a, a, n) for a, b, n in byq[mq] if n == sys.argv[2]), reverse=True)[:12]
+        for d, a, n in slow:
+            print(f"    {n} {d / 1e3:7.1f} us at +{(a - t0) / 1e6:7.2f} ms, grid {grid.get((a, n), '?')}")
     # concurrency profile
     pts = sorted([(a, 1) for a, b, _, _ in win] + [(b, -1) for a, b, _, _ in win])
     lvl, last, hist = 0, t0, collections.Counter()
