@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round 5: PMC passes over the depthwise conv and the eval attention at the M shape (bs 256), one
+# Round 5: PMC passes over the depthwise conv and the eval attention (fa4 and fa5) at the M shape (bs 256), one
 # rocprofv3 run per pass, summarised per kernel; raw CSVs deleted afterwards (gpurun_out cap).
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-KB="python tools/kern_bench.py --only dw,attn --attn-kerns 4 --reps 5"
+KB="python tools/kern_bench.py --only dw,attn --attn-kerns 4,6 --reps 5"
 O=gpurun_out/r5_na
 rm -rf $O; mkdir -p $O
 i=0
@@ -13,5 +13,5 @@ for ctr in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   i=$((i+1))
   timeout -s KILL 150 rocprofv3 --pmc $ctr -d $O/p$i -o run --output-format csv -- $KB > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; exit 1; }
 done
-python tools/pmc_by_kernel.py $O/p1 $O/p2 --match dwconv3,attn_fa4 --json gpurun_out/r5_na_pmc.json
+python tools/pmc_by_kernel.py $O/p1 $O/p2 --match dwconv3,attn_fa4,attn_fa5 --json gpurun_out/r5_na_pmc.json
 rm -rf $O/p1 $O/p2
