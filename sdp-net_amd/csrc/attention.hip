@@ -1479,13 +1479,13 @@ static size_t attn_fa_bytes(int N, int hd) {
 }
 
 // bf16 flash kernel selection (highest tier allowed; each applies where it fits, else the next):
-//   6 (default) attn_fa5_bf16: N <= 224, K / V double-buffered within 160 KiB (M: 91-102 vs fa4's
-//     103-109 us alone, model-neutral);
-//   4 attn_fa4_bf16: N <= 256, two workgroups per CU;
+//   6 attn_fa5_bf16: N <= 224, K / V double-buffered within 160 KiB (M: 91-102 vs fa4's 103-109 us
+//     alone, but the M forward 0.25 % slower than with fa4 over 8 interleaved runs -- opt-in);
+//   4 (default) attn_fa4_bf16: N <= 256, two workgroups per CU;
 //   3 attn_fa2_bf16: the whole head staged (XL, N = 260);
 //   then attn_fs_bf16 (5), the streaming kernel, for any longer N (hd % 32 == 0), and attn_fa_bf16
 //   (2) for hd % 32 != 0.  Setting 5 forces attn_fs_bf16; 2 allows only attn_fa_bf16.
-static int g_attn_kernel = 6;
+static int g_attn_kernel = 4;
 extern "C" int sdp_attention_set_kernel(int k) {
   const int old = g_attn_kernel;
   if (k >= 2 && k <= 6) g_attn_kernel = k;
