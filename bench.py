@@ -482,18 +482,21 @@ def gemm_roofline(step, dev, ms_step, config, prof_steps=1):
                          tflops_co_running=round(e["fl"] / (e["ms"] * 1e-3) / 1e12, 1))
                  for k, e in per_shape.items()}
     union_ms_step = med["union_ms"]
-    achieved = fast_fl / (union_ms_step * 1e-3) / 1e12
+    # the GEMM union is measured on a replay of the timed schedule; when that replay runs slower than
+    # the timed steps (the union exceeds the step, e.g. at 4 sub-batch streams) the step itself is the
+    # denominator, i.e. the no-overlap lower bound
+    union_ok = union_ms_step <= ms_step * 1.02
+    achieved = fast_fl / ((union_ms_step if union_ok else ms_step) * 1e-3) / 1e12
     per_launch_tf = fast_fl / (fast_ms * 1e-3) / 1e12 if fast_ms else 0.0
     kname = FAST_GEMM_NAMES.get(sp.lib().sdp_gemm_set_fast_kernel(0), "?")
     traffic, traffic_src = measured_traffic(kname, config) if config in ("m", "xl") else (None, None)
-    # the GEMM union is measured on a replay of the timed schedule: it must fit in the timed step
-    # (a 2 % margin for replay-to-replay clock variation; the line reports both)
-    assert union_ms_step <= ms_step * 1.02, (union_ms_step, ms_step)
     return {"bound": "mfma", "kernel": kname,
             "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "achieved_basis": "GEMM FLOPs per step / union of the GEMM launch intervals per step, "
-                              "measured in a graph replay of the timed schedule (same sub-batch streams "
-                              "and kernels; device-clock launch timeline, median of 5 replays)",
+            "achieved_basis": ("GEMM FLOPs per step / union of the GEMM launch intervals per step, "
+                               "measured in a graph replay of the timed schedule (same sub-batch streams "
+                               "and kernels; device-clock launch timeline, median of 5 replays)") if union_ok
+                              else ("GEMM FLOPs per step / ms_per_step (the profiled replay's GEMM union "
+                                    "exceeded the timed step by > 2 %, so the lower bound is reported)"),
             "gemm_union_ms_per_step": round(union_ms_step, 3),
             "ms_per_step": round(ms_step, 3),
             "union_le_step": bool(union_ms_step <= ms_step),
