@@ -189,8 +189,7 @@ int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstri
                const float* stats, const float* ln_gamma, const float* ln_beta,
                const float* weight, const float* bias, void* Y, int64_t ldy, int y_grp,
                int64_t y_gstride, int y_off, int B, int H, int W, int C, int k, void* stream);
-/* Select the depthwise kernel: 4 = tier 3 with the tap-row A fragments moved between lanes by DPP
- * (two LDS reads per channel instead of k; bit-identical to 3), 3 (default) = MFMA Toeplitz form
+/* Select the depthwise kernel: 3 (default) = MFMA Toeplitz form
  * (bf16, C % 32 == 0, H, W <= 16, k in {3,5,7}), 2 = 64-channel x band blocks with an fp32 LDS tile
  * (C % 8 == 0, k in {3,5,7}, 16-B aligned rows), 1 = 32-channel blocks with a
  * bf16 tile (any shape); each falls back to the next where it does not apply.  Other values leave the selection unchanged.
@@ -211,12 +210,15 @@ int sdp_attention(int dtype, const void* QKV, int64_t ld_qkv, void* O, int64_t l
                   int n_head, int head_dim, const float* q_gamma, const float* q_beta,
                   const float* k_gamma, const float* k_beta, float eps, const float* mask,
                   int64_t mask_sb, int64_t mask_sh, void* stream);
-/* Kernel sdp_attention takes for this shape: 4 = two persistent 4-wave flash
- * workgroups per CU, one LDS-DMA K/V buffer each (hd % 32 == 0, N <= 256), 3 = two-workgroups-per-CU
- * flash kernel (hd % 32 == 0), 2 = one-workgroup flash kernel, 0 = generic. */
+/* Kernel sdp_attention takes for this shape: 6 = attn_fa5, one double-buffered 8-wave workgroup per
+ * CU (opt-in, hd % 32 == 0, N <= 224), 4 = two persistent 4-wave flash workgroups per CU, one LDS-DMA
+ * K/V buffer each (hd % 32 == 0, N <= 256), 3 = two-workgroups-per-CU whole-head flash kernel
+ * (hd % 32 == 0, head within 160 KiB of LDS), 5 = streaming flash kernel (hd % 32 == 0, any N),
+ * 2 = one-workgroup flash kernel, 0 = generic. */
 int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask);
-/* Select the bf16 flash kernel: 4 (default) = attn_fa4, 3 = attn_fa2, 2 = attn_fa
- * (each where it applies, else the next lower one).
+/* Select the bf16 flash kernel tier: 6 = allow attn_fa5, 4 (default) = attn_fa4, 3 = attn_fa2 (both
+ * falling back to the streaming attn_fs for heads that do not fit LDS), 5 = force attn_fs, 2 = attn_fa
+ * only (each where it applies, else the next lower one).
  * Other values leave the selection unchanged.  Returns the previous selection. */
 int sdp_attention_set_kernel(int k);
 /* Workgroups per CU of the persistent fa4 kernel (0 = as many as LDS and registers allow, at
