@@ -670,10 +670,13 @@ SDP_DEV void attn_qtile_pipe(const bf16_t* Ks, const bf16_t* Vs, const bf16x8 (&
 // tile, so the two waves of a SIMD overlap each other's phases.
 // The next Q tile (qnext) is loaded into qn after the last chunk's
 // exponentials, when the S^T registers are free: the loads overlap the P V^T phase.
-template <int HDT, int NKT, int CH, bool PF = true>
+// KT0 / KT1: the key tiles this call covers (default all NKT).  part != nullptr: instead of the
+// normalised O row, store the unnormalised partial of row r -- part[0] = running max (raw score),
+// part[1] = row sum, part[4 + d] = O numerator of head dim d -- for a later merge over key ranges.
+template <int HDT, int NKT, int CH, bool PF = true, int KT0 = 0, int KT1 = NKT>
 SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8 (&qf)[2 * HDT], int N,
                                 float scale_log2, int lane, bf16_t* orow, const bf16_t* qnext,
-                                bf16x8 (&qn)[2 * HDT]) {
+                                bf16x8 (&qn)[2 * HDT], float* part = nullptr) {
   constexpr int HD = 32 * HDT;
   const int r = lane & 31, hf = lane >> 5;
   f32x16 acc[HDT];  // first written by the first P V^T MFMA (zero C operand): not live before
@@ -686,10 +689,8 @@ SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8
   const char* kb0 = (const char*)(Ks + (size_t)r * HD) + 16 * ((hf) ^ kswz);
   const char* kb1 = (const char*)(Ks + (size_t)r * HD) + 16 * ((2 + hf) ^ kswz);
 #pragma unroll
-  for (int c0 = 0; c0 < NKT; c0 += CH) {
-    constexpr int dummy = 0;
-    (void)dummy;
-    const int n = NKT - c0 < CH ? NKT - c0 : CH;  // compile-time after unrolling
+  for (int c0 = KT0; c0 < KT1; c0 += CH) {
+    const int n = KT1 - c0 < CH ? KT1 - c0 : CH;  // compile-time after unrolling
     f32x16 st[CH];
 #pragma unroll
     for (int t = 0; t < CH; ++t)
@@ -713,7 +714,7 @@ SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8
 #pragma unroll
         for (int i = 0; i < 16; i += 2) mx = fmaxf(fmaxf(mx, st[t][i]), st[t][i + 1]);
     mx = xhalf_max(mx);
-    if (c0 > 0) {  // acc holds earlier chunks
+    if (c0 > KT0) {  // acc holds earlier chunks
       const float mn = fmaxf(m, mx);
       const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale_log2);
       l2 *= alpha;
@@ -746,7 +747,7 @@ SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8
         }
         asm volatile("" : "+v"(pb[t][0]), "+v"(pb[t][1]), "+v"(l2));  // one tile's exponentials at a time
       }
-    if (PF && c0 + n == NKT) {
+    if (PF && c0 + n == KT1) {
       asm volatile("" ::: "memory");
       attn_load_q<HDT>(qnext, hf, qn);
     }  // P complete before P V^T (bounds the live registers)
@@ -773,7 +774,7 @@ SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8
         for (int dt = 0; dt < HDT; ++dt) {
           asm volatile("" : "+v"(lo[dt]), "+v"(hi[dt]));
           const bf16x8 vf = {lo[dt][0], lo[dt][1], lo[dt][2], lo[dt][3], hi[dt][0], hi[dt][1], hi[dt][2], hi[dt][3]};
-          if (kt == 0 && s2 == 0) {
+          if (kt == KT0 && s2 == 0) {
             const f32x16 z = {};
             acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[t][s2], z, 0, 0, 0);
           } else {
@@ -784,6 +785,19 @@ SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8
     }
   }
   const float l = xhalf_sum(l2.x + l2.y);
+  if (part) {
+    if (hf == 0) {
+      part[0] = m;
+      part[1] = l;
+    }
+#pragma unroll
+    for (int dt = 0; dt < HDT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *(f32x4*)(part + 4 + dt * 32 + 8 * g + 4 * hf) =
+            f32x4{acc[dt][4 * g], acc[dt][4 * g + 1], acc[dt][4 * g + 2], acc[dt][4 * g + 3]};
+    return;
+  }
   const float inv = 1.0f / l;
   if (orow) {
 #pragma unroll
@@ -823,7 +837,7 @@ SDP_DEV void attn_qtile_chunked(const bf16_t* Ks, const bf16_t* Vs, const bf16x8
 #define ATTN_CH2 3  // at 168 VGPRs (three waves on a SIMD): 4 spills at hd 96
 #endif
 template <int HDT, int NKT = 0>
-__global__ __launch_bounds__(576) __attribute__((amdgpu_waves_per_eu(NKT > 0 ? 3 : (HDT <= 3 ? 4 : 2)))) void attn_fa2_bf16(
+__global__ __launch_bounds__(NKT > 0 ? 64 * (NKT + 2) : 576) __attribute__((amdgpu_waves_per_eu(NKT > 0 ? 3 : (HDT <= 3 ? 4 : 2)))) void attn_fa2_bf16(
     const bf16_t* __restrict__ QKV, int64_t ldq, bf16_t* __restrict__ O, int64_t ldo, int B, int N, int H,
     const float* __restrict__ gq, const float* __restrict__ bq, const float* __restrict__ gk,
     const float* __restrict__ bk, float eps, float scale_log2) {
@@ -892,17 +906,64 @@ __global__ __launch_bounds__(576) __attribute__((amdgpu_waves_per_eu(NKT > 0 ? 3
 
   const int r = lane & 31, hf = lane >> 5;
   const int nqt = NP32 / 32;
-  for (int qt = wave; qt < nqt; qt += nwaves) {
+  if constexpr (NKT > 0) {
+    // NKT + 2 waves: waves 0 .. NKT-2 one full query tile each; the last (partial) query tile's keys
+    // split in three chunk-aligned ranges over waves NKT-1 .. NKT+1, so each SIMD runs ~2.3 tiles of
+    // work instead of one SIMD running three; the three unnormalised partials meet in LDS.
+    static_assert(NKT == 9 && ATTN_CH2 == 3, "key-split last tile assumes 9 key tiles in 3 chunks");
+    constexpr int PP = HD + 4;  // partial row pitch (floats): m, l, pad, pad, O numerator
+    const int nlast = N - (NKT - 1) * 32;  // rows of the last query tile
+    float* part = (float*)(Vs + (size_t)NP16 * HD);  // [3][nlast][PP]
+    const int qt = wave < NKT - 1 ? wave : NKT - 1;
     const int q = qt * 32 + r;
     const bool qok = q < N;
     bf16x8 qf[2 * HDT];
     attn_load_q<HDT>(base + (int64_t)(qok ? q : N - 1) * ldq, hf, qf);
     if (gq) attn_norm_q<HDT>(qf, qok, hf, gq, bq, eps);
-    bf16_t* orow = qok ? O + ((int64_t)b * N + q) * ldo + hh * HD : nullptr;
-    if constexpr (NKT > 0)
+    if (wave < NKT - 1) {
+      bf16_t* orow = O + ((int64_t)b * N + q) * ldo + hh * HD;
       attn_qtile_chunked<HDT, NKT, ATTN_CH2, false>(Ks, Vs, qf, N, scale_log2, lane, orow, nullptr, qf);
-    else
+    } else {
+      const int sl = wave - (NKT - 1);
+      float* pr = qok ? part + ((size_t)sl * nlast + r) * PP : nullptr;
+      if (sl == 0)
+        attn_qtile_chunked<HDT, NKT, ATTN_CH2, false, 0, 3>(Ks, Vs, qf, N, scale_log2, lane, nullptr, nullptr, qf, pr);
+      else if (sl == 1)
+        attn_qtile_chunked<HDT, NKT, ATTN_CH2, false, 3, 6>(Ks, Vs, qf, N, scale_log2, lane, nullptr, nullptr, qf, pr);
+      else
+        attn_qtile_chunked<HDT, NKT, ATTN_CH2, false, 6, 9>(Ks, Vs, qf, N, scale_log2, lane, nullptr, nullptr, qf, pr);
+    }
+    __syncthreads();
+    if (wave == NKT - 1) {  // merge: O = sum_i 2^((m_i - M) s) acc_i / sum_i 2^((m_i - M) s) l_i
+      constexpr int D4 = HD / 4;
+      for (int i = lane; i < nlast * D4; i += 64) {
+        const int row = i / D4, d4 = i - row * D4;
+        const float* p0 = part + (size_t)row * PP;
+        const float* p1 = p0 + (size_t)nlast * PP;
+        const float* p2 = p1 + (size_t)nlast * PP;
+        const float mx = fmaxf(fmaxf(p0[0], p1[0]), p2[0]);
+        const float w0 = __builtin_amdgcn_exp2f((p0[0] - mx) * scale_log2);
+        const float w1 = __builtin_amdgcn_exp2f((p1[0] - mx) * scale_log2);
+        const float w2 = __builtin_amdgcn_exp2f((p2[0] - mx) * scale_log2);
+        const float inv = 1.0f / (w0 * p0[1] + w1 * p1[1] + w2 * p2[1]);
+        const f32x4 a0 = *(const f32x4*)(p0 + 4 + 4 * d4), a1 = *(const f32x4*)(p1 + 4 + 4 * d4),
+                    a2 = *(const f32x4*)(p2 + 4 + 4 * d4);
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (short)f2bf((w0 * a0[e] + w1 * a1[e] + w2 * a2[e]) * inv);
+        *(bf16x4*)(O + ((int64_t)b * N + (NKT - 1) * 32 + row) * ldo + hh * HD + 4 * d4) = o;
+      }
+    }
+  } else {
+    for (int qt = wave; qt < nqt; qt += nwaves) {
+      const int q = qt * 32 + r;
+      const bool qok = q < N;
+      bf16x8 qf[2 * HDT];
+      attn_load_q<HDT>(base + (int64_t)(qok ? q : N - 1) * ldq, hf, qf);
+      if (gq) attn_norm_q<HDT>(qf, qok, hf, gq, bq, eps);
+      bf16_t* orow = qok ? O + ((int64_t)b * N + q) * ldo + hh * HD : nullptr;
       attn_qtile<HDT>(Ks, Vs, qf, N, nqt, scale_log2, lane, orow);
+    }
   }
 }
 
@@ -912,14 +973,19 @@ template <int HDT>
 static int launch_attn_fa2(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H,
                            const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
                            hipStream_t s) {
-  const size_t bytes = attn_fa2_bytes(N, 32 * HDT);
+  size_t bytes = attn_fa2_bytes(N, 32 * HDT);
   // one query tile per wave up to 9 tiles (N <= 288: XL's 260 tokens are 8 full tiles + 4 rows;
   // with 8 waves one wave did two tiles and set the block's time), else 8 waves looping; at exactly
   // 9 key tiles (XL) the chunked single-max softmax (hd <= 96: hd 128 would spill at 168 VGPRs)
+  // with the last query tile's keys split over three more waves (11 in all)
   int waves = (N + 31) / 32;
   if (waves > 9) waves = 8;
-  const void* fn = waves == 9 && HDT <= 3 ? (const void*)attn_fa2_bf16<HDT, HDT <= 3 ? 9 : 0>
-                                          : (const void*)attn_fa2_bf16<HDT, 0>;
+  const bool split = waves == 9 && HDT <= 3;
+  const void* fn = split ? (const void*)attn_fa2_bf16<HDT, HDT <= 3 ? 9 : 0> : (const void*)attn_fa2_bf16<HDT, 0>;
+  if (split) {
+    waves = 11;
+    bytes += (size_t)3 * (N - 256) * (32 * HDT + 4) * 4;
+  }
   if (bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;
