@@ -212,8 +212,9 @@ int sdp_attention(int dtype, const void* QKV, int64_t ld_qkv, void* O, int64_t l
                   int64_t mask_sb, int64_t mask_sh, void* stream);
 /* Kernel sdp_attention takes for this shape: 6 = attn_fa5, one double-buffered 8-wave workgroup per
  * CU (opt-in, hd % 32 == 0, N <= 224), 4 = two persistent 4-wave flash workgroups per CU, one LDS-DMA
- * K/V buffer each (hd % 32 == 0, N <= 256), 3 = two-workgroups-per-CU whole-head flash kernel
- * (hd % 32 == 0, head within 160 KiB of LDS), 5 = streaming flash kernel (hd % 32 == 0, any N),
+ * K/V buffer each (hd % 32 == 0, N <= 256), 3 = whole-head flash kernels (hd % 32 == 0, head within
+ * 160 KiB of LDS; at 9 key tiles the persistent attn_fa6 with three rotating K / V images where they
+ * fit, else attn_fa2), 5 = streaming flash kernel (hd % 32 == 0, any N),
  * 2 = one-workgroup flash kernel, 0 = generic. */
 int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask);
 /* Select the bf16 flash kernel tier: 6 = allow attn_fa5, 4 (default) = attn_fa4, 3 = attn_fa2 (both

@@ -324,21 +324,25 @@ struct AttnKV {
       vo[r] = (uint32_t)(((int64_t)row * ldq + 2 * C + 8 * pc) * 2);
     }
   }
-  // base: row 0 / column hh * HD of the pair; bytes: extent of the image's QKV rows from base
+  // base: row 0 / column hh * HD of the pair; bytes: extent of the image's QKV rows from base.
+  // DK / DV: stage K / V (attn_fa6 stages them at different times).
+  template <bool DK = true, bool DV = true>
   SDP_DEV void issue(const bf16_t* base, uint64_t bytes, char* Ks, char* Vs, int NP16, int64_t ldq, int wave,
                      int nwaves) const {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)base, 0, (int)(bytes < 0xffffffffull ? bytes : 0xffffffffull), 0x00020000);
     const int U = NP16 >> 4, w0 = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform unit index
     const uint32_t ustep = (uint32_t)(16 * ldq * 2);
-    for (int u = w0; u < U; u += nwaves)
+    if constexpr (DK)
+      for (int u = w0; u < U; u += nwaves)
 #pragma unroll
-      for (int r = 0; r < HDT; ++r)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (AS3 void*)(Ks + (u * HDT + r) * 1024), 16, (int)ko[r], (int)(u * ustep), 0, 0);
-    for (int u = w0; u < U; u += nwaves)
+        for (int r = 0; r < HDT; ++r)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (AS3 void*)(Ks + (u * HDT + r) * 1024), 16, (int)ko[r], (int)(u * ustep), 0, 0);
+    if constexpr (DV)
+      for (int u = w0; u < U; u += nwaves)
 #pragma unroll
-      for (int r = 0; r < HDT; ++r)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (AS3 void*)(Vs + (u * HDT + r) * 1024), 16, (int)vo[r], (int)(u * ustep), 0, 0);
+        for (int r = 0; r < HDT; ++r)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (AS3 void*)(Vs + (u * HDT + r) * 1024), 16, (int)vo[r], (int)(u * ustep), 0, 0);
   }
 };
 // ---------------------------------------------------------------------------
@@ -969,6 +973,12 @@ __global__ __launch_bounds__(NKT > 0 ? 64 * (NKT + 2) : 576) __attribute__((amdg
 
 static size_t attn_fa2_bytes(int N, int hd) { return (size_t)2 * ((N + 15) / 16 * 16) * hd * 2; }
 
+static size_t attn_fa6_bytes(int N, int hd);
+template <int HDT>
+static int launch_attn_fa6(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H,
+                           const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
+                           hipStream_t s);
+
 template <int HDT>
 static int launch_attn_fa2(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H,
                            const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
@@ -982,6 +992,9 @@ static int launch_attn_fa2(const void* QKV, int64_t ldq, void* O, int64_t ldo, i
   if (waves > 9) waves = 8;
   const bool split = waves == 9 && HDT <= 3;
   const void* fn = split ? (const void*)attn_fa2_bf16<HDT, HDT <= 3 ? 9 : 0> : (const void*)attn_fa2_bf16<HDT, 0>;
+  if constexpr (HDT <= 3)
+    if (split && attn_fa6_bytes(N, 32 * HDT) <= 160 * 1024)  // persistent form, K / V staging hidden
+      return launch_attn_fa6<HDT>(QKV, ldq, O, ldo, B, N, H, gq, bq, gk, bk, eps, scale, s);
   if (split) {
     waves = 11;
     bytes += (size_t)3 * (N - 256) * (32 * HDT + 4) * 4;
@@ -1250,6 +1263,201 @@ __global__ __launch_bounds__(512) void attn_fa5_bf16(const bf16_t* __restrict__ 
     }
     SDP_ASTAMP5(j, 4);
   }
+}
+
+// ---------------------------------------------------------------------------
+// attn_fa6_bf16 — the XL shape (256 < N <= 288, 9 key tiles, hd <= 96): one persistent 12-wave
+// workgroup per CU.  A whole head does not fit twice in LDS (N = 260, hd = 96: K or V 52,224 B),
+// but three K / V images do, so the head is staged in two halves that each hide behind a phase:
+//   phase 1: waves 0..8 k-normalise K_j (32 rows each) while V_j lands (DMA issued at the end of
+//            pair j-1), waves 9..10 merge pair j-1's last-tile partials, every compute wave loads
+//            its Q fragments;
+//   phase 2: waves 0..7 compute query tiles 0..7 and waves 8..10 the last (partial) tile over key
+//            tiles 0-2 / 3-5 / 6-8 (attn_fa2's split), while the producer (wave 11) stages K_{j+1}
+//            into the spare image.
+// The three images rotate (K_j's image takes V_{j+1}, V_j's becomes the spare): two barriers per
+// pair, no staging or launch on the critical path except V's DMA behind the k-norm.
+// LDS: 3 x NP16 x HD x 2 B + gamma / beta + 3 x nlast x (HD + 4) x 4 B (N = 260, hd = 96: 163,008 B).
+// ---------------------------------------------------------------------------
+template <int HDT>
+__global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(3))) void attn_fa6_bf16(
+    const bf16_t* __restrict__ QKV, int64_t ldq, bf16_t* __restrict__ O, int64_t ldo, int B, int N, int H,
+    const float* __restrict__ gq, const float* __restrict__ bq, const float* __restrict__ gk,
+    const float* __restrict__ bk, float eps, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  constexpr int NKT = 9, HD = 32 * HDT, PP = HD + 4, D4 = HD / 4;
+  static_assert(ATTN_CH2 == 3, "the last tile's key ranges are whole chunks of 3 key tiles");
+  const int NP16 = (N + 15) / 16 * 16;
+  const size_t kvb = (size_t)NP16 * HD * sizeof(bf16_t);  // bytes of one K (or V) image
+  float* const prm = (float*)(sm + 3 * kvb);              // gq | bq | gk | bk
+  float* const part = prm + 4 * HD;                       // [3][nlast][PP]
+  const int nlast = N - (NKT - 1) * 32;
+  // wave index made scalar: the producer / compute / merge branches are then uniform to the
+  // compiler, and nothing staged under them needs a waterfall loop
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int npairs = B * H, G = gridDim.x, x = blockIdx.x;
+  const int nj = (npairs - x + G - 1) / G;
+  if (nj <= 0) return;
+  const int C = H * HD;
+  const bool norm = gq != nullptr;
+  if (norm) {
+    for (int i = tid; i < 4 * HD; i += 768) {
+      const int k = i / HD, d = i - k * HD;
+      prm[i] = (k == 0 ? gq : k == 1 ? bq : k == 2 ? gk : bk)[d];
+    }
+  }
+  auto pair_of = [&](int j) {  // XCD-contiguous pair order, as attn_fa4
+    const int v = x + j * G;
+    const int xcd = v & 7, qd = npairs >> 3, rem = npairs & 7;
+    return (xcd < rem ? xcd * (qd + 1) : rem * (qd + 1) + (xcd - rem) * qd) + (v >> 3);
+  };
+  auto qkv_base = [&](int pair) {
+    const int b = pair / H, hh = pair - (pair / H) * H;
+    return QKV + (int64_t)b * N * ldq + hh * HD;
+  };
+  auto img = [&](int i) { return (bf16_t*)(sm + (size_t)i * kvb); };
+  const bool producer = wave == NKT + 2;
+  // (the DMA offsets are rebuilt per stage: kept live they cost the compute waves registers)
+  auto stage_k = [&](int pair_, int i_) {
+    // pair / image are wave-uniform; say so, or the DMA's resource and M0 get waterfall loops
+    const int pair = __builtin_amdgcn_readfirstlane(pair_), i = __builtin_amdgcn_readfirstlane(i_);
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const AttnKV<HDT> kv(ln, ldq, C);
+    const int hh = pair - (pair / H) * H;
+    kv.template issue<true, false>(qkv_base(pair), (uint64_t)((int64_t)(N - 1) * ldq + 3 * C - hh * HD) * 2,
+                                   (char*)img(i), nullptr, NP16, ldq, 0, 1);
+  };
+  auto stage_v = [&](int pair_, int i_) {
+    // pair / image are wave-uniform; say so, or the DMA's resource and M0 get waterfall loops
+    const int pair = __builtin_amdgcn_readfirstlane(pair_), i = __builtin_amdgcn_readfirstlane(i_);
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const AttnKV<HDT> kv(ln, ldq, C);
+    const int hh = pair - (pair / H) * H;
+    kv.template issue<false, true>(qkv_base(pair), (uint64_t)((int64_t)(N - 1) * ldq + 3 * C - hh * HD) * 2,
+                                   nullptr, (char*)img(i), NP16, ldq, 0, 1);
+  };
+  // barrier without the vmcnt(0) of __syncthreads (as attn_fa5: the producer waits for its DMA)
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // last tile of `pair` from the three partials: O = sum 2^((m_i - M) s) acc_i / sum 2^((m_i - M) s) l_i;
+  // waves 9 and 10 share the nlast x HD outputs
+  auto merge = [&](int pair) {
+    const int b = pair / H, hh = pair - (pair / H) * H;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    for (int i = ln + 64 * (wave - NKT); i < nlast * D4; i += 128) {
+      const int row = i / D4, d4 = i - row * D4;
+      const float* p0 = part + (size_t)row * PP;
+      const float* p1 = p0 + (size_t)nlast * PP;
+      const float* p2 = p1 + (size_t)nlast * PP;
+      const float mx = fmaxf(fmaxf(p0[0], p1[0]), p2[0]);
+      const float w0 = __builtin_amdgcn_exp2f((p0[0] - mx) * scale_log2);
+      const float w1 = __builtin_amdgcn_exp2f((p1[0] - mx) * scale_log2);
+      const float w2 = __builtin_amdgcn_exp2f((p2[0] - mx) * scale_log2);
+      const float inv = 1.0f / (w0 * p0[1] + w1 * p1[1] + w2 * p2[1]);
+      const f32x4 a0 = *(const f32x4*)(p0 + 4 + 4 * d4), a1 = *(const f32x4*)(p1 + 4 + 4 * d4),
+                  a2 = *(const f32x4*)(p2 + 4 + 4 * d4);
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (short)f2bf((w0 * a0[e] + w1 * a1[e] + w2 * a2[e]) * inv);
+      *(bf16x4*)(O + ((int64_t)b * N + (NKT - 1) * 32 + row) * ldo + hh * HD + 4 * d4) = o;
+    }
+  };
+  const int r = lane & 31;
+  const int qt = wave < NKT - 1 ? wave : NKT - 1;  // waves 8..10: the last tile
+  const int q0 = qt * 32 + r;
+  const bool ok0 = q0 < N;
+  const int64_t off0 = (int64_t)(ok0 ? q0 : N - 1) * ldq;
+  bf16x8 qa[2 * HDT];
+  int ik = 0, iv = 1, is = 2;  // images holding K_j, V_j and the spare
+  int pair = pair_of(0), prev = pair;
+  if (producer) {
+    stage_k(pair, ik);
+    stage_v(pair, iv);
+  }
+  for (int j = 0; j < nj; ++j) {
+    const int nxt = j + 1 < nj ? pair_of(j + 1) : pair;
+    if (producer) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V_j (and at j = 0, K_0) landed
+      if (j == 0) barrier();                             // K_0 and gamma / beta visible
+    } else {
+      if (j == 0) barrier();
+      if (j > 0 && wave >= NKT) merge(prev);
+      if (norm && 32 * wave < NP16) attn_knorm32<HDT>(img(ik), 32 * wave, NP16, lane, prm + 2 * HD, prm + 3 * HD, eps);
+    }
+    barrier();  // K_j normalised, V_j landed, pair j-1's partials consumed
+    if (producer) {
+      if (j + 1 < nj) {
+        stage_k(nxt, is);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else {
+      // lane-derived values re-made opaque each pair: hoisted out of the loop they stay live
+      // through the compute (masks, LDS lane offsets) and push it past 168 VGPRs
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int b = pair / H, hh = pair - (pair / H) * H;
+      attn_load_q<HDT>(qkv_base(pair) + off0, ln >> 5, qa);
+      if (norm) attn_norm_q<HDT>(qa, ok0, ln >> 5, prm, prm + HD, eps);
+      if (wave < NKT - 1) {
+        bf16_t* orow = O + ((int64_t)b * N + q0) * ldo + hh * HD;
+        attn_qtile_chunked<HDT, NKT, ATTN_CH2, false>(img(ik), img(iv), qa, N, scale_log2, ln, orow, nullptr, qa);
+      } else {
+        const int sl = wave - (NKT - 1);
+        float* pr = ok0 ? part + ((size_t)sl * nlast + (ln & 31)) * PP : nullptr;
+        if (sl == 0)
+          attn_qtile_chunked<HDT, NKT, ATTN_CH2, false, 0, 3>(img(ik), img(iv), qa, N, scale_log2, ln, nullptr, nullptr, qa, pr);
+        else if (sl == 1)
+          attn_qtile_chunked<HDT, NKT, ATTN_CH2, false, 3, 6>(img(ik), img(iv), qa, N, scale_log2, ln, nullptr, nullptr, qa, pr);
+        else
+          attn_qtile_chunked<HDT, NKT, ATTN_CH2, false, 6, 9>(img(ik), img(iv), qa, N, scale_log2, ln, nullptr, nullptr, qa, pr);
+      }
+    }
+    barrier();  // K_j / V_j images free, K_{j+1} landed, pair j's partials written
+    if (producer && j + 1 < nj) stage_v(nxt, ik);
+    const int t = ik;
+    ik = is;
+    is = iv;
+    iv = t;
+    prev = pair;
+    pair = nxt;
+  }
+  if (!producer && wave >= NKT) merge(prev);
+}
+
+static size_t attn_fa6_bytes(int N, int hd) {
+  const size_t np16 = (size_t)(N + 15) / 16 * 16;
+  return 3 * np16 * hd * 2 + (size_t)16 * hd + (size_t)3 * (N > 256 ? N - 256 : 0) * (hd + 4) * 4;
+}
+
+template <int HDT>
+static int launch_attn_fa6(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H,
+                           const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
+                           hipStream_t s) {
+  if (N <= 256 || N > 288) return (int)hipErrorInvalidValue;  // 9 key tiles only
+  const size_t bytes = attn_fa6_bytes(N, 32 * HDT);
+  const void* fn = (const void*)attn_fa6_bf16<HDT>;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) return (int)e;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  int grid = ncu / 8 * 8;  // one workgroup per CU (LDS)
+  if (grid < 8) grid = 8;
+  if (grid > B * H) grid = B * H;
+  const float sl = scale * 1.4426950408889634f;
+  const bf16_t* q = (const bf16_t*)QKV;
+  bf16_t* o = (bf16_t*)O;
+  void* args[] = {(void*)&q, (void*)&ldq, (void*)&o, (void*)&ldo, (void*)&B, (void*)&N, (void*)&H, (void*)&gq,
+                  (void*)&bq, (void*)&gk, (void*)&bk, (void*)&eps, (void*)&sl};
+  e = hipLaunchKernel(fn, dim3(grid), dim3(768), args, bytes, s);
+  if (e != hipSuccess) return (int)e;
+  return SDP_CHECK_LAUNCH();
 }
 
 // ---------------------------------------------------------------------------
@@ -1548,7 +1756,8 @@ static size_t attn_fa_bytes(int N, int hd) {
 //   6 attn_fa5_bf16: N <= 224, K / V double-buffered within 160 KiB (M: 91-102 vs fa4's 103-109 us
 //     alone, but the M forward 0.25 % slower than with fa4 over 8 interleaved runs -- opt-in);
 //   4 (default) attn_fa4_bf16: N <= 256, two workgroups per CU;
-//   3 attn_fa2_bf16: the whole head staged (XL, N = 260);
+//   3 attn_fa2_bf16: the whole head staged; at 9 key tiles (XL, N = 260) attn_fa6_bf16, persistent
+//     with three rotating K / V images, where those fit 160 KiB;
 //   then attn_fs_bf16 (5), the streaming kernel, for any longer N (hd % 32 == 0), and attn_fa_bf16
 //   (2) for hd % 32 != 0.  Setting 5 forces attn_fs_bf16; 2 allows only attn_fa_bf16.
 static int g_attn_kernel = 4;

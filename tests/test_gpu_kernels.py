@@ -263,7 +263,7 @@ def test_attention(dtype, B, N, H, hd, kern):
 
 def test_attention_mfma_path_is_taken_for_canonical_shapes():
     assert sp.attention_variant(BF, 200, 8, 96) == 4   # two persistent workgroups per CU
-    assert sp.attention_variant(BF, 260, 8, 96) == 3   # N > 256 -> two-workgroups-per-CU single-pass kernel
+    assert sp.attention_variant(BF, 260, 8, 96) == 3   # N > 256 -> whole-head kernels (attn_fa6 at XL)
     assert sp.attention_variant(BF, 200, 8, 16) == 2   # hd % 32 != 0 -> one-workgroup kernel
 
 
@@ -289,6 +289,23 @@ def test_attention_fused_qk_norm(dtype, B, N, H, hd, kern):
     finally:
         sp.lib().sdp_attention_set_kernel(old)
     close(o, ref, dtype, rel=2e-5 if dtype == torch.float32 else 2e-2, what=f"fused qk-norm attn variant {v}")
+
+
+@pytest.mark.parametrize("B,N,H,hd", [(100, 260, 8, 96), (70, 280, 12, 64), (40, 257, 8, 32), (3, 270, 8, 96)])
+def test_attention_xl_persistent(B, N, H, hd):
+    # 9 key tiles: attn_fa6 (persistent, three rotating K / V images) when its LDS fits, else the
+    # 11-wave attn_fa2; B * H > 3 x 256 so every workgroup cycles through all three images
+    C = H * hd
+    qkv = rnd(B * N, 3 * C, dtype=BF, seed=50, scale=2.0)
+    gq, bq, gk, bk = (rnd(hd, seed=s) * 0.1 + (1 if s % 2 == 0 else 0) for s in (51, 52, 53, 54))
+    ref_in = qkv.float().clone()
+    ref_in[:, :C] = F.layer_norm(ref_in[:, :C].view(-1, H, hd), (hd,), gq, bq).view(-1, C)
+    ref_in[:, C:2 * C] = F.layer_norm(ref_in[:, C:2 * C].view(-1, H, hd), (hd,), gk, bk).view(-1, C)
+    ref = attn_ref(ref_in.to(BF), B, N, H, hd)
+    o = torch.full((B * N, C), float("nan"), dtype=BF, device=DEV)
+    assert sp.attention_variant(BF, N, H, hd) == 3
+    sp.attention(qkv, o, B, N, H, hd, qk_norm=(gq, bq, gk, bk), eps=1e-5)
+    close(o, ref, BF, rel=2e-2, what=f"XL-shape attention B={B} N={N} hd={hd}")
 
 
 @pytest.mark.parametrize("N", [200, 260, 77])
