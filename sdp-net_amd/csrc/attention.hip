@@ -1071,9 +1071,16 @@ __device__ unsigned long long g_attn_stamps[1024 * 2 * 8 * 5];
     if ((wave == 0 || wave == 7) && lane == 0 && (j) < 8 && blockIdx.x < 1024)                         \
       g_attn_stamps[(((int64_t)blockIdx.x * 2 + (wave == 7)) * 8 + (j)) * 5 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// attn_fa6: waves 0 (a compute wave) and 11 (the producer)
+#define SDP_ASTAMP6(j, k)                                                                              \
+  do {                                                                                                 \
+    if ((wave == 0 || wave == 11) && lane == 0 && (j) < 8 && blockIdx.x < 1024)                        \
+      g_attn_stamps[(((int64_t)blockIdx.x * 2 + (wave == 11)) * 8 + (j)) * 5 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
 #define SDP_ASTAMP(j, k) do {} while (0)
 #define SDP_ASTAMP5(j, k) do {} while (0)
+#define SDP_ASTAMP6(j, k) do {} while (0)
 #endif
 template <int HDT, int NKT>
 __global__ __launch_bounds__(256, 2) void attn_fa4_bf16(const bf16_t* __restrict__ QKV, int64_t ldq,
@@ -1382,20 +1389,25 @@ __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(3))) void a
   }
   for (int j = 0; j < nj; ++j) {
     const int nxt = j + 1 < nj ? pair_of(j + 1) : pair;
+    SDP_ASTAMP6(j, 0);
     if (producer) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V_j (and at j = 0, K_0) landed
+      SDP_ASTAMP6(j, 1);
       if (j == 0) barrier();                             // K_0 and gamma / beta visible
     } else {
       if (j == 0) barrier();
       if (j > 0 && wave >= NKT) merge(prev);
       if (norm && 32 * wave < NP16) attn_knorm32<HDT>(img(ik), 32 * wave, NP16, lane, prm + 2 * HD, prm + 3 * HD, eps);
+      SDP_ASTAMP6(j, 1);
     }
     barrier();  // K_j normalised, V_j landed, pair j-1's partials consumed
+    SDP_ASTAMP6(j, 2);
     if (producer) {
       if (j + 1 < nj) {
         stage_k(nxt, is);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      SDP_ASTAMP6(j, 3);
     } else {
       // lane-derived values re-made opaque each pair: hoisted out of the loop they stay live
       // through the compute (masks, LDS lane offsets) and push it past 168 VGPRs
@@ -1418,7 +1430,9 @@ __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(3))) void a
           attn_qtile_chunked<HDT, NKT, ATTN_CH2, false, 6, 9>(img(ik), img(iv), qa, N, scale_log2, ln, nullptr, nullptr, qa, pr);
       }
     }
+    if (!producer) SDP_ASTAMP6(j, 3);
     barrier();  // K_j / V_j images free, K_{j+1} landed, pair j's partials written
+    SDP_ASTAMP6(j, 4);
     if (producer && j + 1 < nj) stage_v(nxt, ik);
     const int t = ik;
     ik = is;

@@ -1,4 +1,4 @@
-"""Per-pair phase timeline of attn_fa4 from the stamped diagnostic library.
+"""Per-pair phase timeline of attn_fa4 / attn_fa5 / attn_fa6 (--shape xl) from the stamped diagnostic library.
 
   make -C sdp-net_amd/csrc stamps
   SDPNET_HIP_LIB=sdp-net_amd/lib_stamps/libsdpnet_hip.so python tools/attn_stamps.py [--shape m|xl]
@@ -23,11 +23,12 @@ import sdpnet_hip as sp  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--shape", default="m", choices=["m"])
-    ap.add_argument("--kernel", type=int, default=4, help="attention kernel tier (4: fa4, 6 / 7: fa5)")
+    ap.add_argument("--shape", default="m", choices=["m", "xl"], help="m: bs 256, N 200; xl: bs 512, N 260")
+    ap.add_argument("--kernel", type=int, default=4,
+                    help="attention kernel tier (4: fa4, 6: fa5; 3 at --shape xl: fa6)")
     args = ap.parse_args()
     sp.lib().sdp_attention_set_kernel(args.kernel)
-    B, N, H, hd = 256, 200, 8, 96
+    B, N, H, hd = (256, 200, 8, 96) if args.shape == "m" else (512, 260, 8, 96)
     C = H * hd
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -44,7 +45,7 @@ def main():
         run()
     e1.record()
     torch.cuda.synchronize()
-    print(f"attention M shape: {1e3 * e0.elapsed_time(e1) / 20:.1f} us per launch (events), variant "
+    print(f"attention {args.shape} shape: {1e3 * e0.elapsed_time(e1) / 20:.1f} us per launch (events), variant "
           f"{sp.attention_variant(torch.bfloat16, N, H, hd)}")
     L = sp.lib()
     buf = np.zeros(1024 * 2 * 8 * 5, dtype=np.uint64)
@@ -52,11 +53,18 @@ def main():
     run()
     assert L.sdp_attn_stamps(buf.ctypes.data, buf.nbytes) == 0
     st = buf.reshape(1024, 2, 8, 5).astype(np.int64)
-    if args.kernel >= 6:  # attn_fa5: compute / produce, reach barrier 1, k-norm, barrier 2
+    if args.shape == "xl":  # attn_fa6: wave 0 / producer phases of one pair
+        names = None
+        waves = ["wave 0", "wave 11 (producer)"]
+        wnames = [["k-norm", "barrier 2", "q + compute", "barrier 1"],
+                  ["wait V", "barrier 2", "stage K+1", "barrier 1"]]
+    elif args.kernel >= 6:  # attn_fa5: compute / produce, reach barrier 1, k-norm, barrier 2
         names, waves = ["work", "barrier 1", "k-norm", "barrier 2"], ["wave 0", "wave 7 (producer)"]
     else:
         names, waves = ["stage+wait", "k-norm", "slot 0", "slot 1"], ["wave 0", "wave 3"]
     for w, wn in enumerate(waves):
+        if args.shape == "xl":
+            names = wnames[w]
         print(f"  {wn}: mean cycles per phase by pair index (workgroups with that pair)")
         for j in range(8):
             ok = (st[:, w, j, :] != 0).all(axis=1)
