@@ -100,8 +100,29 @@ def measured_traffic(kernel, config="m"):
         except (OSError, ValueError):
             continue
         if d.get("kernel") == kernel and d.get("config", "m") == config:
-            return int(d["hbm_bytes_per_launch"]), os.path.relpath(f, REPO)
-    return None, None
+            return int(d["hbm_bytes_per_launch"]), os.path.relpath(f, REPO), traffic_staleness(d)
+    return None, None, None
+
+
+def gemm_source_sha16():
+    """Hash of the sources the fast GEMM is built from (its kernel file and the shared header)."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in ("sdp-net_amd/csrc/gemm.hip", "sdp-net_amd/csrc/common.h"):
+        with open(os.path.join(REPO, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def traffic_staleness(d):
+    """Ties a committed PMC traffic summary to the build it describes (VERDICT r05 'what's weak' 7):
+    the summary records the GEMM source hash and the library md5 it was measured with.  True when
+    the GEMM source differs from the one built here, False when it matches, None for a summary
+    that predates the record (unknown)."""
+    src = d.get("gemm_src_sha16")
+    if not src:
+        return None
+    return src != gemm_source_sha16()
 
 
 XXS_CFG = dict(M_CFG, embedding_dim=128, num_blocks=7)   # BASELINE.json configs[0] (SURVEY.md §0)
@@ -489,7 +510,7 @@ def gemm_roofline(step, dev, ms_step, config, prof_steps=1):
     achieved = fast_fl / ((union_ms_step if union_ok else ms_step) * 1e-3) / 1e12
     per_launch_tf = fast_fl / (fast_ms * 1e-3) / 1e12 if fast_ms else 0.0
     kname = FAST_GEMM_NAMES.get(sp.lib().sdp_gemm_set_fast_kernel(0), "?")
-    traffic, traffic_src = measured_traffic(kname, config) if config in ("m", "xl") else (None, None)
+    traffic, traffic_src, stale = measured_traffic(kname, config) if config in ("m", "xl") else (None, None, None)
     return {"bound": "mfma", "kernel": kname,
             "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "achieved_basis": ("GEMM FLOPs per step / union of the GEMM launch intervals per step, "
@@ -507,6 +528,7 @@ def gemm_roofline(step, dev, ms_step, config, prof_steps=1):
             "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
             "traffic_unit": "bytes per launch, L2-to-fabric (PMC 2*FETCH_SIZE+WRITE_SIZE; Infinity Cache hits "
                             "included)", "traffic_source": traffic_src,
+            "traffic_stale": stale,
             "algorithmic_bytes_per_launch": int(fast_by / max(1, fast_n)),
             "launches_per_step": fast_n,
             "avg_launch_us": round(1e3 * fast_ms / max(1, fast_n), 2),
@@ -587,9 +609,9 @@ def main():
         ks = max(1, min(args.secondary_steps, args.steps))
         torch.cuda.empty_cache()
         xl, xl_sd = forward_bench(CONFIGS["xl"], CONFIGS["xl"]["batch"], ks, min(args.warmup, 3), dev, 1, rank,
-                                  graph=not args.no_graph, roofline=False, config="xl")
+                                  graph=not args.no_graph, roofline=True, config="xl")
         sec["xl_fwd"] = {k: xl[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "model_mfma_frac",
-                                           "model_flops_per_image_gf")}
+                                           "model_flops_per_image_gf", "roofline")}
         sec["xl_fwd"]["per_gpu_batch"] = CONFIGS["xl"]["batch"]
         if xl_sd is not None:
             cpu_sds["SdP-Net-XL"] = (xl_sd, XL_CFG)

@@ -87,25 +87,28 @@ int sdp_gemm_force_generic(int on);
 /* Select the bf16 fast kernel: 14 = 8-phase ping-pong 256x256x64 with the
  * whole-line (LDS-staged) epilogue, all row groups staged before the first store
  * (default); 9 = same main loop, permlane-paired 16-B register epilogue (also the
- * automatic fallback for unaligned rows and resid_pre with an activation).  Any other
- * value leaves the selection unchanged.  Returns the previous selection. */
+ * automatic fallback for unaligned rows and resid_pre with an activation).  0 queries;
+ * any other value returns -1 and leaves the selection unchanged.  Returns the previous selection. */
 int sdp_gemm_set_fast_kernel(int k);
 
 /* Output store policy of the whole-line GEMM epilogue: 1 = non-temporal (streaming)
- * stores, 0 = default.  Returns the previous value. */
+ * stores, 0 = default.  Returns the previous value.  The product library offers only 0 (a
+ * request for 1 returns -1); the diagnostic build (make stamps) keeps the A/B arm. */
 int sdp_gemm_set_store_policy(int nt);
 
 /* Epilogue specialisation of the whole-line fast-GEMM epilogue: 1 (default) = the model's
  * flag combinations (plain; bias; LN fold + bias; residual + LN partials [+ bias]) with no / GELU
  * activation run an instantiation with the flags fixed at compile time (packed residual add,
  * dot2 partial sums); 0 = the run-time-flag epilogue for every call.  Outputs are
- * bit-identical; the emitted LN partials agree to fp32 rounding.  Returns the previous value. */
+ * bit-identical; the emitted LN partials agree to fp32 rounding.  Returns the previous value.
+ * The product library offers only 1 (a request for 0 returns -1; diagnostic build: both). */
 int sdp_gemm_set_epi_spec(int on);
 
 /* Phases per K-tile of the fast GEMM's data-parallel main loop: 2 (default, 32 MFMAs per
- * wave-group section, half the group-to-group hand-overs) or 4 (16 MFMAs per section).  Same
- * arithmetic order, bit-identical outputs.  Also selects the weight-gradient kernel's loop
- * (sdp_gemm_wgrad).  Returns the previous value; any other n only queries it. */
+ * wave-group section, half the group-to-group hand-overs) or 4 (16 MFMAs per section; diagnostic
+ * build only).  Same arithmetic order, bit-identical outputs.  Also selects the weight-gradient
+ * kernel's loop (sdp_gemm_wgrad).  Returns the previous value; 0 queries it; a value the loaded
+ * library does not offer returns -1. */
 int sdp_gemm_set_kloop_phases(int n);
 
 /* Launch timeline of the bf16 fast GEMM (measurement only; bench.py's roofline inside a replayed
@@ -192,8 +195,8 @@ int sdp_dwconv(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstri
 /* Select the depthwise kernel: 3 (default) = MFMA Toeplitz form
  * (bf16, C % 32 == 0, H, W <= 16, k in {3,5,7}), 2 = 64-channel x band blocks with an fp32 LDS tile
  * (C % 8 == 0, k in {3,5,7}, 16-B aligned rows), 1 = 32-channel blocks with a
- * bf16 tile (any shape); each falls back to the next where it does not apply.  Other values leave the selection unchanged.
- * Returns the previous selection. */
+ * bf16 tile (any shape); each falls back to the next where it does not apply.  0 queries; any other
+ * value returns -1 and leaves the selection unchanged.  Returns the previous selection. */
 int sdp_dwconv_set_kernel(int k);
 
 /*
@@ -211,16 +214,17 @@ int sdp_attention(int dtype, const void* QKV, int64_t ld_qkv, void* O, int64_t l
                   const float* k_gamma, const float* k_beta, float eps, const float* mask,
                   int64_t mask_sb, int64_t mask_sh, void* stream);
 /* Kernel sdp_attention takes for this shape: 6 = attn_fa5, one double-buffered 8-wave workgroup per
- * CU (opt-in, hd % 32 == 0, N <= 224), 4 = two persistent 4-wave flash workgroups per CU, one LDS-DMA
+ * CU (diagnostic build only, opt-in, hd % 32 == 0, N <= 224), 4 = two persistent 4-wave flash workgroups per CU, one LDS-DMA
  * K/V buffer each (hd % 32 == 0, N <= 256), 3 = whole-head flash kernels (hd % 32 == 0, head within
  * 160 KiB of LDS; at 9 key tiles the persistent attn_fa6 with three rotating K / V images where they
  * fit, else attn_fa2), 5 = streaming flash kernel (hd % 32 == 0, any N),
  * 2 = one-workgroup flash kernel, 0 = generic. */
 int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask);
-/* Select the bf16 flash kernel tier: 6 = allow attn_fa5, 4 (default) = attn_fa4, 3 = attn_fa2 (both
- * falling back to the streaming attn_fs for heads that do not fit LDS), 5 = force attn_fs, 2 = attn_fa
- * only (each where it applies, else the next lower one).
- * Other values leave the selection unchanged.  Returns the previous selection. */
+/* Select the bf16 flash kernel tier: 4 (default) = attn_fa4, 3 = attn_fa2 (both falling back to the
+ * streaming attn_fs for heads that do not fit LDS), 5 = force attn_fs (each where it applies, else the
+ * next lower one; attn_fa stays the path for hd % 32 != 0).  Diagnostic build only: 6 = allow attn_fa5,
+ * 2 = attn_fa only.  0 queries; an unavailable value returns -1 and leaves the selection unchanged.
+ * Returns the previous selection. */
 int sdp_attention_set_kernel(int k);
 /* Workgroups per CU of the persistent fa4 kernel (0 = as many as LDS and registers allow, at
  * most 4); returns the previous setting. */

@@ -1165,6 +1165,7 @@ __global__ __launch_bounds__(256, 2) void attn_fa4_bf16(const bf16_t* __restrict
   }
 }
 
+#ifdef SDP_DIAG  // attn_fa5: opt-in tier 6, slower in the model than fa4 (round 5); diagnostic build only
 // ---------------------------------------------------------------------------
 // attn_fa5_bf16 — one persistent 8-wave workgroup per CU with K / V double-buffered in LDS
 // (2 x (K + V) x NP16 x HD x 2 B + gamma / beta; N = 200, hd = 96: 161,280 of 163,840 B).
@@ -1272,6 +1273,7 @@ __global__ __launch_bounds__(512) void attn_fa5_bf16(const bf16_t* __restrict__ 
   }
 }
 
+#endif  // SDP_DIAG (attn_fa5)
 // ---------------------------------------------------------------------------
 // attn_fa6_bf16 — the XL shape (256 < N <= 288, 9 key tiles, hd <= 96): one persistent 12-wave
 // workgroup per CU.  A whole head does not fit twice in LDS (N = 260, hd = 96: K or V 52,224 B),
@@ -1705,6 +1707,7 @@ static int launch_attn_fa4(const void* QKV, int64_t ldq, void* O, int64_t ldo, i
   return SDP_CHECK_LAUNCH();
 }
 
+#ifdef SDP_DIAG
 static size_t attn_fa5_bytes(int N, int hd) { return (size_t)4 * ((N + 15) / 16 * 16) * hd * 2 + 16 * (size_t)hd; }
 
 template <int HDT>
@@ -1741,6 +1744,8 @@ static int launch_attn_fa5(const void* QKV, int64_t ldq, void* O, int64_t ldo, i
   return SDP_CHECK_LAUNCH();
 }
 
+#endif  // SDP_DIAG
+
 template <int HDT>
 static int launch_attn_fa(const void* QKV, int64_t ldq, void* O, int64_t ldo, int B, int N, int H, int hd,
                           const float* gq, const float* bq, const float* gk, const float* bk, float eps, float scale,
@@ -1774,18 +1779,28 @@ static size_t attn_fa_bytes(int N, int hd) {
 //     with three rotating K / V images, where those fit 160 KiB;
 //   then attn_fs_bf16 (5), the streaming kernel, for any longer N (hd % 32 == 0), and attn_fa_bf16
 //   (2) for hd % 32 != 0.  Setting 5 forces attn_fs_bf16; 2 allows only attn_fa_bf16.
+// The product library accepts tiers 3, 4 and 5; tier 2 (attn_fa for every shape) and 6 (attn_fa5)
+// exist only in the diagnostic build (make stamps).  An unknown or unavailable tier returns -1 and
+// leaves the selection unchanged; 0 queries it.
 static int g_attn_kernel = 4;
 extern "C" int sdp_attention_set_kernel(int k) {
   const int old = g_attn_kernel;
-  if (k >= 2 && k <= 6) g_attn_kernel = k;
-  return old;
+  if (k == 0) return old;
+#ifdef SDP_DIAG
+  if (k >= 2 && k <= 6) { g_attn_kernel = k; return old; }
+#else
+  if (k >= 3 && k <= 5) { g_attn_kernel = k; return old; }
+#endif
+  return -1;
 }
 
 extern "C" int sdp_attention_variant(int dtype, int N, int n_head, int head_dim, int has_mask) {
   if (dtype != 1 || has_mask || head_dim > 128 || head_dim % 16 != 0) return 0;
   const bool hd32 = head_dim % 32 == 0;
   if (g_attn_kernel == 5 && hd32) return 5;
+#ifdef SDP_DIAG
   if (g_attn_kernel == 6 && hd32 && N <= 224 && attn_fa5_bytes(N, head_dim) <= 160 * 1024) return 6;
+#endif
   if (g_attn_kernel >= 4 && g_attn_kernel != 5 && hd32 && N <= 256 && attn_fa4_bytes(N, head_dim) <= 160 * 1024)
     return 4;
   if (g_attn_kernel >= 3 && hd32 && attn_fa2_bytes(N, head_dim) <= 160 * 1024) return 3;
@@ -1821,6 +1836,7 @@ extern "C" int sdp_attention(int dtype, const void* QKV, int64_t ldq, void* O, i
       default: return launch_attn_fs<4>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
     }
   }
+#ifdef SDP_DIAG
   if (variant == 6) {
     const float *gq = norm ? q_gamma : nullptr, *bq = norm ? q_beta : nullptr;
     const float *gk = norm ? k_gamma : nullptr, *bk = norm ? k_beta : nullptr;
@@ -1831,6 +1847,7 @@ extern "C" int sdp_attention(int dtype, const void* QKV, int64_t ldq, void* O, i
       default: return launch_attn_fa5<4>(QKV, ldq, O, ldo, B, N, n_head, gq, bq, gk, bk, eps, scale, s);
     }
   }
+#endif
   if (variant == 4) {
     const float *gq = norm ? q_gamma : nullptr, *bq = norm ? q_beta : nullptr;
     const float *gk = norm ? k_gamma : nullptr, *bk = norm ? k_beta : nullptr;

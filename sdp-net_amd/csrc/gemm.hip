@@ -452,8 +452,11 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
       ow.step8();
       if (m < M && col_ok) {
         bf16x8* dst = (bf16x8*)(epi.out + (uint64_t)prow * (uint32_t)epi.ldc + col);
-        if (epi.nt_store) __builtin_nontemporal_store(o, dst);
-        else *dst = o;
+#ifdef SDP_DIAG
+        if (epi.nt_store) __builtin_nontemporal_store(o, dst);  // store-policy experiment (diagnostic build)
+        else
+#endif
+        *dst = o;
       }
       if constexpr (TRN == 1) {  // h = dropout(act(z)) from the stored z: sdp_act_fwd's arithmetic
         const float inv = epi.p2 > 0.f ? 1.0f / (1.0f - epi.p2) : 1.0f;
@@ -1179,11 +1182,13 @@ extern "C" int sdp_gemm_force_generic(int on) {
 // bf16 fast-kernel selection: 14 (default) = 8-phase ping-pong 256x256 with the whole-line
 // LDS-staged epilogue (every row group staged before the first store); 9 = the same main
 // loop with the permlane-paired 16-B register epilogue (also the fallback for unaligned /
-// resid_pre-with-activation calls).  Other ids are refused (the old value is kept).
+// resid_pre-with-activation calls).
 static int g_fast_kernel = 14;
-extern "C" int sdp_gemm_set_fast_kernel(int k) {
-  int old = g_fast_kernel;
-  if (k == 9 || k == 14) g_fast_kernel = k;
+extern "C" int sdp_gemm_set_fast_kernel(int k) {  // 0 queries; an unknown id returns -1
+  const int old = g_fast_kernel;
+  if (k == 0) return old;
+  if (k != 9 && k != 14) return -1;
+  g_fast_kernel = k;
   return old;
 }
 
@@ -1224,30 +1229,49 @@ static unsigned long long* tl_take() {
   return g_tl_buf + 2 * (g_tl_next++);
 }
 
-// Phases per K-tile of the 8-phase kernel's main loop: 2 (default: 32 MFMAs per wave-group section,
-// half the group-to-group hand-overs: 3.2k vs 4.3k cycles per K-tile, profiles/r04_gemm_ph2.md) or
-// 4 (16 MFMAs per section).  
-static int g_kloop_phases = 2;
+// Phases per K-tile of the 8-phase kernel's main loop: 2 (32 MFMAs per wave-group section, half the
+// group-to-group hand-overs: 3.2k vs 4.3k cycles per K-tile, profiles/r04_gemm_ph2.md).  The 4-phase
+// loop (16 MFMAs per section), the run-time-flag epilogue for the model's flag combinations
+// (EPI_SPEC=0) and the non-temporal store policy are A/B arms of earlier rounds: they are compiled
+// only into the diagnostic library (make stamps, -DSDP_DIAG).  In the product the setters accept
+// only the product value (0 = query) and return -1 for anything else, so a stale selection fails
+// loudly instead of silently running the default.
+#ifdef SDP_DIAG
+static int g_kloop_phases = 2, g_epi_spec = 1, g_nt_store = 0;
+#else
+static constexpr int g_kloop_phases = 2, g_epi_spec = 1, g_nt_store = 0;
+#endif
 extern "C" int sdp_gemm_set_kloop_phases(int n) {
   const int old = g_kloop_phases;
-  if (n == 2 || n == 4) g_kloop_phases = n;
-  return old;
+  if (n == 0 || n == g_kloop_phases) return old;
+#ifdef SDP_DIAG
+  if (n == 2 || n == 4) { g_kloop_phases = n; return old; }
+#endif
+  return -1;
 }
 
-// 1 (default): the model's epilogue flag combinations take tile_epilogue_fl; 0: the run-time
-// flag epilogue for every call (A/B switch, SDPNET_GEMM_EPI_SPEC=0)
-static int g_epi_spec = 1;
+// 1: the model's epilogue flag combinations take tile_epilogue_fl (product); 0: the run-time flag
+// epilogue for every call (diagnostic build only)
 extern "C" int sdp_gemm_set_epi_spec(int on) {
-  int old = g_epi_spec;
+  const int old = g_epi_spec;
+  if ((on ? 1 : 0) == g_epi_spec) return old;
+#ifdef SDP_DIAG
   g_epi_spec = on ? 1 : 0;
   return old;
+#else
+  return -1;
+#endif
 }
 
-static int g_nt_store = 0;
 extern "C" int sdp_gemm_set_store_policy(int nt) {
-  int old = g_nt_store;
+  const int old = g_nt_store;
+  if ((nt ? 1 : 0) == g_nt_store) return old;
+#ifdef SDP_DIAG
   g_nt_store = nt ? 1 : 0;
   return old;
+#else
+  return -1;
+#endif
 }
 
 #ifdef SDP_GEMM_STAMPS
@@ -1391,6 +1415,7 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
         e.part = part;
         if (part_done) *part_done = true;
       }
+#ifdef SDP_DIAG
 #define SDP_8PH(A, E)                                                                                               \
   do {                                                                                                              \
     if (g_kloop_phases == 2)                                                                                        \
@@ -1400,6 +1425,11 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
       hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, false>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,             \
                          (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn);                     \
   } while (0)
+#else
+#define SDP_8PH(A, E)                                                                                               \
+  hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, true>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,                  \
+                     (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
+#endif
       // exact-erf GELU goes through the runtime-activation epilogue (apply_act)
       const int ak = (act == ACT_GELU && g_exact_gelu) ? -1 : act;
       // the model's epilogue combinations get compile-time flags (tile_epilogue_fl)

@@ -1013,10 +1013,13 @@ static int launch_dw3(int k, const void* X, int64_t ldx, RowMap xm, const float*
 // Highest kernel tier allowed (each tier falls back to the next lower one per shape):
 // 3 (default) = dwconv3_mfma where it applies (bf16, H, W <= 16, C % 32 == 0, k in {3,5,7}),
 // 2 = dwconv2_nhwc (C % 8 == 0, 16-B rows), 1 = dwconv_ln_nhwc (any shape)
+// An unknown tier returns -1 and leaves the selection unchanged (0 queries it).
 static int g_dw_kernel = 3;
 extern "C" int sdp_dwconv_set_kernel(int k) {
   const int old = g_dw_kernel;
-  if (k >= 1 && k <= 3) g_dw_kernel = k;
+  if (k == 0) return old;
+  if (k < 1 || k > 3) return -1;
+  g_dw_kernel = k;
   return old;
 }
 

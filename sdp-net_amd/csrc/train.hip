@@ -1861,19 +1861,21 @@ extern "C" int sdp_ce_loss_ignore(int dtype, const void* logits, int64_t ldl, co
                           ignore_index);
 }
 
-// n[0] = number of labels != ignore_index (float), one workgroup sweeping the labels once.
+// n[0] = number of labels != ignore_index, one workgroup sweeping the labels once.  Counted in
+// integers (exact for every B < 2^31, as torch's count) and converted to float once at the end.
 __global__ __launch_bounds__(1024) void ce_count_k(const int64_t* __restrict__ y, int B, int64_t ignore,
                                                    float* __restrict__ n) {
-  __shared__ float ws[16];
-  float c = 0.f;
-  for (int i = threadIdx.x; i < B; i += 1024) c += (y[i] != ignore) ? 1.f : 0.f;
-  c = wave_sum(c);
+  __shared__ unsigned ws[16];
+  unsigned c = 0;
+  for (int i = threadIdx.x; i < B; i += 1024) c += (y[i] != ignore) ? 1u : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += (unsigned)__shfl_xor((int)c, o, 64);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
   __syncthreads();
   if (threadIdx.x == 0) {
-    float t = 0.f;
+    unsigned t = 0;
     for (int w = 0; w < 16; ++w) t += ws[w];
-    n[0] = t;
+    n[0] = (float)t;
   }
 }
 

@@ -278,12 +278,15 @@ extern "C" int sdp_gemm_wgrad(const void* A, int64_t lda, const void* B, int64_t
   const int64_t nwg = (int64_t)ti * tj * splits;
   if (nwg > (1 << 30)) return (int)hipErrorInvalidValue;
   // the main-loop phase count follows the forward GEMM's (sdp_gemm_set_kloop_phases; 0 = query)
-  if (sdp_gemm_set_kloop_phases(0) == 2)
-    hipLaunchKernelGGL(wg::gemm_wgrad_8ph<true>, dim3((unsigned)nwg), dim3(wg::NTHREADS), 0, (hipStream_t)stream,
+  // (the 4-phase loop exists only in the diagnostic build)
+#ifdef SDP_DIAG
+  if (sdp_gemm_set_kloop_phases(0) != 2)
+    hipLaunchKernelGGL(wg::gemm_wgrad_8ph<false>, dim3((unsigned)nwg), dim3(wg::NTHREADS), 0, (hipStream_t)stream,
                        (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, split_stride, ti, tj, nkt, kchunk_tiles,
                        ktok, (const bf16_t*)zrow);
   else
-    hipLaunchKernelGGL(wg::gemm_wgrad_8ph<false>, dim3((unsigned)nwg), dim3(wg::NTHREADS), 0, (hipStream_t)stream,
+#endif
+    hipLaunchKernelGGL(wg::gemm_wgrad_8ph<true>, dim3((unsigned)nwg), dim3(wg::NTHREADS), 0, (hipStream_t)stream,
                        (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, split_stride, ti, tj, nkt, kchunk_tiles,
                        ktok, (const bf16_t*)zrow);
   return SDP_CHECK_LAUNCH();

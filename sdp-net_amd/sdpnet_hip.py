@@ -170,18 +170,20 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
-        kern = os.environ.get("SDPNET_GEMM_KERNEL")  # A/B switch for the bf16 fast GEMM (benchmarks)
-        if kern:
-            L.sdp_gemm_set_fast_kernel(int(kern))
-        kern = os.environ.get("SDPNET_GEMM_NT_STORE")  # streaming output stores in the GEMM epilogue
-        if kern:
-            L.sdp_gemm_set_store_policy(int(kern))
-        kern = os.environ.get("SDPNET_GEMM_EPI_SPEC")  # compile-time-flag GEMM epilogues (1 default)
-        if kern:
-            L.sdp_gemm_set_epi_spec(int(kern))
-        kern = os.environ.get("SDPNET_GEMM_KLOOP_PHASES")  # 2 (default) or 4 phases per K-tile
-        if kern:
-            L.sdp_gemm_set_kloop_phases(int(kern))
+        # A/B switches of the benchmarks (bench.py records every SDPNET_* variable).  A selection the
+        # loaded library does not offer (the 4-phase k-loop, the run-time-flag epilogue, the NT-store
+        # policy and attention tiers 2 / 6 exist only in the diagnostic build) raises instead of
+        # silently running the default.
+        def knob(var, setter, what):
+            v = os.environ.get(var)
+            if v and setter(int(v)) < 0:
+                raise RuntimeError(f"{var}={v}: {what} not available in {LIB_PATH} (sdp_build_info() = "
+                                   f"{L.sdp_build_info()}); the A/B arms of earlier rounds are compiled only "
+                                   "into the diagnostic library (make -C sdp-net_amd/csrc stamps)")
+        knob("SDPNET_GEMM_KERNEL", L.sdp_gemm_set_fast_kernel, "bf16 fast GEMM kernel id")
+        knob("SDPNET_GEMM_NT_STORE", L.sdp_gemm_set_store_policy, "GEMM store policy")
+        knob("SDPNET_GEMM_EPI_SPEC", L.sdp_gemm_set_epi_spec, "GEMM epilogue specialisation")
+        knob("SDPNET_GEMM_KLOOP_PHASES", L.sdp_gemm_set_kloop_phases, "GEMM k-loop phases")
         kern = os.environ.get("SDPNET_DEBUG_SKIP")  # timing experiments, diagnostic library only
         if kern and int(kern) and L.sdp_debug_skip(int(kern)) < 0:
             raise RuntimeError("SDPNET_DEBUG_SKIP needs the diagnostic library (make -C sdp-net_amd/csrc stamps, "
@@ -190,12 +192,8 @@ def lib():
         kern = os.environ.get("SDPNET_GEMM_GROUP_M")  # tile raster of the 8-phase GEMM (-1 auto, 1 row-major)
         if kern:
             L.sdp_gemm_set_group_m(int(kern))
-        kern = os.environ.get("SDPNET_DW_KERNEL")  # A/B switch for the depthwise conv
-        if kern:
-            L.sdp_dwconv_set_kernel(int(kern))
-        kern = os.environ.get("SDPNET_ATTN_KERNEL")  # A/B switch for the bf16 flash attention
-        if kern:
-            L.sdp_attention_set_kernel(int(kern))
+        knob("SDPNET_DW_KERNEL", L.sdp_dwconv_set_kernel, "depthwise-conv tier")
+        knob("SDPNET_ATTN_KERNEL", L.sdp_attention_set_kernel, "attention tier")
         kern = os.environ.get("SDPNET_ATTN_PER_CU")  # fa4 workgroups per CU (0 = occupancy-derived)
         if kern:
             L.sdp_attn_set_per_cu(int(kern))

@@ -224,8 +224,10 @@ def _layer_setup_context(ctx, inputs, output):
     ctx.save_for_backward(output[1], *params)
     ctx.handle = handle
     ctx.layer = layer
-    ctx.in_shape = list(t.shape)
-    ctx.in_dtype = DTYPE_CODES[t.dtype]
+    # layer 0's input is the image, whose gradient the compiled ops refuse (an empty tensor comes
+    # back): its shape / dtype are not needed, and an fp16 / fp64 image has no dtype code
+    ctx.in_shape = list(t.shape) if layer != 0 else []
+    ctx.in_dtype = DTYPE_CODES[t.dtype] if layer != 0 else 0
 
 
 def _layer_backward_formula(ctx, grad_out, grad_key):

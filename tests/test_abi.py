@@ -44,13 +44,16 @@ def test_attention_variant_selection():
     assert L.sdp_attention_variant(1, 200, 8, 96, 0) == 4   # M: two persistent workgroups per CU
     assert L.sdp_attention_variant(1, 260, 8, 96, 0) == 3   # XL: whole head staged
     assert L.sdp_attention_variant(1, 1000, 8, 96, 0) == 5  # long heads: streamed K / V
-    old = L.sdp_attention_set_kernel(6)                      # opt-in: double-buffered persistent kernel
-    try:
-        assert L.sdp_attention_variant(1, 200, 8, 96, 0) == 6
-        assert L.sdp_attention_variant(1, 240, 8, 96, 0) == 4   # N > 224 -> fa4
-        assert L.sdp_attention_variant(1, 200, 4, 128, 0) == 4  # fa5's double buffer exceeds 160 KiB
-    finally:
-        L.sdp_attention_set_kernel(old)
+    old = L.sdp_attention_set_kernel(6)  # attn_fa5 (slower in the model): diagnostic build only
+    if L.sdp_build_info() == 0:
+        assert old == -1 and L.sdp_attention_set_kernel(0) == 4  # refused, selection unchanged
+    else:
+        try:
+            assert L.sdp_attention_variant(1, 200, 8, 96, 0) == 6
+            assert L.sdp_attention_variant(1, 240, 8, 96, 0) == 4   # N > 224 -> fa4
+            assert L.sdp_attention_variant(1, 200, 4, 128, 0) == 4  # fa5's double buffer exceeds 160 KiB
+        finally:
+            L.sdp_attention_set_kernel(old)
     assert L.sdp_attention_variant(1, 200, 8, 96, 1) == 0   # masks -> generic
     assert L.sdp_attention_variant(0, 200, 8, 96, 0) == 0   # fp32 -> generic
     assert L.sdp_attention_variant(1, 53, 8, 12, 0) == 0    # hd % 8 != 0

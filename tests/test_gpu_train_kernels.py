@@ -276,8 +276,10 @@ def test_gemm_wgrad_kloop_phases_bit_identical(N, K, M, kchunk):
     x = rnd(M, K, seed=36, dtype=BF)
     splits = -(-(-(-M // 64)) // kchunk)
     outs = []
-    for ph in (4, 2):
+    diag = sp.lib().sdp_build_info() != 0  # the 4-phase loop exists only in the diagnostic build
+    for ph in ((4, 2) if diag else (2,)):
         old = sp.lib().sdp_gemm_set_kloop_phases(ph)
+        assert old >= 0
         try:
             slabs = torch.full((splits, N, K), float("nan"), device=DEV)
             sp.gemm_wgrad(dy, x, slabs, M, kchunk, split_stride=N * K)
@@ -285,7 +287,9 @@ def test_gemm_wgrad_kloop_phases_bit_identical(N, K, M, kchunk):
             outs.append(slabs)
         finally:
             sp.lib().sdp_gemm_set_kloop_phases(old)
-    assert torch.equal(outs[0], outs[1])
+    if len(outs) == 2:
+        assert torch.equal(outs[0], outs[1])
+    close(outs[-1].sum(0), dy.float().t() @ x.float(), 1e-3, what="wgrad slab sum vs fp32")
 
 
 def test_gemm_wgrad_8ph_strided_and_training_dispatch():

@@ -23,8 +23,15 @@ import json
 import os
 import re
 import shutil
+import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def gemm_source_sha16():
+    sys.path.insert(0, REPO)
+    import bench as _bench  # the same hash bench.py compares against
+    return _bench.gemm_source_sha16()
 
 
 def short(name):
@@ -143,7 +150,10 @@ def main():
                            write_size_kib_sum=write[kname][0], hbm_bytes_per_launch=int(per),
                            algorithmic_bytes_per_launch=rf["algorithmic_bytes_per_launch"],
                            method="(2*FETCH_SIZE + WRITE_SIZE)*1024 per dispatch, separate --pmc passes, "
-                                  "averaged over all dispatches of the kernel in the bench command")
+                                  "averaged over all dispatches of the kernel in the bench command",
+                           # the build this describes (bench.py reports traffic_stale against it)
+                           lib_md5=bench.get("config", {}).get("lib_md5"),
+                           gemm_src_sha16=gemm_source_sha16())
             L.append(f"- measured HBM-side traffic per launch: {per / 1e6:.1f} MB "
                      f"({per / rf['algorithmic_bytes_per_launch']:.2f}x algorithmic)")
         L.append("")
