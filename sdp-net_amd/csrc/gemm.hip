@@ -1073,6 +1073,326 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   }
 }
 
+// ---------------------------------------------------------------------------
+// Cross-tile kernel (gemm_bf16_ct): the two 4-wave groups of a 512-thread workgroup own DIFFERENT
+// output tiles and run half a tile period apart, so one group's epilogue (GELU / LN fold / residual
+// / stores / LN partials) executes while the other group issues MFMAs on the same SIMDs.
+// gemm_bf16_8ph's two groups share one 256 x 256 tile and reach its epilogue together: every CU's
+// matrix pipes idle for the whole epilogue (4.5-11 us of a ~28-33 us K = 768 tile, round-5 stamps).
+//
+// Workgroup = a run of T consecutive 256 x 256 "pair" tiles of the raster; group g computes the
+// 128 x 256 half [m0 + 128 g, m0 + 128 g + 128) of each (gemm_bf16_8ph's wave-group split), wave
+// wn = 0..3 its 128 x 64 column slice (same acc[4][8] layout, same MFMA, same per-accumulator k
+// order, same epilogue arithmetic: outputs are bit-identical to gemm_bf16_8ph).  Splitting M keeps
+// the large operand X read once per pair tile; only the small weight panel is staged twice (a
+// 256 x 128 split doubled the X traffic and ran the K = 3072 shapes at half speed).  Each group
+// streams its operands through its own 3-slot LDS ring of 32-deep K-steps (X 128 x 32 + W 256 x 32
+// bf16 = 24 KiB per slot, 2 x 72 KiB in all), two steps ahead across tile boundaries, so the next
+// tile's first K-steps land during the epilogue (no prologue on the critical path).
+//
+// Schedule: every K-step of a group is  [load phase: fragment reads of step g, DMA of step g + 2,
+// vmcnt retiring step g + 1] [section: barrier, 32 MFMAs, barrier]; group 1 runs one barrier behind
+// group 0 (as in gemm_bf16_8ph), so one group's load phase lies under the other's MFMA section.  An
+// epilogue step keeps that barrier pattern: its VALU-heavy half (residual loads, staging through LDS
+// with bias / LN fold / activation) lies under the partner's MFMA section, its store half under the
+// partner's load phase.  Group 1 additionally starts half a tile period (S + E steps) late and group
+// 0 pads its end by the same amount, so their epilogues alternate.  Both groups execute the same
+// barrier count (2 + 2 pad + 2 T (S + E)), all control flow is wave-uniform.
+//
+// LDS ring slot: [128 X rows][32 bf16] then [256 W rows][32 bf16], 64-B rows; 16-B chunk c of row r
+// stored at c ^ h((r >> 2) & 3), h = {0, 2, 3, 1}: each 16-lane group of a ds_read_b128 fragment
+// read hits 16 distinct 16-B bank slots.  One LDS-DMA instruction fills 16 rows (1 KiB).
+// ---------------------------------------------------------------------------
+namespace ctk {
+constexpr int GBM = 128, CBN = 256, CBK = 32;
+constexpr int XSB = GBM * CBK * 2;  // 8 KiB
+constexpr int WSB = CBN * CBK * 2;  // 16 KiB
+constexpr int SLOT = XSB + WSB;    // 24 KiB
+constexpr int RING = 3 * SLOT;     // 72 KiB per group
+SDP_DEV int hsw(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+}  // namespace ctk
+
+template <int ACT, int FL, int RE>
+__global__ __launch_bounds__(NTHREADS) void gemm_bf16_ct(const bf16_t* __restrict__ X, int64_t ldx, RowMap xmap,
+                                                        const bf16_t* __restrict__ W, int64_t ldw, Epi<bf16_t> epi,
+                                                        int M, int N, int K, int tiles_m, int tiles_n, int T) {
+  using namespace ctk;
+  constexpr bool HB = FL & EF_BIAS, HL = FL & EF_LN, HR = FL & EF_RESID, HP = FL & EF_PART;
+  constexpr int E = 8 / RE;  // epilogue steps per tile
+  static_assert(8 % RE == 0 && RE * 2048 * 4 <= SLOT, "epilogue staging must fit one ring slot");
+  __shared__ __attribute__((aligned(16))) char smem[2 * RING];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, w4 = wave & 3, wn = w4;
+  constexpr int wm = 0;  // a group's 128 rows are one wave row
+  const int fr = lane & 15, fq = lane >> 4;
+  char* const ring = smem + grp * RING;
+  if (epi.tline && tid == 0) atomicMin(epi.tline, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+
+  // this workgroup's run of pair tiles (XCD-aware: blocks b, b + 8, ... share an XCD and take a
+  // contiguous stretch of runs)
+  int wgi;
+  {
+    const int nwg = gridDim.x, xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+    wgi = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  }
+  const int p0 = wgi * T;
+  const int Tw = min(T, tiles_m * tiles_n - p0);  // >= 1 (host: grid = ceil(pairs / T))
+  const int S = K / CBK;                          // K-steps per tile (>= 2)
+  const int nsteps = Tw * S;
+  const int padB = (S + E) / 2;
+  auto tile_origin = [&](int p, int& m0, int& n0) {
+    int tm, tn;
+    tile_coords(p, tiles_m, tiles_n, epi.group_m, tm, tn);
+    m0 = tm * (2 * GBM) + grp * GBM;
+    n0 = tn * CBN;
+  };
+
+  // ---- LDS-DMA: per wave 2 X pieces (rows 16 (w4 + 4 i) ..) and 4 W pieces per K-step
+  const int prow = lane >> 2;
+  const int pcol = ((lane & 3) ^ hsw(prow)) * 8;  // logical element offset this lane loads
+  const bf16_t* xsrc[2];
+  const bf16_t* wsrc[4];
+  int f_ks = 0, f_tile = 0, f_slot = 0;  // fetch cursor: K-step in tile, tile index, ring slot
+  auto fetch = [&]() {
+    if (f_ks == 0) {
+      int m0, n0;
+      tile_origin(p0 + f_tile, m0, n0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = min(m0 + (w4 + 4 * i) * 16 + prow, M - 1);
+        xsrc[i] = X + xmap(r) * ldx + pcol;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = min(n0 + (w4 + 4 * i) * 16 + prow, N - 1);
+        wsrc[i] = W + (int64_t)r * ldw + pcol;
+      }
+    }
+    char* slot = ring + f_slot * SLOT;
+    const int64_t ko = (int64_t)f_ks * CBK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const AS1 void*)(xsrc[i] + ko), (AS3 void*)(slot + (w4 + 4 * i) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((const AS1 void*)(wsrc[i] + ko), (AS3 void*)(slot + XSB + (w4 + 4 * i) * 1024),
+                                       16, 0, 0);
+    if (++f_ks == S) { f_ks = 0; ++f_tile; }
+    f_slot = f_slot == 2 ? 0 : f_slot + 1;
+  };
+
+  // ---- fragments and MFMAs (gemm_bf16_8ph's D[n][m] layout: A = W rows, B = X rows)
+  const int loff = fr * 64 + ((fq ^ hsw(fr)) << 4);
+  f32x4 acc[4][8];
+  bf16x8 xf[8], wf[4];
+  auto read_frags = [&](const char* slot) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wf[i] = *(const bf16x8*)(slot + XSB + (wn * 64 + i * 16) * 64 + loff);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xf[j] = *(const bf16x8*)(slot + (j * 16) * 64 + loff);
+  };
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // group 1 is the younger half of every SIMD pair: static priority (gemm_bf16_8ph, SDP_PH2_PRIO 1)
+  if (grp == 1) __builtin_amdgcn_s_setprio(1);
+
+  // prologue: K-steps 0 and 1 of the first tile; retire step 0
+  fetch();
+  fetch();
+  SDP_VMCNT(6);
+  bar();
+  if (grp == 1) {  // one barrier behind, and half a tile period late
+    bar();
+    for (int i = 0; i < padB; ++i) { bar(); bar(); }
+  }
+  int fetched = 2, cslot = 0;
+  for (int t = 0; t < Tw; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < S; ++ks) {
+      // load phase: DMA of step g + 2 (into the slot step g - 1 used), fragment reads of step g
+      const bool more = fetched < nsteps;
+      if (more) {
+        fetch();
+        ++fetched;
+      }
+      read_frags(ring + cslot * SLOT);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+      // retire step g + 1 (the next load phase reads it) behind the MFMAs: its DMA had the whole load
+      // phase and section of step g to land; the closing barrier then publishes it to the group
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) SDP_VMCNT(6);
+      else SDP_VMCNT(0);
+      bar();
+      cslot = cslot == 2 ? 0 : cslot + 1;
+    }
+
+    // ---- epilogue of this tile (tile_epilogue_fl's arithmetic, RE row groups per step); the
+    // staging area is the ring slot of the tile's last K-step, free once its section ended
+    char* const stg = ring + (cslot == 0 ? 2 : cslot - 1) * SLOT + w4 * (RE * 2048);
+    int m0, n0;
+    tile_origin(p0 + t, m0, n0);
+    const int cbase = n0 + wn * 64 + pair_col0(fq);
+    f32x4 bv[2][2], sv[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int c0 = min(cbase + 32 * p, N - 8);
+      if constexpr (HB || HL) {
+        if (epi.bias) {
+          bv[p][0] = *(const f32x4*)(epi.bias + c0);
+          bv[p][1] = *(const f32x4*)(epi.bias + c0 + 4);
+        } else {
+          bv[p][0] = bv[p][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      if constexpr (HL) {
+        sv[p][0] = *(const f32x4*)(epi.lnsum + c0);
+        sv[p][1] = *(const f32x4*)(epi.lnsum + c0 + 4);
+      }
+    }
+    const int rlo = lane >> 3, ch = lane & 7;
+    const int col = n0 + wn * 64 + ch * 8;
+    const bool col_ok = col < N;
+    const int wchunk0 = ((fq & 1) << 1) | (fq >> 1);
+    const int mb = m0 + wm * 128 + rlo;
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(epi.out, 0, (int)epi.out_bytes, 0x00020000);
+    RowOff ow(epi.cmap, mb, (uint32_t)epi.ldc * 2u);
+    const uint32_t colb = (uint32_t)col * 2u;
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t prs;
+    [[maybe_unused]] uint32_t pcolb = 0;
+    RowOff pw(epi.cmap, mb, (uint32_t)(N >> 6) * 8u);
+    if constexpr (HP) {
+      prs = __builtin_amdgcn_make_buffer_rsrc(epi.part, 0, (int)epi.part_bytes, 0x00020000);
+      pcolb = (uint32_t)((n0 + wn * 64) >> 6) * 8u;
+    }
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t rrs;
+    RowOff rw(epi.rmap, mb, (uint32_t)epi.ldr * 2u);
+    if constexpr (HR) rrs = __builtin_amdgcn_make_buffer_rsrc((void*)epi.resid, 0, (int)epi.res_bytes, 0x00020000);
+    u32x4 rres[RE][2];
+    static_for<0, E>([&](auto e) {
+      // half 1 (under the partner group's MFMA section): residual loads, staging
+      static_for<0, RE>([&](auto jj) {
+        constexpr int j = decltype(e)::value * RE + decltype(jj)::value;
+        if constexpr (HR) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int m = mb + j * 16 + 8 * q;
+            const uint32_t ro = rw.off;
+            rw.step8();
+            rres[jj][q] = __builtin_bit_cast(
+                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, (m < M && col_ok) ? ro + colb : OFF_DROP, 0, 0));
+          }
+        }
+        char* sl = stg + jj * 2048;
+        f32x2 lr2 = {1.f, 1.f}, lm2 = {0.f, 0.f};
+        if constexpr (HL) {
+          const int mrow = min(m0 + wm * 128 + j * 16 + fr, M - 1);
+          const float2 st = *(const float2*)(epi.lnst + 2 * (int64_t)mrow);
+          lr2 = f32x2{st.y, st.y};
+          lm2 = f32x2{-st.y * st.x, -st.y * st.x};
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          float v[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                       __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+            v[r] = __uint_as_float(sw[0]);
+            v[4 + r] = __uint_as_float(sw[1]);
+          }
+          u32x4 o;
+#pragma unroll
+          for (int e2 = 0; e2 < 8; e2 += 2) {
+            f32x2 x2 = {v[e2], v[e2 + 1]};
+            if constexpr (HL) {
+              const f32x2 b2 = {bv[p][e2 >> 2][e2 & 3], bv[p][e2 >> 2][(e2 & 3) + 1]};
+              const f32x2 s2 = {sv[p][e2 >> 2][e2 & 3], sv[p][e2 >> 2][(e2 & 3) + 1]};
+              x2 = x2 * lr2 + (s2 * lm2 + b2);
+            } else if constexpr (HB) {
+              x2 = x2 + f32x2{bv[p][e2 >> 2][e2 & 3], bv[p][e2 >> 2][(e2 & 3) + 1]};
+            }
+            if constexpr (ACT == ACT_GELU) {
+              x2 = gelu_fast2(x2);
+            } else if constexpr (ACT != ACT_NONE) {
+              x2.x = epi_act<ACT>(epi.act, x2.x);
+              x2.y = epi_act<ACT>(epi.act, x2.y);
+            }
+            o[e2 >> 1] = pack_bf16x2(x2.x, x2.y);
+          }
+          *(u32x4*)(sl + fr * 128 + (((4 * p + wchunk0) ^ (fr & 7)) << 4)) = o;
+        }
+      });
+      bar();
+      // half 2 (under the partner's load phase): read back whole lines, residual add, stores, partials
+      static_for<0, RE>([&](auto jj) {
+        constexpr int j = decltype(e)::value * RE + decltype(jj)::value;
+        const char* sl = stg + jj * 2048;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int r = rlo + 8 * q;
+          u32x4 o = *(const u32x4*)(sl + r * 128 + ((ch ^ (r & 7)) << 4));
+          const int m = mb + j * 16 + 8 * q;
+          if constexpr (HR) o = add_bf16x8(o, rres[jj][q]);
+          const bool ok = m < M && col_ok;
+          const uint32_t rowoff = ow.off;
+          ow.step8();
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4v, o), ors, ok ? rowoff + colb : OFF_DROP, 0, 0);
+          if constexpr (HP) {
+            const bf16x2n one = {(__bf16)1.0f, (__bf16)1.0f};
+            float sm = 0.f;
+            uint32_t uv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              uint32_t u = o[i];
+              asm volatile("" : "+v"(u));  // see tile_epilogue_fl (hipcc dot2 operand miscompile)
+              uv[i] = u;
+              sm = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2n, u), one, sm, false);
+            }
+            sm = dpp_sum8(sm);
+            const float mean = sm * (1.0f / 64.0f);
+            const f32x2 mu2 = {mean, mean};
+            f32x2 q2 = {0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const f32x2 d = f32x2{__uint_as_float(uv[i] << 16), __uint_as_float(uv[i] & 0xffff0000u)} - mu2;
+              q2 = d * d + q2;
+            }
+            const float m2 = dpp_sum8(q2.x + q2.y);
+            const uint32_t poff = pw.off;
+            pw.step8();
+            __builtin_amdgcn_raw_buffer_store_b64(i32x2v{__float_as_int(mean), __float_as_int(m2)}, prs,
+                                                  (ok && ch == 0) ? poff + pcolb : OFF_DROP, 0, 0);
+          }
+        }
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();
+    });
+  }
+  if (grp == 0) {  // the same barrier count as group 1
+    bar();
+    for (int i = 0; i < padB; ++i) { bar(); bar(); }
+  }
+  if (epi.tline) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) atomicMax(epi.tline + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+}
+
 #undef SDP_VMCNT
 
 }  // namespace fast
@@ -1274,6 +1594,19 @@ extern "C" int sdp_gemm_set_store_policy(int nt) {
 #endif
 }
 
+// Cross-tile kernel (gemm_bf16_ct): pair tiles per workgroup (0 = off: gemm_bf16_8ph everywhere)
+// and row groups per epilogue step (1 or 2); applied to the specialised-epilogue calls with
+// K <= g_ct_kmax.
+static int g_ct_tiles = 0, g_ct_re = 2, g_ct_kmax = 1024;
+extern "C" int sdp_gemm_set_ct(int tiles, int re, int kmax) {
+  const int old = g_ct_tiles;
+  if (tiles < 0 || tiles > 64 || (re != 1 && re != 2) || kmax < 64) return -1;
+  g_ct_tiles = tiles;
+  g_ct_re = re;
+  g_ct_kmax = kmax;
+  return old;
+}
+
 #ifdef SDP_GEMM_STAMPS
 extern "C" int sdp_gemm_phase_stamps(void* dst) {
   hipError_t rc = hipDeviceSynchronize();
@@ -1450,7 +1783,31 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
       const bool spec = g_epi_spec && fk == 14 && small && !e.nt_store && (ak == ACT_NONE || ak == ACT_GELU) &&
                         (fl == 0 || fl == fast::EF_BIAS || fl == (fast::EF_BIAS | fast::EF_LN) ||
                          fl == (fast::EF_RESID | fast::EF_PART) || fl == (fast::EF_BIAS | fast::EF_RESID | fast::EF_PART));
-      if (spec) {
+      if (spec && g_ct_tiles > 0 && K <= g_ct_kmax) {
+        const int pairs = tm * tn;
+        const int grid = (pairs + g_ct_tiles - 1) / g_ct_tiles;
+#define SDP_CT(A, F)                                                                                              \
+  do {                                                                                                            \
+    if (g_ct_re == 2)                                                                                             \
+      hipLaunchKernelGGL((fast::gemm_bf16_ct<A, F, 2>), dim3(grid), dim3(fast::NTHREADS), 0, s, (const bf16_t*)X, \
+                         ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, g_ct_tiles);                        \
+    else                                                                                                          \
+      hipLaunchKernelGGL((fast::gemm_bf16_ct<A, F, 1>), dim3(grid), dim3(fast::NTHREADS), 0, s, (const bf16_t*)X, \
+                         ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, g_ct_tiles);                        \
+  } while (0)
+#define SDP_CT_FL(A)                                                            \
+  do {                                                                          \
+    if (fl == (fast::EF_BIAS | fast::EF_LN)) SDP_CT(A, 3);                      \
+    else if (fl == (fast::EF_RESID | fast::EF_PART)) SDP_CT(A, 12);             \
+    else if (fl == 0) SDP_CT(A, 0);                                             \
+    else if (fl == fast::EF_BIAS) SDP_CT(A, 1);                                 \
+    else SDP_CT(A, 13);                                                         \
+  } while (0)
+        if (ak == ACT_NONE) SDP_CT_FL(ACT_NONE);
+        else SDP_CT_FL(ACT_GELU);
+#undef SDP_CT_FL
+#undef SDP_CT
+      } else if (spec) {
 #define SDP_8PH_FL(A)                                                           \
   do {                                                                          \
     if (fl == (fast::EF_BIAS | fast::EF_LN)) SDP_8PH(A, 16 + 3);                \

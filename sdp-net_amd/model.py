@@ -163,18 +163,15 @@ class MainModel(SdPModel):
                 # one opaque op per sub-layer, each with an op as its autograd formula
                 # (sdpnet_ops.train_layer), or the whole model as one op pair
                 # (SDPNET_COMPILE_TRAIN_OPS=model: sdpnet_ops.train_forward / train_backward)
-                if return_raw_outputs:
-                    raise NotImplementedError("sdpnet training path returns logits only")
-                if x.requires_grad:  # the compiled ops give the image no gradient: refuse, never drop it
-                    raise NotImplementedError("sdpnet compiled training: no gradient into the input image "
-                                              "(the eager training path computes it)")
+                # (raw outputs and an image that requires grad take the per-layer ops: the head op with
+                # raw outputs, layer 0's backward with the image gradient)
                 code = sdpnet_ops.DTYPE_CODES[compute_dtype(x, self)]
-                if _COMPILE_TRAIN_OPS == "model":
+                if _COMPILE_TRAIN_OPS == "model" and not return_raw_outputs and not x.requires_grad:
                     params = [p for p in self.parameters()]
                     logits, _ = torch.ops.sdpnet.train_forward(x, params, self._sdp_handle, num_registers, code)
                     return logits
                 import sdpnet_train
-                return sdpnet_train.compiled_train_forward(self, x, num_registers, code)
+                return sdpnet_train.compiled_train_forward(self, x, num_registers, code, return_raw_outputs)
             import sdpnet_train
             return sdpnet_train.train_forward(self, x, num_registers, return_raw_outputs)
         if torch.compiler.is_compiling():

@@ -26,7 +26,7 @@ import torch
 from torch import Tensor
 
 from sdpnet_engine import num_reg_rows
-from typing import List
+from typing import List, Optional
 
 _MODELS: "dict[int, weakref.ref]" = {}
 _NEXT = itertools.count(1)
@@ -164,18 +164,20 @@ train_forward.register_autograd(_train_backward_formula, setup_context=_train_se
 # selects the single op pair above): one op per patch-embedding / ConvMixer / EncoderLayer /
 # head (sdpnet_train.train_layers order), each with an autograd formula that is a second op:
 #
-#   sdpnet::train_layer(t, params, handle, layer, num_registers, dtype_code, batch) -> (out, key)
+#   sdpnet::train_layer(t, params, handle, layer, num_registers, dtype_code, batch, need_dx) -> (out, key)
 #   sdpnet::train_layer_backward(grad_out, key, params, handle, layer, in_shape, in_dtype) -> (grad_in, grads)
 #
-# so the compiled backward runs layer by layer and DDP (training_tools.py:36-39 compiles the
+# (need_dx: layer 0's image requires grad, its backward op then returns the image gradient), so the
+# compiled backward runs layer by layer and DDP (training_tools.py:36-39 compiles the
 # DDP-wrapped model) all-reduces a bucket while earlier layers' backward ops still run.  The
 # layer's ctx is parked under key.data_ptr() as for the whole-model pair.
 # ---------------------------------------------------------------------------
 @torch.library.custom_op("sdpnet::train_layer", mutates_args=(), device_types="cuda")
 def train_layer(t: Tensor, params: List[Tensor], handle: int, layer: int, num_registers: int, dtype_code: int,
-                batch: int) -> Tuple[Tensor, Tensor]:
+                batch: int, need_dx: int) -> Tuple[Tensor, Tensor]:
     import sdpnet_train
-    out, rec = sdpnet_train.layer_forward(lookup(handle), layer, t, num_registers, _DTYPES[dtype_code])
+    out, rec = sdpnet_train.layer_forward(lookup(handle), layer, t, num_registers, _DTYPES[dtype_code],
+                                          need_dx=bool(need_dx))
     key = torch.empty(1, dtype=torch.int64, device=t.device)
     _TAPES[key.data_ptr()] = rec
     weakref.finalize(key, _drop_tape, key.data_ptr())
@@ -183,7 +185,7 @@ def train_layer(t: Tensor, params: List[Tensor], handle: int, layer: int, num_re
 
 
 @train_layer.register_fake
-def _train_layer_fake(t, params, handle, layer, num_registers, dtype_code, batch):
+def _train_layer_fake(t, params, handle, layer, num_registers, dtype_code, batch, need_dx):
     import sdpnet_train
     model = lookup(handle)
     kind, _ = sdpnet_train.train_layers(model)[layer]
@@ -206,35 +208,108 @@ def train_layer_backward(grad_out: Tensor, key: Tensor, params: List[Tensor], ha
     if rec is None:
         raise RuntimeError("sdpnet: no saved training forward for this layer's backward (backward run twice?)")
     gin, grads = sdpnet_train.layer_backward(rec, grad_out)
-    if gin is None:  # the image input of layer 0 gets no gradient (ConvPatcher input, as eager)
+    if gin is None:  # layer 0 with an image that needs no gradient
         gin = grad_out.new_empty((0,))
     return gin, grads
+
+
+# dtypes a layer input (and so its gradient) may have: the token rows are fp32 / bf16, an image that
+# requires grad may also be fp16 / fp64 (patchify converts it to the compute dtype)
+_GRAD_DTYPES = [torch.float32, torch.bfloat16, torch.float16, torch.float64]
 
 
 @train_layer_backward.register_fake
 def _train_layer_backward_fake(grad_out, key, params, handle, layer, in_shape, in_dtype):
     # (in_shape, in_dtype): the layer's forward input, i.e. its gradient's shape / dtype; the input
-    # itself is not kept alive for the backward (eager frees it once the layer's ctx is done with it)
-    gin = grad_out.new_empty((0,)) if layer == 0 else grad_out.new_empty(in_shape, dtype=_DTYPES[in_dtype])
+    # itself is not kept alive for the backward (eager frees it once the layer's ctx is done with it).
+    # Layer 0 records an empty shape when the image needs no gradient.
+    gin = grad_out.new_empty(in_shape, dtype=_GRAD_DTYPES[in_dtype]) if in_shape else grad_out.new_empty((0,))
     return gin, [torch.empty_like(p) for p in params]
 
 
 def _layer_setup_context(ctx, inputs, output):
-    t, params, handle, layer, num_registers, dtype_code, batch = inputs
+    t, params, handle, layer, num_registers, dtype_code, batch, need_dx = inputs
     ctx.save_for_backward(output[1], *params)
     ctx.handle = handle
     ctx.layer = layer
-    # layer 0's input is the image, whose gradient the compiled ops refuse (an empty tensor comes
-    # back): its shape / dtype are not needed, and an fp16 / fp64 image has no dtype code
-    ctx.in_shape = list(t.shape) if layer != 0 else []
-    ctx.in_dtype = DTYPE_CODES[t.dtype] if layer != 0 else 0
+    ctx.want_gin = layer != 0 or bool(need_dx)
+    ctx.in_shape = list(t.shape) if ctx.want_gin else []
+    ctx.in_dtype = _GRAD_DTYPES.index(t.dtype) if ctx.want_gin else 0
 
 
 def _layer_backward_formula(ctx, grad_out, grad_key):
     key, *params = ctx.saved_tensors
     gin, grads = torch.ops.sdpnet.train_layer_backward(grad_out, key, params, ctx.handle, ctx.layer, ctx.in_shape,
                                                        ctx.in_dtype)
-    return (None if ctx.layer == 0 else gin), list(grads), None, None, None, None, None
+    return (gin if ctx.want_gin else None), list(grads), None, None, None, None, None, None
 
 
 train_layer.register_autograd(_layer_backward_formula, setup_context=_layer_setup_context)
+
+
+# The head layer with the raw outputs (return_raw_outputs=True in train mode, model.py:145-149):
+#   sdpnet::train_head_raw(t, params, handle, layer, num_registers, dtype_code, batch, hp, wp)
+#       -> (logits, x_raw_output [B, C, hp, wp], registers [B, R, C], key)
+#   sdpnet::train_head_raw_backward(grad_logits, grad_x_raw?, grad_registers?, key, params, handle,
+#       in_shape, in_dtype) -> (grad_t, grads)
+# The raw outputs are copies of the final token rows (_RawOutFn's kernels); their gradients are added
+# to the head's token-row gradient by a HIP pass inside the backward op.
+@torch.library.custom_op("sdpnet::train_head_raw", mutates_args=(), device_types="cuda")
+def train_head_raw(t: Tensor, params: List[Tensor], handle: int, layer: int, num_registers: int, dtype_code: int,
+                   batch: int, hp: int, wp: int) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    import sdpnet_train
+    model = lookup(handle)
+    C = model.conv_init.conv.out_channels
+    geo = (batch, _register_rows(model, num_registers), hp, wp, C)
+    xo, regs = sdpnet_train.raw_outputs(t, geo)
+    logits, rec = sdpnet_train.layer_forward(model, layer, t, num_registers, _DTYPES[dtype_code])
+    key = torch.empty(1, dtype=torch.int64, device=t.device)
+    _TAPES[key.data_ptr()] = (rec, geo)
+    weakref.finalize(key, _drop_tape, key.data_ptr())
+    return logits, xo, regs, key
+
+
+@train_head_raw.register_fake
+def _train_head_raw_fake(t, params, handle, layer, num_registers, dtype_code, batch, hp, wp):
+    model = lookup(handle)
+    lins = [m for m in model.output_head.output_head if isinstance(m, torch.nn.Linear)]
+    C = model.conv_init.conv.out_channels
+    R = _register_rows(model, num_registers)
+    return (t.new_empty((batch, lins[-1].out_features), dtype=_DTYPES[dtype_code]),
+            t.new_empty((batch, C, hp, wp)), t.new_empty((batch, R, C)), t.new_empty((1,), dtype=torch.int64))
+
+
+@torch.library.custom_op("sdpnet::train_head_raw_backward", mutates_args=(), device_types="cuda")
+def train_head_raw_backward(grad_logits: Tensor, grad_xo: Optional[Tensor], grad_regs: Optional[Tensor], key: Tensor,
+                            params: List[Tensor], handle: int, in_shape: List[int],
+                            in_dtype: int) -> Tuple[Tensor, List[Tensor]]:
+    import sdpnet_train
+    tape = _TAPES.pop(key.data_ptr(), None)
+    if tape is None:
+        raise RuntimeError("sdpnet: no saved training forward for the head's backward (backward run twice?)")
+    rec, geo = tape
+    gin, grads = sdpnet_train.layer_backward(rec, grad_logits)
+    return sdpnet_train.add_raw_output_grads(gin, grad_xo, grad_regs, geo), grads
+
+
+@train_head_raw_backward.register_fake
+def _train_head_raw_backward_fake(grad_logits, grad_xo, grad_regs, key, params, handle, in_shape, in_dtype):
+    return grad_logits.new_empty(in_shape, dtype=_GRAD_DTYPES[in_dtype]), [torch.empty_like(p) for p in params]
+
+
+def _head_raw_setup_context(ctx, inputs, output):
+    t, params, handle, layer, num_registers, dtype_code, batch, hp, wp = inputs
+    ctx.save_for_backward(output[3], *params)
+    ctx.handle = handle
+    ctx.in_shape = list(t.shape)
+    ctx.in_dtype = _GRAD_DTYPES.index(t.dtype)
+
+
+def _head_raw_backward_formula(ctx, grad_logits, grad_xo, grad_regs, grad_key):
+    key, *params = ctx.saved_tensors
+    gin, grads = torch.ops.sdpnet.train_head_raw_backward(grad_logits, grad_xo, grad_regs, key, params, ctx.handle,
+                                                          ctx.in_shape, ctx.in_dtype)
+    return gin, list(grads), None, None, None, None, None, None, None
+
+
+train_head_raw.register_autograd(_head_raw_backward_formula, setup_context=_head_raw_setup_context)

@@ -755,7 +755,7 @@ class _EmbedFn(torch.autograd.Function):
         if R:
             sp.copy_rows(table.contiguous(), C, 0, tok, C, N * C, B, R, C)
         # the image gradient (an input that requires grad, e.g. input-gradient attacks) needs w and the
-        # image geometry; the compiled per-layer path never asks for it (compiled_train_forward refuses)
+        # image geometry (the compiled per-layer path passes need_dx to layer 0's op)
         need_dx = bool(getattr(ctx, "needs_input_grad", (False,))[0])
         ctx.st = dict(patches=patches, geo=(B, R, Hp, Wp, C, P, N, p, kp), dt=dt, sdt=sdt, conv_emb=conv_emb, act=act, z=z,
                       nrow_eh=None if conv_emb else eh.shape[0], nrow_ew=None if conv_emb else ew.shape[0],
@@ -1353,13 +1353,15 @@ class _Session:
     pass
 
 
-def layer_forward(model, layer: int, t: torch.Tensor, num_registers: int, dt):
+def layer_forward(model, layer: int, t: torch.Tensor, num_registers: int, dt, need_dx: bool = False):
     """Forward of sub-layer ``layer`` (train_layers order) with its ctx returned for the
-    backward op.  Layer 0 takes the image and opens the session, the last layer closes it."""
+    backward op.  Layer 0 takes the image and opens the session, the last layer closes it;
+    need_dx: the image requires grad (layer 0 then keeps what its input gradient needs)."""
     global _WPREP
     kind, mod = train_layers(model)[layer]
     params = layer_params(model, kind, mod)
     ctx = _Ctx()
+    ctx.needs_input_grad = (bool(need_dx),)
     if kind == "embed":
         S = _Session()
         B, _, Hi, Wi = t.shape
@@ -1432,16 +1434,48 @@ def layer_backward(rec, g: torch.Tensor):
         if t._base is not None:  # e.g. the q/k/v slices of one fused dW: op outputs may not alias
             t = t.clone()
         grads.append(t)
-    return (outs[0] if fn is not _EmbedFn else None), grads
+    return outs[0], grads  # layer 0: the image gradient, or None when the image needs none
 
 
-def compiled_train_forward(model, x: torch.Tensor, num_registers: int, dtype_code: int) -> torch.Tensor:
-    """The training forward as a chain of sdpnet::train_layer ops (traced by Dynamo)."""
-    t = x  # (MainModel.forward refuses an image that requires grad on this path)
+def raw_outputs(tok: torch.Tensor, geo):
+    """(x_raw_output [B, C, H, W], registers [B, R, C]) of the final token buffer (model.py:147-148),
+    _RawOutFn's forward without autograd (the compiled head-with-raw-outputs op)."""
+    return _RawOutFn.forward(_Ctx(), tok, geo)
+
+
+def add_raw_output_grads(dtok: torch.Tensor, dxo, dregs, geo) -> torch.Tensor:
+    """dtok + the token-row gradient of the raw outputs (_RawOutFn.backward), summed by a HIP pass
+    (the eager path leaves that sum to autograd's accumulation)."""
+    if dxo is None and dregs is None:
+        return dtok
+    ctx = _Ctx()
+    ctx.geo, ctx.sdt = geo, dtok.dtype
+    draw, _ = _RawOutFn.backward(ctx, dxo, dregs)
+    M, C = dtok.shape
+    out = torch.empty_like(dtok)
+    sp.rowscale_add(_dense(dtok), _dense(out), M, C, resid=_dense(draw))
+    return out
+
+
+def compiled_train_forward(model, x: torch.Tensor, num_registers: int, dtype_code: int,
+                           return_raw_outputs: bool = False):
+    """The training forward as a chain of sdpnet::train_layer ops (traced by Dynamo).  An image that
+    requires grad gets its gradient from layer 0's backward op (the eager path's dY W + col2im);
+    return_raw_outputs runs the head as sdpnet::train_head_raw, which also returns
+    (x_raw_output, registers) and sums their gradients into the token rows in its backward op."""
+    t = x
     B = x.shape[0]
-    for i, (kind, mod) in enumerate(train_layers(model)):
+    need_dx = int(x.requires_grad)
+    layers = train_layers(model)
+    for i, (kind, mod) in enumerate(layers):
         params = [q for q in layer_params(model, kind, mod) if q is not None]
-        t, _ = torch.ops.sdpnet.train_layer(t, params, model._sdp_handle, i, num_registers, dtype_code, B)
+        if return_raw_outputs and i == len(layers) - 1:
+            p = model.conv_init.patch_size
+            logits, xo, regs, _ = torch.ops.sdpnet.train_head_raw(t, params, model._sdp_handle, i, num_registers,
+                                                                  dtype_code, B, x.shape[2] // p, x.shape[3] // p)
+            return logits, xo, regs
+        t, _ = torch.ops.sdpnet.train_layer(t, params, model._sdp_handle, i, num_registers, dtype_code, B,
+                                            need_dx if i == 0 else 0)
     return t
 
 

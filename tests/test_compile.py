@@ -162,6 +162,60 @@ def test_train_mode_fullgraph_one_op_per_sublayer(conv_first):
     assert "train_layer_backward" in str(torch.ops.sdpnet.train_layer_backward)
 
 
+def test_train_mode_raw_outputs_and_image_grad_trace_fullgraph():
+    """model.train() under torch.compile with return_raw_outputs=True and an image that requires grad
+    (both refused before round 6): one train_layer op per sub-layer, the head as train_head_raw (logits,
+    x_raw_output, registers), layer 0 told that its image needs a gradient, 0 graph breaks."""
+    m = _model(ffn_dropout=0.2).train()
+    with FakeTensorMode(allow_non_fake_inputs=True):
+        x = torch.empty(2, 3, 224, 224, device="cuda", requires_grad=True)
+        gm, _ = torch._dynamo.export(lambda t: m(t, return_raw_outputs=True))(x)
+    nodes = _sdp_nodes(gm)
+    layers = [n for n in nodes if "train_layer" in str(n.target)]
+    heads = [n for n in nodes if "train_head_raw" in str(n.target)]
+    assert len(heads) == 1 and len(layers) == len(__import__("sdpnet_train").train_layers(m)) - 1
+    assert layers[0].args[7] == 1 and all(n.args[7] == 0 for n in layers[1:])  # need_dx on layer 0 only
+    assert len(heads[0].args) == 9  # ..., batch, hp, wp: the image grid of the raw output (symbolic here)
+    # the graph returns the head op's first three outputs: logits [B, 10], x_raw [B, C, hp, wp], registers [B, R, C]
+    out = [n for n in gm.graph.nodes if n.op == "output"][0]
+    assert len(out.args[0]) == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bf16", [False, True])
+def test_compiled_train_raw_outputs_and_image_grad_equal_eager(bf16):
+    """Compiled training (fullgraph=True, dynamic=True) with return_raw_outputs=True and an image
+    that requires grad: logits, raw outputs, every parameter gradient and the image gradient equal
+    the eager training path's bit for bit (reference model.py:145-149 returns the raw outputs)."""
+    import torch.nn.functional as F
+    torch.manual_seed(0)
+    m = _model(ffn_dropout=0.2, attn_dropout=0.2, stochastic_depth_p=[0.1, 0.2]).to("cuda").train()
+    x0 = torch.randn(3, 3, 224, 224, device="cuda")
+    y = torch.randint(0, 10, (3,), device="cuda")
+
+    def step(mod):
+        m.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        torch.manual_seed(7)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+            logits, xo, regs = mod(x, return_raw_outputs=True)
+        loss = F.cross_entropy(logits.float(), y) + 0.1 * xo.float().square().mean() + regs.float().mean()
+        loss.backward()
+        grads = {k: (p.grad.clone() if p.grad is not None else torch.zeros_like(p)) for k, p in m.named_parameters()}
+        return loss.detach(), logits.detach(), xo.detach(), regs.detach(), x.grad.clone(), grads
+
+    eager = step(m)
+    torch._dynamo.reset()
+    comp = step(torch.compile(m, fullgraph=True, dynamic=True))
+    for a, b, what in zip(eager[:5], comp[:5], ("loss", "logits", "x_raw", "registers", "image grad")):
+        assert a.shape == b.shape and torch.equal(a, b), what
+    assert eager[4].abs().sum() > 0
+    for k in eager[5]:
+        assert torch.equal(eager[5][k], comp[5][k]), k
+    import sdpnet_ops
+    assert not sdpnet_ops._TAPES
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("ops", ["layer", "model"])
 @pytest.mark.parametrize("bf16", [False, True])

@@ -718,3 +718,54 @@ def test_gemm_two_streams_and_graph_replay():
     torch.cuda.synchronize()
     for y, r in zip(ys, ref):
         assert torch.equal(y, r)
+
+
+# ------------------------------------------------- cross-tile GEMM (gemm_bf16_ct)
+@pytest.mark.parametrize("tiles,re", [(1, 2), (2, 2), (3, 1), (4, 2), (5, 1)])
+@pytest.mark.parametrize("combo", ["ln_bias", "resid_part", "bias_resid_part", "plain", "bias"])
+@pytest.mark.parametrize("M,N,K,act", [(25088, 768, 768, 1), (1003, 3072, 768, 1), (300, 2304, 768, 0),
+                                       (513, 320, 128, 1), (4000, 768, 3072, 0), (777, 1000, 64, 1)])
+def test_gemm_cross_tile_bit_identical(tiles, re, combo, M, N, K, act):
+    """The cross-tile kernel (two wave groups on different tiles, half a tile period apart, one LDS
+    ring each) runs gemm_bf16_8ph's MFMAs in the same per-accumulator order and its epilogue
+    arithmetic: outputs and LN partials are bit-identical -- row-mapped token buffer, in-place
+    residual, ragged M / N, runs of 1..5 pair tiles per workgroup (ragged last run)."""
+    if N % 8:
+        pytest.skip("whole-line epilogue needs N % 8 == 0")
+    B_, R = 2, 3
+    P = (M + B_ - 1) // B_
+    Mt = B_ * P
+    Nt = R + P
+    x = rnd(Mt, K, dtype=BF, seed=181)
+    w = rnd(N, K, dtype=BF, seed=182, scale=0.05)
+    b = rnd(N, seed=183) if combo in ("ln_bias", "bias", "bias_resid_part") else None
+    has_r = combo in ("resid_part", "bias_resid_part")
+    tok0 = rnd(B_ * Nt, N, dtype=BF, seed=184)
+    nch = (N + 63) // 64
+    ln = None
+    if combo == "ln_bias":
+        part_x = torch.empty(Mt, (K + 63) // 64, 2, device=DEV)
+        sp.row_partials(sp.dense(x), Mt, K, part_x)
+        st = torch.empty(Mt, 2, device=DEV)
+        sp.ln_stats(part_x, sp.dense(x), Mt, K, 1e-5, st)
+        g, be = rnd(K, seed=185) * 0.2 + 1, rnd(K, seed=186) * 0.2
+        w, colsum, b = sp.fold_ln_weight(w.float(), g, be, b, BF)
+        ln = (st, colsum)
+    outs = []
+    for ct in (0, tiles):
+        old = sp.lib().sdp_gemm_set_ct(ct, re, 4096)
+        assert old >= 0
+        try:
+            tok = tok0.clone()
+            img = sp.Rows(tok, N, P, Nt, R)
+            part = torch.full((B_ * Nt, nch, 2), float("nan"), device=DEV) if has_r and N % 64 == 0 else None
+            sp.gemm(sp.dense(x), w, img, Mt, N, K, bias=b, resid=img if has_r else None, act=act, ln=ln, part=part)
+            torch.cuda.synchronize()
+            outs.append((tok, part))
+        finally:
+            sp.lib().sdp_gemm_set_ct(old, 2, 1024)
+    assert torch.equal(outs[0][0], outs[1][0]), "cross-tile output differs from gemm_bf16_8ph"
+    if outs[0][1] is not None:  # (register rows stay NaN in both)
+        p0, p1 = outs[0][1], outs[1][1]
+        assert torch.equal(torch.isnan(p0), torch.isnan(p1)), "cross-tile LN partials: rows written differ"
+        assert torch.equal(p0.nan_to_num(0.0), p1.nan_to_num(0.0)), "cross-tile LN partials differ"

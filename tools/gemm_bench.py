@@ -59,14 +59,15 @@ def main():
     ap.add_argument("--exact-gelu", default="0", help="GELU forms to A/B (0 tanh form, 1 exact erf)")
     ap.add_argument("--epi-spec", default="1", help="epilogue specialisation A/B (0 run-time flags, 1 compile-time)")
     ap.add_argument("--kloop", default="2", help="main-loop phases per K-tile A/B (4, 2)")
+    ap.add_argument("--ct", default="0", help="cross-tile kernel settings to A/B: 'tiles[:re[:kmax]]' items, 0 = off")
     ap.add_argument("--warm-s", type=float, default=0.5, help="seconds of warm-up launches per variant")
     ap.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) as a yardstick")
     args = ap.parse_args()
 
     def combos():
-        return [(kk, int(s_), int(d), int(c), int(e), int(kl)) for kk in args.kernels.split(",")
+        return [(kk, int(s_), int(d), c, int(e), int(kl)) for kk in args.kernels.split(",")
                 for s_ in args.streams.split(",") for d in args.exact_gelu.split(",")
-                for c in ["0"] for e in args.epi_spec.split(",") for kl in args.kloop.split(",")]
+                for c in args.ct.split(",") for e in args.epi_spec.split(",") for kl in args.kloop.split(",")]
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(0)
     total_us = {}
@@ -78,6 +79,8 @@ def main():
             sp.lib().sdp_gemm_set_kloop_phases(kl)
             sp.lib().sdp_gemm_set_fast_kernel(int(kern))
             sp.lib().sdp_gemm_set_exact_gelu(dsy)
+            ct_t, ct_re, ct_k = (sch.split(":") + ["2", "1024"][len(sch.split(":")) - 1:])[:3]
+            assert sp.lib().sdp_gemm_set_ct(int(ct_t), int(ct_re), int(ct_k)) >= 0
             streams = [torch.cuda.Stream() for _ in range(ns)]
             parts = []
             step = (M + ns - 1) // ns
@@ -117,7 +120,7 @@ def main():
             diff = float((y.float() - ref_y.float()).abs().max())
             tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
             total_us[(name, kern, ns, dsy, sch, spc, kl)] = us
-            print(f"{name:11s} M={M:6d} N={N:5d} K={K:5d} kern={kern} streams={ns} exact_gelu={dsy} spec={spc} kloop={kl} "
+            print(f"{name:11s} M={M:6d} N={N:5d} K={K:5d} kern={kern} ct={sch} streams={ns} exact_gelu={dsy} spec={spc} kloop={kl} "
                   f"{us:9.1f} us  {tf:7.1f} TF/s  ({100 * tf / 2516.6:4.1f}% of bf16 peak)  max|diff vs first| {diff:.3g}", flush=True)
         if args.torch:  # vendor-library yardstick (plain GEMM, no epilogue) -- not used by the product
             import torch.nn.functional as F
@@ -139,7 +142,7 @@ def main():
     for key in combos():
         if all((n, *key) in total_us for n in counts):
             t = sum(total_us[(n, *key)] * c for n, c in counts.items())
-            print(f"GEMM time per M forward (kernel, streams, exact_gelu, unused, spec, kloop = {key}): {t / 1e3:.2f} ms")
+            print(f"GEMM time per M forward (kernel, streams, exact_gelu, ct, spec, kloop = {key}): {t / 1e3:.2f} ms")
 
 
 if __name__ == "__main__":
