@@ -121,12 +121,13 @@ int sdp_gemm_set_kloop_phases(int n);
  * nothing in the reference. */
 int sdp_gemm_set_timeline(void* buf, int slots);
 
-/* Cross-tile bf16 GEMM kernel (gemm_bf16_ct): `tiles` 256 x 256 pair tiles per workgroup (0 = off),
- * `re` row groups per epilogue step (1 or 2), taken by the specialised-epilogue calls with K <= kmax.
- * The two 4-wave groups of a workgroup own different 256 x 128 tiles and run half a tile period
- * apart, so one group's epilogue runs under the other's MFMAs.  Bit-identical to the 8-phase
- * kernel.  Returns the previous tile count, -1 for invalid arguments. */
-int sdp_gemm_set_ct(int tiles, int re, int kmax);
+/* Cross-tile bf16 GEMM kernel (gemm_bf16_ct): `tiles` 256 x 256 pair tiles per workgroup (0 = off,
+ * -1 = one row of pair tiles), `re` row groups per epilogue step (1 or 2), taken by the
+ * specialised-epilogue calls with K <= kmax and N <= nmax.  The two 4-wave groups of a workgroup own
+ * different 128 x 256 tiles and run an epilogue's length apart, so one group's epilogue runs under
+ * the other's MFMAs.  Bit-identical to the 8-phase kernel.  Returns the previous tile count, -2 for
+ * invalid arguments. */
+int sdp_gemm_set_ct(int tiles, int re, int kmax, int nmax);
 int sdp_gemm_timeline_count(void);
 
 /* Timing experiments only, diagnostic library (`make stamps`, -DSDP_DIAG): bit 0 makes sdp_dwconv,

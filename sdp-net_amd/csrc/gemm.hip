@@ -1073,6 +1073,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
   }
 }
 
+#ifdef SDP_DIAG  // measured slower than gemm_bf16_8ph (round 6): diagnostic build only
 // ---------------------------------------------------------------------------
 // Cross-tile kernel (gemm_bf16_ct): the two 4-wave groups of a 512-thread workgroup own DIFFERENT
 // output tiles and run half a tile period apart, so one group's epilogue (GELU / LN fold / residual
@@ -1095,9 +1096,9 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_8ph(const bf16_t* __restri
 // group 0 (as in gemm_bf16_8ph), so one group's load phase lies under the other's MFMA section.  An
 // epilogue step keeps that barrier pattern: its VALU-heavy half (residual loads, staging through LDS
 // with bias / LN fold / activation) lies under the partner's MFMA section, its store half under the
-// partner's load phase.  Group 1 additionally starts half a tile period (S + E steps) late and group
-// 0 pads its end by the same amount, so their epilogues alternate.  Both groups execute the same
-// barrier count (2 + 2 pad + 2 T (S + E)), all control flow is wave-uniform.
+// partner's load phase.  Group 1 additionally starts E steps (one epilogue) late and group 0 pads its
+// end by the same amount, so their epilogues alternate.  Both groups execute the same barrier count
+// (2 + 2 E + 2 T (S + E)), all control flow is wave-uniform.
 //
 // LDS ring slot: [128 X rows][32 bf16] then [256 W rows][32 bf16], 64-B rows; 16-B chunk c of row r
 // stored at c ^ h((r >> 2) & 3), h = {0, 2, 3, 1}: each 16-lane group of a ds_read_b128 fragment
@@ -1141,7 +1142,11 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_ct(const bf16_t* __restric
   const int Tw = min(T, tiles_m * tiles_n - p0);  // >= 1 (host: grid = ceil(pairs / T))
   const int S = K / CBK;                          // K-steps per tile (>= 2)
   const int nsteps = Tw * S;
-  const int padB = (S + E) / 2;
+  // group 1's offset: E steps is the least that puts every epilogue of one group beside K-steps of the
+  // other (group 0's tile-t epilogue beside group 1's last E K-steps of tile t, group 1's beside group
+  // 0's first E K-steps of tile t + 1); a larger offset only lengthens the workgroup's unpaired start
+  // and end
+  const int padB = E;
   auto tile_origin = [&](int p, int& m0, int& n0) {
     int tm, tn;
     tile_coords(p, tiles_m, tiles_n, epi.group_m, tm, tn);
@@ -1393,6 +1398,8 @@ __global__ __launch_bounds__(NTHREADS) void gemm_bf16_ct(const bf16_t* __restric
   }
 }
 
+#endif  // SDP_DIAG (gemm_bf16_ct)
+
 #undef SDP_VMCNT
 
 }  // namespace fast
@@ -1594,16 +1601,22 @@ extern "C" int sdp_gemm_set_store_policy(int nt) {
 #endif
 }
 
-// Cross-tile kernel (gemm_bf16_ct): pair tiles per workgroup (0 = off: gemm_bf16_8ph everywhere)
-// and row groups per epilogue step (1 or 2); applied to the specialised-epilogue calls with
-// K <= g_ct_kmax.
-static int g_ct_tiles = 0, g_ct_re = 2, g_ct_kmax = 1024;
-extern "C" int sdp_gemm_set_ct(int tiles, int re, int kmax) {
+// Cross-tile kernel (gemm_bf16_ct): pair tiles per workgroup (0 = off: gemm_bf16_8ph everywhere;
+// -1 = one whole row of pair tiles, i.e. tiles_n) and row groups per epilogue step (1 or 2); applied
+// to the specialised-epilogue calls with K <= g_ct_kmax and N <= g_ct_nmax.
+static int g_ct_tiles = 0, g_ct_re = 2, g_ct_kmax = 1024, g_ct_nmax = 1 << 30;
+extern "C" int sdp_gemm_set_ct(int tiles, int re, int kmax, int nmax) {
   const int old = g_ct_tiles;
-  if (tiles < 0 || tiles > 64 || (re != 1 && re != 2) || kmax < 64) return -1;
+#ifndef SDP_DIAG
+  // the product library does not contain the cross-tile kernel (profiles/r06_ct_gemm.md): only "off"
+  (void)re, (void)kmax, (void)nmax;
+  return tiles == 0 ? old : -2;
+#endif
+  if (tiles < -1 || tiles > 64 || (re != 1 && re != 2) || kmax < 64 || nmax < 8) return -2;
   g_ct_tiles = tiles;
   g_ct_re = re;
   g_ct_kmax = kmax;
+  g_ct_nmax = nmax;
   return old;
 }
 
@@ -1783,17 +1796,19 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
       const bool spec = g_epi_spec && fk == 14 && small && !e.nt_store && (ak == ACT_NONE || ak == ACT_GELU) &&
                         (fl == 0 || fl == fast::EF_BIAS || fl == (fast::EF_BIAS | fast::EF_LN) ||
                          fl == (fast::EF_RESID | fast::EF_PART) || fl == (fast::EF_BIAS | fast::EF_RESID | fast::EF_PART));
-      if (spec && g_ct_tiles > 0 && K <= g_ct_kmax) {
+#ifdef SDP_DIAG
+      if (spec && g_ct_tiles != 0 && K <= g_ct_kmax && N <= g_ct_nmax) {
         const int pairs = tm * tn;
-        const int grid = (pairs + g_ct_tiles - 1) / g_ct_tiles;
+        const int ctt = g_ct_tiles > 0 ? g_ct_tiles : tn;
+        const int grid = (pairs + ctt - 1) / ctt;
 #define SDP_CT(A, F)                                                                                              \
   do {                                                                                                            \
     if (g_ct_re == 2)                                                                                             \
       hipLaunchKernelGGL((fast::gemm_bf16_ct<A, F, 2>), dim3(grid), dim3(fast::NTHREADS), 0, s, (const bf16_t*)X, \
-                         ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, g_ct_tiles);                        \
+                         ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, ctt);                               \
     else                                                                                                          \
       hipLaunchKernelGGL((fast::gemm_bf16_ct<A, F, 1>), dim3(grid), dim3(fast::NTHREADS), 0, s, (const bf16_t*)X, \
-                         ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, g_ct_tiles);                        \
+                         ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn, ctt);                               \
   } while (0)
 #define SDP_CT_FL(A)                                                            \
   do {                                                                          \
@@ -1807,7 +1822,9 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
         else SDP_CT_FL(ACT_GELU);
 #undef SDP_CT_FL
 #undef SDP_CT
-      } else if (spec) {
+      } else
+#endif
+      if (spec) {
 #define SDP_8PH_FL(A)                                                           \
   do {                                                                          \
     if (fl == (fast::EF_BIAS | fast::EF_LN)) SDP_8PH(A, 16 + 3);                \

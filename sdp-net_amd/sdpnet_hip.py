@@ -41,7 +41,7 @@ _SIGS = {
     "sdp_gemm_set_store_policy": ([_i32], _i32),
     "sdp_gemm_set_epi_spec": ([_i32], _i32),
     "sdp_gemm_set_kloop_phases": ([_i32], _i32),
-    "sdp_gemm_set_ct": ([_i32, _i32, _i32], _i32),
+    "sdp_gemm_set_ct": ([_i32, _i32, _i32, _i32], _i32),
     "sdp_gemm_set_timeline": ([_vp, _i32], _i32),
     "sdp_gemm_timeline_count": ([], _i32),
     "sdp_debug_skip": ([_i32], _i32),
@@ -185,10 +185,10 @@ def lib():
         knob("SDPNET_GEMM_NT_STORE", L.sdp_gemm_set_store_policy, "GEMM store policy")
         knob("SDPNET_GEMM_EPI_SPEC", L.sdp_gemm_set_epi_spec, "GEMM epilogue specialisation")
         knob("SDPNET_GEMM_KLOOP_PHASES", L.sdp_gemm_set_kloop_phases, "GEMM k-loop phases")
-        v = os.environ.get("SDPNET_GEMM_CT")  # cross-tile GEMM: "tiles[,re[,kmax]]"
+        v = os.environ.get("SDPNET_GEMM_CT")  # cross-tile GEMM: "tiles[,re[,kmax[,nmax]]]"
         if v:
-            a = [int(u) for u in v.split(",")] + [2, 1024][len(v.split(",")) - 1:]
-            if L.sdp_gemm_set_ct(a[0], a[1], a[2]) < 0:
+            a = [int(u) for u in v.split(",")] + [2, 1024, 1 << 30][len(v.split(",")) - 1:]
+            if L.sdp_gemm_set_ct(a[0], a[1], a[2], a[3]) < -1:
                 raise RuntimeError(f"SDPNET_GEMM_CT={v}: invalid cross-tile setting")
         kern = os.environ.get("SDPNET_DEBUG_SKIP")  # timing experiments, diagnostic library only
         if kern and int(kern) and L.sdp_debug_skip(int(kern)) < 0:

@@ -721,7 +721,7 @@ def test_gemm_two_streams_and_graph_replay():
 
 
 # ------------------------------------------------- cross-tile GEMM (gemm_bf16_ct)
-@pytest.mark.parametrize("tiles,re", [(1, 2), (2, 2), (3, 1), (4, 2), (5, 1)])
+@pytest.mark.parametrize("tiles,re", [(1, 2), (2, 2), (3, 1), (4, 2), (5, 1), (-1, 2)])
 @pytest.mark.parametrize("combo", ["ln_bias", "resid_part", "bias_resid_part", "plain", "bias"])
 @pytest.mark.parametrize("M,N,K,act", [(25088, 768, 768, 1), (1003, 3072, 768, 1), (300, 2304, 768, 0),
                                        (513, 320, 128, 1), (4000, 768, 3072, 0), (777, 1000, 64, 1)])
@@ -730,6 +730,8 @@ def test_gemm_cross_tile_bit_identical(tiles, re, combo, M, N, K, act):
     ring each) runs gemm_bf16_8ph's MFMAs in the same per-accumulator order and its epilogue
     arithmetic: outputs and LN partials are bit-identical -- row-mapped token buffer, in-place
     residual, ragged M / N, runs of 1..5 pair tiles per workgroup (ragged last run)."""
+    if not DIAG:
+        pytest.skip("gemm_bf16_ct (measured slower, round 6) is compiled only into the diagnostic library")
     if N % 8:
         pytest.skip("whole-line epilogue needs N % 8 == 0")
     B_, R = 2, 3
@@ -753,8 +755,8 @@ def test_gemm_cross_tile_bit_identical(tiles, re, combo, M, N, K, act):
         ln = (st, colsum)
     outs = []
     for ct in (0, tiles):
-        old = sp.lib().sdp_gemm_set_ct(ct, re, 4096)
-        assert old >= 0
+        old = sp.lib().sdp_gemm_set_ct(ct, re, 4096, 1 << 30)
+        assert old >= -1
         try:
             tok = tok0.clone()
             img = sp.Rows(tok, N, P, Nt, R)
@@ -763,7 +765,7 @@ def test_gemm_cross_tile_bit_identical(tiles, re, combo, M, N, K, act):
             torch.cuda.synchronize()
             outs.append((tok, part))
         finally:
-            sp.lib().sdp_gemm_set_ct(old, 2, 1024)
+            sp.lib().sdp_gemm_set_ct(old, 2, 1024, 1 << 30)
     assert torch.equal(outs[0][0], outs[1][0]), "cross-tile output differs from gemm_bf16_8ph"
     if outs[0][1] is not None:  # (register rows stay NaN in both)
         p0, p1 = outs[0][1], outs[1][1]

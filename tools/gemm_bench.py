@@ -80,7 +80,7 @@ def main():
             sp.lib().sdp_gemm_set_fast_kernel(int(kern))
             sp.lib().sdp_gemm_set_exact_gelu(dsy)
             ct_t, ct_re, ct_k = (sch.split(":") + ["2", "1024"][len(sch.split(":")) - 1:])[:3]
-            assert sp.lib().sdp_gemm_set_ct(int(ct_t), int(ct_re), int(ct_k)) >= 0
+            assert sp.lib().sdp_gemm_set_ct(int(ct_t), int(ct_re), int(ct_k), 1 << 30) >= -1
             streams = [torch.cuda.Stream() for _ in range(ns)]
             parts = []
             step = (M + ns - 1) // ns
