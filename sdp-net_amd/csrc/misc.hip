@@ -73,6 +73,48 @@ __global__ __launch_bounds__(256) void patchify_rows_k(const TI* __restrict__ im
   }
 }
 
+// One workgroup per patch-row strip (b, ph): the strip's 3 x p image rows are read as pixel pairs in
+// image order (coalesced rows of Wp p pixels per channel), each pair lands in one patch row (p even),
+// and the Kpad - 3 p p padding columns of the strip's Wp patch rows are zeroed.  The per-patch-row
+// kernel above walked each patch's p-pixel segments in its own workgroup, so the image lines shared by
+// neighbouring patches were fetched once per patch (XL, p = 14: 2.4x the algorithmic bytes).
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void patchify_strip_k(const TI* __restrict__ img, TO* __restrict__ out, int Hi,
+                                                        int Wi, int p, int Hp, int Wp, int Kpad) {
+  const int strip = blockIdx.x;  // b * Hp + ph
+  const int ph = strip % Hp, b = strip / Hp;
+  const int pp = p * p, W2 = Wp * p / 2;  // pixel pairs per image row segment
+  const int n = 3 * p * W2;
+  const TI* base = img + (int64_t)b * 3 * Hi * Wi + (int64_t)(ph * p) * Wi;
+  TO* obase = out + (int64_t)strip * Wp * Kpad;
+  for (int t = threadIdx.x; t < n; t += 256) {
+    const int w2 = t % W2, ci = t / W2, c = ci / p, i = ci - c * p;
+    const int w = 2 * w2, pw = w / p, j = w - pw * p;
+    const TI* src = base + ((int64_t)c * Hi + i) * Wi + w;
+    float v0, v1;
+    if constexpr (sizeof(TI) == 4) {
+      const float2 f = *(const float2*)src;
+      v0 = f.x;
+      v1 = f.y;
+    } else {
+      const uint32_t u = *(const uint32_t*)src;
+      v0 = bf2f((bf16_t)(u & 0xffffu));
+      v1 = bf2f((bf16_t)(u >> 16));
+    }
+    TO* dst = obase + (int64_t)pw * Kpad + c * pp + i * p + j;
+    if constexpr (sizeof(TO) == 2) {
+      *(uint32_t*)dst = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+    } else {
+      *(float2*)dst = float2{v0, v1};
+    }
+  }
+  const int padc = Kpad - 3 * pp;
+  for (int t = threadIdx.x; t < Wp * padc; t += 256) {
+    const int pw = t / padc;
+    obase[(int64_t)pw * Kpad + 3 * pp + (t - pw * padc)] = from_f<TO>(0.f);
+  }
+}
+
 extern "C" int sdp_patchify(int dtype_in, const void* img, int dtype_out, void* out, int B, int Hi, int Wi, int p,
                             int Kpad, void* stream) {
   if (!img || !out || p <= 0 || Kpad < 3 * p * p) return (int)hipErrorInvalidValue;
@@ -81,6 +123,22 @@ extern "C" int sdp_patchify(int dtype_in, const void* img, int dtype_out, void* 
   if (total == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const int64_t rows = (int64_t)B * Hp * Wp;
+  // pixel pairs: p and Wi even, the pairs 4-B (bf16 in) / 8-B (fp32 in) aligned
+  const int ein = dtype_in == 0 ? 4 : 2;
+  if (p % 2 == 0 && Wi % 2 == 0 && Kpad % 2 == 0 && (uintptr_t)img % (2 * ein) == 0 &&
+      (uintptr_t)out % (dtype_out == 0 ? 8 : 4) == 0 && (int64_t)B * Hp < (1ll << 31) &&
+      (int64_t)3 * Hi * Wi < (1ll << 31)) {
+#define SDP_PATCH_STRIP(TI, TO)                                                                                     \
+  hipLaunchKernelGGL((patchify_strip_k<TI, TO>), dim3((unsigned)(B * Hp)), dim3(256), 0, s, (const TI*)img,        \
+                     (TO*)out, Hi, Wi, p, Hp, Wp, Kpad)
+    if (dtype_in == 0 && dtype_out == 1) SDP_PATCH_STRIP(float, bf16_t);
+    else if (dtype_in == 0 && dtype_out == 0) SDP_PATCH_STRIP(float, float);
+    else if (dtype_in == 1 && dtype_out == 1) SDP_PATCH_STRIP(bf16_t, bf16_t);
+    else if (dtype_in == 1 && dtype_out == 0) SDP_PATCH_STRIP(bf16_t, float);
+    else return (int)hipErrorInvalidValue;
+#undef SDP_PATCH_STRIP
+    return SDP_CHECK_LAUNCH();
+  }
   if (rows < (1ll << 31) && (int64_t)3 * Hi * Wi < (1ll << 31)) {
 #define SDP_PATCH_ROWS(TI, TO)                                                                                   \
   hipLaunchKernelGGL((patchify_rows_k<TI, TO>), dim3((unsigned)rows), dim3(256), 0, s, (const TI*)img, (TO*)out, \

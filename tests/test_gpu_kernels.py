@@ -363,15 +363,18 @@ def test_attention_spiky_scores(kern):
 
 
 # ------------------------------------------------------------------ misc kernels
-@pytest.mark.parametrize("p,img", [(16, 224), (14, 224), (8, 64), (16, 112)])
+@pytest.mark.parametrize("p,img", [(16, 224), (14, 224), (8, 64), (16, 112), (16, 230), (7, 70), (14, 226)])
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
-def test_patchify(p, img, dtype):
-    B = 2
-    x = rnd(B, 3, img, img, seed=50)
+@pytest.mark.parametrize("idt", [torch.float32, BF])
+def test_patchify(p, img, dtype, idt):
+    # even p / width: the strip kernel (pixel pairs, coalesced image rows); odd: the per-patch kernel;
+    # widths past Wp * p (230 = 14 * 16 + 6) are dropped as the stride-p conv drops them
+    B = 3
+    x = rnd(B, 3, img, img, seed=50).to(idt)
     kp = (3 * p * p + 63) // 64 * 64
-    out = torch.empty(B * (img // p) ** 2, kp, dtype=dtype, device=DEV)
+    out = torch.full((B * (img // p) ** 2, kp), float("nan"), dtype=dtype, device=DEV)
     sp.patchify(x, out, p, kp)
-    ref = F.unfold(x, p, stride=p).transpose(1, 2).reshape(-1, 3 * p * p)
+    ref = F.unfold(x.float(), p, stride=p).transpose(1, 2).reshape(-1, 3 * p * p)
     close(out[:, : 3 * p * p], ref, dtype, rel=4e-3 if dtype == BF else 0)
     assert (out[:, 3 * p * p:] == 0).all()
 
