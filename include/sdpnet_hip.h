@@ -410,6 +410,19 @@ int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstri
 int sdp_ln_fwd_mixed(int x_dtype, int y_dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
                      float eps, const float* gamma, const float* beta, float* stats, void* Y, int64_t ldy, int y_grp,
                      int64_t y_gstride, int y_off, int M, int C, void* stream);
+
+/* Residual add + LayerNorm forward in one pass (training forward): y = act / dropout(x) * scale[m / sgrp]
+ * + r (sdp_rowscale_add_mixed / sdp_rowscale_add_dropout mode 1 arithmetic; x in x_dtype, r and y in
+ * y_dtype) and a = LN(y) with its (mean, rstd) statistics (sdp_ln_fwd_mixed; a in a_dtype), bit-identical
+ * to the two passes.  hipErrorNotSupported where the one-pass form does not apply (C % 8, C <= 128, C > 2048,
+ * unaligned rows, dropout mode 2).  Replaces the branch add + LayerNorm pairs of layers.py:99-103
+ * (ConvMixer, x + drop_path(act(PW(.))) then layer_norm_2) and :300-306 (EncoderLayer, x +
+ * drop_path(dropout(o_proj(.))) then norm2) in the training step. */
+int sdp_add_ln_fwd(int x_dtype, int y_dtype, int a_dtype, int act, const void* X, int64_t ldx, int x_grp,
+                   int64_t x_gstride, int x_off, const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp,
+                   int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off,
+                   float p, uint64_t seed, int dmode, float eps, const float* gamma, const float* beta, float* stats,
+                   void* A, int64_t lda, int a_grp, int64_t a_gstride, int a_off, int M, int C, void* stream);
 int sdp_ln_bwd_mixed(int x_dtype, int dy_dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
                      const float* stats, const float* gamma, const void* DY, int64_t lddy, int dy_grp,
                      int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,

@@ -1215,6 +1215,130 @@ static int ln_fwd_impl(int xdt, int ydt, const void* X, int64_t ldx, int x_grp, 
   });
 }
 
+// Residual add + LayerNorm forward in one pass (training forward, the branch add that feeds the
+// next LayerNorm inside one sub-layer: ConvMixer's x_ = x + drop_path(act(PW(..))) -> LN2,
+// EncoderLayer's x + drop_path(dropout(o_proj(..))) -> norm2; layers.py:99-103, :300-306):
+//   y = rowscale(act / dropout(x)) * scale[m / sgrp] + r   (sdp_rowscale_add[_mixed / _dropout] mode 1)
+//   a = LN(y) with its (mean, rstd) statistics            (sdp_ln_fwd[_mixed])
+// One wave per row; y is rounded to its dtype before the statistics, so both outputs and the
+// statistics are bit-identical to the two separate passes (which stored y and re-read it).  Saves
+// the re-read of y and one launch per sub-layer.
+template <typename TX, typename TY, typename TA, int V>
+__global__ __launch_bounds__(256) void add_ln_fwd_v8(const TX* __restrict__ X, int64_t ldx, RowMap xm,
+                                                     const float* __restrict__ sc, int sgrp, const TY* __restrict__ R,
+                                                     int64_t ldr, RowMap rm, TY* __restrict__ Y, int64_t ldy,
+                                                     RowMap ym, int act, float p, uint64_t seed, int dmode, float eps,
+                                                     const float* __restrict__ g, const float* __restrict__ b,
+                                                     float* __restrict__ st, TA* __restrict__ A, int64_t lda,
+                                                     RowMap am, int M, int C) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const float inv = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  const float s_ = sc ? sc[m / sgrp] : 1.0f;
+  const TX* xp = X + xm(m) * ldx;
+  const TY* rp = R + rm(m) * ldr;
+  TY* yp = Y + ym(m) * ldy;
+  V8<TY> y[V];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int c = 8 * lane + 512 * i;
+    if (c < C) {
+      V8<TX> x;
+      x.load(xp + c);
+      if (act != ACT_NONE) {  // rowscale_v8's arithmetic, step by step
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x.v[q] = to_f<TX>(from_f<TX>(apply_act(act, x.v[q])));
+      }
+      if (dmode == 1) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          x.v[q] = to_f<TX>(from_f<TX>(uniform01(seed, (uint64_t)m * C + c + q) >= p ? x.v[q] * inv : 0.f));
+      }
+      y[i].load(rp + c);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) y[i].v[q] = fmaf(x.v[q], s_, y[i].v[q]);
+      y[i].store(yp + c);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        y[i].v[q] = to_f<TY>(from_f<TY>(y[i].v[q]));  // the stored value, as ln_fwd_v8 would load it
+        s += y[i].v[q];
+      }
+    }
+  }
+  // ln_fwd_v8's statistics and output, same summation order
+  const float mean = wave_sum(s) / (float)C;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int c = 8 * lane + 512 * i;
+    if (c < C) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ss = fmaf(y[i].v[q] - mean, y[i].v[q] - mean, ss);
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)C + eps);
+  if (lane == 0) *(float2*)(st + 2 * m) = float2{mean, rstd};
+  TA* ap = A + am(m) * lda;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int c = 8 * lane + 512 * i;
+    if (c < C) {
+      const f32x4 g0 = *(const f32x4*)(g + c), g1 = *(const f32x4*)(g + c + 4);
+      const f32x4 b0 = *(const f32x4*)(b + c), b1 = *(const f32x4*)(b + c + 4);
+      V8<TA> o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        o.v[q] = (y[i].v[q] - mean) * rstd * (q < 4 ? g0[q] : g1[q - 4]) + (q < 4 ? b0[q] : b1[q - 4]);
+      o.store(ap + c);
+    }
+  }
+}
+
+// C ABI of add_ln_fwd_v8: x in x_dtype; r, y in y_dtype (the residual stream); a in a_dtype (the
+// next GEMM's operand).  hipErrorNotSupported where the one-pass form does not apply (C % 8 != 0,
+// C > 2048, rows not 16-B aligned, dmode 2): the caller then runs the two passes.
+extern "C" int sdp_add_ln_fwd(int x_dtype, int y_dtype, int a_dtype, int act, const void* X, int64_t ldx, int x_grp,
+                              int64_t x_gstride, int x_off, const float* scale, int sgrp, const void* R, int64_t ldr,
+                              int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
+                              int64_t y_gstride, int y_off, float p, uint64_t seed, int dmode, float eps,
+                              const float* gamma, const float* beta, float* stats, void* A, int64_t lda, int a_grp,
+                              int64_t a_gstride, int a_off, int M, int C, void* stream) {
+  if (!X || !R || !Y || !A || !stats || !gamma || !beta || M < 0 || C <= 0 || (scale && sgrp <= 0) || act < 0 ||
+      act > ACT_KELU || p < 0.f || p >= 1.f || dmode < 0 || dmode > 2)
+    return (int)hipErrorInvalidValue;
+  if (p == 0.f) dmode = 0;
+  // (C <= 128: sdp_ln_fwd takes the several-rows-per-wave kernel, whose sums run in another order)
+  if (dmode == 2 || C % 8 || C <= 128 || C > 2048 || ldx % 8 || ldr % 8 || ldy % 8 || lda % 8 || (uintptr_t)X % 16 ||
+      (uintptr_t)R % 16 || (uintptr_t)Y % 16 || (uintptr_t)A % 16 || (uintptr_t)gamma % 16 || (uintptr_t)beta % 16 ||
+      (uintptr_t)stats % 8)
+    return (int)hipErrorNotSupported;
+  if ((x_dtype != 0 && x_dtype != 1) || (y_dtype != 0 && y_dtype != 1) || (a_dtype != 0 && a_dtype != 1))
+    return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), rm = mk_tmap(r_grp, r_gstride, r_off),
+               ym = mk_tmap(y_grp, y_gstride, y_off), am = mk_tmap(a_grp, a_gstride, a_off);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((M + 3) / 4);
+  const int v8 = (C + 511) / 512;
+  auto launch = [&](auto tx, auto ty, auto ta) {
+    using TX = typename decltype(tx)::type;
+    using TY = typename decltype(ty)::type;
+    using TA = typename decltype(ta)::type;
+#define SDP_ALN(VV)                                                                                               \
+  hipLaunchKernelGGL((add_ln_fwd_v8<TX, TY, TA, VV>), grid, dim3(256), 0, s, (const TX*)X, ldx, xm, scale, sgrp, \
+                     (const TY*)R, ldr, rm, (TY*)Y, ldy, ym, act, p, seed, dmode, eps, gamma, beta, stats, (TA*)A,  \
+                     lda, am, M, C)
+    if (v8 <= 1) SDP_ALN(1); else if (v8 <= 2) SDP_ALN(2); else SDP_ALN(4);
+#undef SDP_ALN
+    return SDP_CHECK_LAUNCH();
+  };
+  return by_dtypes(x_dtype, y_dtype, [&](auto tx, auto ty) {
+    return a_dtype == 1 ? launch(tx, ty, DTag<bf16_t>{}) : launch(tx, ty, DTag<float>{});
+  });
+}
+
 extern "C" int sdp_ln_fwd(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off, float eps,
                           const float* gamma, const float* beta, float* stats, void* Y, int64_t ldy, int y_grp,
                           int64_t y_gstride, int y_off, int M, int C, void* stream) {

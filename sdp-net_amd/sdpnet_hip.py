@@ -99,6 +99,8 @@ _SIGS = {
                                   *_ROWMAP, _i32, _i32, _f32, _u64, _i32, _vp], _i32),
     "sdp_ln_fwd_mixed": ([_i32, _i32, _vp, _i64, *_ROWMAP, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp],
                          _i32),
+    "sdp_add_ln_fwd": ([_i32, _i32, _i32, _i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP,
+                        _f32, _u64, _i32, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_ln_bwd_mixed": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _vp,
                           _i64, *_ROWMAP, _i32, _i32, _vp, _vp], _i32),
     "sdp_ln_apply": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
@@ -731,6 +733,26 @@ def rowscale_add(x: Rows, y: Rows, M: int, N: int, scale: Optional[torch.Tensor]
         rc = lib().sdp_rowscale_add(dcode(x.t.dtype), *x.args(), _ptr(scale), sgrp, *_rows_args(resid), *y.args(), M,
                                     N, _stream(y.t))
     _check(rc, "rowscale_add")
+
+
+def add_ln_fwd(x: Rows, y: Rows, a: Rows, M: int, C: int, resid: Rows, eps: float, gamma: torch.Tensor,
+               beta: torch.Tensor, stats: torch.Tensor, scale: Optional[torch.Tensor] = None, sgrp: int = 1,
+               act: int = 0, p: float = 0.0, seed: int = 0, dmode: int = 0) -> bool:
+    """y = act / dropout(x) * scale[m / sgrp] + resid and a = LN(y) (+ its statistics) in one pass
+    (sdp_add_ln_fwd; bit-identical to rowscale_add followed by ln_fwd).  False where the one-pass form
+    does not apply (the caller runs the two passes)."""
+    _need_cuda(x.t, y.t, a.t, resid.t, gamma, beta, stats, scale)
+    _req(resid.t.dtype == y.t.dtype, "add_ln_fwd: resid dtype = y dtype")
+    _req(stats.dtype == gamma.dtype == beta.dtype == torch.float32, "add_ln_fwd fp32 params")
+    _req(scale is None or scale.dtype == torch.float32, "add_ln_fwd scale fp32")
+    rc = lib().sdp_add_ln_fwd(dcode(x.t.dtype), dcode(y.t.dtype), dcode(a.t.dtype), int(act), *x.args(), _ptr(scale),
+                              sgrp, *resid.args(), *y.args(), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(dmode),
+                              float(eps), gamma.data_ptr(), beta.data_ptr(), stats.data_ptr(), *a.args(), M, C,
+                              _stream(y.t))
+    if rc == _HIP_NOT_SUPPORTED:
+        return False
+    _check(rc, "add_ln_fwd")
+    return True
 
 
 def ln_apply(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, y: Rows, M: int, C: int):

@@ -403,6 +403,23 @@ def _with_regs(src: torch.Tensor, B: int, R: int, N: int, C: int) -> torch.Tenso
     return out
 
 
+def _add_ln_fwd(x: Rows, y: Rows, M: int, C: int, resid: Rows, g: torch.Tensor, b: torch.Tensor, eps: float, dt,
+                scale=None, sgrp: int = 1, act: int = 0, p: float = 0.0, seed: int = 0, dmode: int = 0):
+    """y = act / dropout(x) * scale + resid (the branch add), then (a, stats) = LN(y): one pass
+    (sp.add_ln_fwd) where it applies, else rowscale_add + _ln_fwd (bit-identical either way)."""
+    st = _empty((M, 2), torch.float32, x.t.device)
+    a = _empty((M, C), dt, x.t.device)
+    if _ADD_LN and sp.add_ln_fwd(x, y, _dense(a), M, C, resid, eps, g, b, st, scale=scale, sgrp=sgrp, act=act, p=p,
+                                 seed=seed, dmode=dmode):
+        return a, st
+    sp.rowscale_add(x, y, M, C, scale=scale, sgrp=sgrp, resid=resid, act=act, p=p, seed=seed, dmode=dmode)
+    return _ln_fwd(y, M, C, g, b, eps, dt)
+
+
+# SDPNET_TRAIN_ADD_LN=0: the branch add and the next LayerNorm as two passes (A/B switch)
+_ADD_LN = os.environ.get("SDPNET_TRAIN_ADD_LN", "1") != "0"
+
+
 def _ln_fwd(x: Rows, M: int, C: int, g: torch.Tensor, b: torch.Tensor, eps: float, dt):
     st = _empty((M, 2), torch.float32, x.t.device)
     a = _empty((M, C), dt, x.t.device)
@@ -454,9 +471,10 @@ class _MixerFn(torch.autograd.Function):
         z1 = _linear(d, W_["ccw"], W_["ccb"], dt)
         mid = _with_regs(tok, B, R, N, C)
         imid = Rows(mid, C, P, N, R)
-        sp.rowscale_add(_dense(z1), imid, M, C, scale=dp2, sgrp=P, resid=img, act=act)   # act + drop path + residual
+        # act + drop path + residual, then LN2 of the sum (one pass)
         # x = drop_path_1(PW_down(act(PW_up(LN2 x_)))) + x_
-        a2, s2 = _ln_fwd(imid, M, C, W_["g2"], W_["b2"], m.layer_norm_2.eps, dt)
+        a2, s2 = _add_ln_fwd(_dense(z1), imid, M, C, img, W_["g2"], W_["b2"], m.layer_norm_2.eps, dt, scale=dp2, sgrp=P,
+                             act=act)
         z2, h = _linear_act(a2, W_["upw"], W_["upb"], dt, act)
         out = _with_regs(mid, B, R, N, C)
         if dp1 is None and tok.dtype == dt:  # residual add in the GEMM epilogue, straight into the token rows
@@ -624,11 +642,11 @@ class _EncoderFn(torch.autograd.Function):
         t2 = _empty((T, C), tok.dtype, dev)                               # stream dtype
         if not _DMODE and p_ff > 0:
             sp.act_fwd(zo, zo, T, C, 0, p_ff, seeds[1])
-        sp.rowscale_add(_dense(zo), _dense(t2), T, C, scale=dp1, sgrp=N, resid=_dense(tok), p=p_ff, seed=seeds[1],
-                        dmode=_DMODE)                                     # dropout + drop path + residual
-        del zo
+        # dropout + drop path + residual, then LN2 of the sum (one pass)
         # x = x + drop_path2(dropout(ff2(dropout(act(ff1(LN2 x))))))   (:306-309)
-        a2, s2 = _ln_fwd(_dense(t2), T, C, W_["n2g"], W_["n2b"], e.norm2.eps, dt)
+        a2, s2 = _add_ln_fwd(_dense(zo), _dense(t2), T, C, _dense(tok), W_["n2g"], W_["n2b"], e.norm2.eps, dt,
+                             scale=dp1, sgrp=N, p=p_ff, seed=seeds[1], dmode=_DMODE)
+        del zo
         z1, h = _linear_act(a2, W_["w1"], W_["b1"], dt, act, p_ff, seeds[2])
         z2 = _linear(h, W_["w2"], W_["b2"], dt)
         out = _empty((T, C), tok.dtype, dev)

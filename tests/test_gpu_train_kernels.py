@@ -605,3 +605,43 @@ def test_gemm_train_epilogues_bit_identical_to_separate_kernels(act, p, M, N, K)
     # shapes the fast kernel does not take are refused without a launch
     assert not sp.gemm_train_epi(1, x[:100].contiguous(), w, z[:100].contiguous(), 100, N, K, bias=b,
                                  y2=h[:100].contiguous(), act=code)
+
+
+@pytest.mark.parametrize("xdt,ydt,adt", [(BF, torch.float32, BF), (BF, BF, BF), (torch.float32, torch.float32,
+                                                                            torch.float32)])
+@pytest.mark.parametrize("act,p", [(0, 0.0), (1, 0.0), (0, 0.2)])
+@pytest.mark.parametrize("C", [768, 96, 1032])
+def test_add_ln_fwd_one_pass_is_bit_identical(xdt, ydt, adt, act, p, C):
+    """sdp_add_ln_fwd (the branch add x + drop_path(act / dropout(z)) and the next LayerNorm in one
+    pass) stores the same sum, the same statistics and the same normalised rows as
+    sdp_rowscale_add[_mixed / _dropout] followed by sdp_ln_fwd[_mixed] -- on the token buffer's image
+    rows (row maps), with a drop-path scale per image, every dtype mix the training step uses."""
+    if p > 0 and act:
+        pytest.skip("the dropout branch carries no activation (EncoderLayer o_proj)")
+    B, R, P = 3, 4, 49
+    N = R + P
+    M = B * P
+    z = rnd(M, C, seed=71, dtype=xdt)
+    tok = rnd(B * N, C, seed=72, dtype=ydt, scale=2.0) + 0.5
+    g, b = rnd(C, seed=73) * 0.2 + 1, rnd(C, seed=74) * 0.2
+    scale = torch.tensor([1.25, 0.0, 1.25], device=DEV)
+    outs = []
+    for fused in (False, True):
+        y = torch.full((B * N, C), float("nan"), dtype=ydt, device=DEV)
+        a = torch.full((M, C), float("nan"), dtype=adt, device=DEV)
+        st = torch.full((M, 2), float("nan"), device=DEV)
+        img, res = sp.Rows(y, C, P, N, R), sp.Rows(tok, C, P, N, R)
+        kw = dict(scale=scale, sgrp=P, act=act, p=p, seed=1234, dmode=1 if p > 0 else 0)
+        if fused and sp.add_ln_fwd(sp.dense(z), img, sp.dense(a), M, C, res, 1e-5, g, b, st, **kw):
+            assert C > 128
+        else:
+            assert not fused or C <= 128  # short rows: the two passes (ln_fwd's several-rows-per-wave kernel)
+            sp.rowscale_add(sp.dense(z), img, M, C, resid=res, **kw)
+            sp.ln_fwd(img, 1e-5, g, b, st, sp.dense(a), M, C)
+        torch.cuda.synchronize()
+        outs.append((y.view(B, N, C)[:, R:], a, st))
+    for u, v in zip(outs[0], outs[1]):
+        assert torch.equal(u, v)
+    # against plain torch: LN of the stored sum
+    ys = outs[1][0].reshape(M, C).float()
+    close(outs[1][1], F.layer_norm(ys, (C,), g, b, 1e-5), 1e-2 if adt == BF else 1e-5, what="add_ln_fwd LN")
