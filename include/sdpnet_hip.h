@@ -20,8 +20,10 @@
  *     (grp = P, gstride = R+P, off = R) without gather/scatter copies.
  *   - Activation codes: 0 none, 1 gelu, 2 relu, 3 tanh, 4 sigmoid,
  *     5 leaky_relu (0.01), 6 selu, 7 kelu (model.py:13-24,
- *     training_utilities.py:91-92).  GELU is the exact erf form everywhere except
- *     the bf16 fast-GEMM epilogue, which uses the tanh form
+ *     training_utilities.py:91-92).  GELU is the erf form x * Phi(x) everywhere except
+ *     the bf16 fast-GEMM epilogue (Phi through erfc by Abramowitz & Stegun 7.1.26: |diff|
+ *     <= 4.2e-7 against double-precision erf, below the 4.5e-7 of the fp32 formula with
+ *     erff), which uses the tanh form which uses the tanh form
  *     x * sigmoid(sqrt(2/pi) (x + 0.044715 x^3)) (|diff| <= 4.7e-4, about one bf16
  *     rounding of the output; a DECLARED deviation from nn.GELU(), model.py:15) unless
  *     sdp_gemm_set_exact_gelu(1) is set.
@@ -147,7 +149,7 @@ int sdp_build_info(void);
 int sdp_gemm_set_group_m(int gm);
 
 /* GELU form of the bf16 fast-GEMM epilogue: 0 = tanh form (default, one v_exp + one
- * v_rcp per element), 1 = exact erf (nn.GELU(), model.py:15; runtime-activation epilogue).
+ * v_rcp per element), 1 = erf form (nn.GELU(), model.py:15; runtime-activation epilogue).
  * Used to bound the tanh form's share of the bf16 logits error.  Returns the previous value. */
 int sdp_gemm_set_exact_gelu(int on);
 
@@ -358,7 +360,7 @@ int sdp_seg_colsum(int dtype, const void* X, int64_t ldx, int G, int len, int64_
                    float* out, int64_t ldo, float scale, int accum, void* stream);
 
 /* Y = act(Z) with dropout p (keep iff hash(seed, m * N + n) >= p, kept values / (1 - p));
- * backward DZ = DY * mask / (1 - p) * act'(Z).  Exact-erf GELU.  p = 0: no mask.
+ * backward DZ = DY * mask / (1 - p) * act'(Z).  Erf-form GELU.  p = 0: no mask.
  * (layers.py:83-88 activation, :308 FFN dropouts, :445-454 head dropout.) */
 int sdp_act_fwd(int dtype, const void* Z, int64_t ldz, void* Y, int64_t ldy, int M, int N, int act, float p,
                 uint64_t seed, void* stream);

@@ -38,7 +38,7 @@ enum SdpAct {
 // = x / (1 + exp2(x (k + k2 x^2))), one v_exp_f32 + one v_rcp_f32 per element.
 // Max |err| vs the exact erf GELU (nn.GELU(), layers.py:88) is 4.7e-4 absolute /
 // 0.22 % relative (|y| > 0.05), i.e. at most one bf16 rounding of the output,
-// which the bf16 path applies anyway.  The generic path keeps libm erff.
+// which the bf16 path applies anyway.  The generic path keeps the erf form (gelu_erf below).
 // gelu_fast (scalar) and gelu_fast2 (packed) perform the same fused operations in
 // the same order, so every epilogue path gives bit-identical results.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -57,9 +57,39 @@ SDP_DEV f32x2 gelu_fast2(f32x2 x) {
   return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
 }
 
+// Phi(x) = P(N(0,1) <= x) and e = exp(-x^2 / 2), branch-free: erfc(|x| / sqrt 2) by Abramowitz &
+// Stegun 7.1.26 (t = 1 / (1 + p z), erfc(z) = t (a1 + .. + a5 t^4) exp(-z^2), |error| <= 1.5e-7),
+// sharing its exp(-z^2) with GELU's derivative.  Measured over [-12, 12] against double-precision
+// erf: |d Phi| <= 3.0e-7, |d gelu| <= 4.2e-7, |d gelu'| <= 3.0e-7 -- the fp32 formula
+// 0.5 x (1 + erff(x / sqrt 2)) is itself off by up to 4.5e-7.  2 transcendental + 12 VALU per
+// element, against ~35 (two erff branches + a full-range expf) before.  Every product / sum is
+// an explicit mul or fma, so no path can contract it differently (all kernels agree bit for bit).
+SDP_DEV float norm_cdf(float x, float& e) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float y = fmaf(t, 1.061405429f, -1.453152027f);
+  y = fmaf(t, y, 1.421413741f);
+  y = fmaf(t, y, -0.284496736f);
+  y = fmaf(t, y, 0.254829592f);
+  y = y * t;
+  const float x2 = x * x;
+  e = __builtin_amdgcn_exp2f(x2 * -0.72134752044448170f);  // exp(-x^2 / 2)
+  const float h = y * e;                                     // erfc(|x| / sqrt 2)
+  return x >= 0.f ? fmaf(-0.5f, h, 1.0f) : 0.5f * h;
+}
+SDP_DEV float gelu_erf(float x) {
+  float e;
+  return x * norm_cdf(x, e);
+}
+SDP_DEV float gelu_erf_grad(float x) {  // Phi(x) + x phi(x)
+  float e;
+  const float cdf = norm_cdf(x, e);
+  return fmaf(x * e, 0.39894228040143268f, cdf);
+}
+
 SDP_DEV float apply_act(int act, float x) {
   switch (act) {
-    case ACT_GELU: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));  // exact erf GELU
+    case ACT_GELU: return gelu_erf(x);  // erf GELU (nn.GELU())
     case ACT_RELU: return fmaxf(x, 0.0f);
     case ACT_TANH: return tanhf(x);
     case ACT_SIGMOID: return 1.0f / (1.0f + expf(-x));
@@ -94,13 +124,20 @@ SDP_DEV float uniform01(uint64_t seed, uint64_t idx) {
   return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 
-// act'(x) of apply_act (training backward; exact-erf GELU).
+// uniform01(seed, idx) >= p in two parts, for runs of consecutive indices: drop_key depends only on
+// the upper 32 index bits (shared by any 8-aligned run of 8), drop_keep is one mix32 per element.
+// Bit-identical to the uniform01 test: (h >> 8) * 2^-24 >= p  <=>  h >= ceil(p * 2^24) << 8 (both
+// sides exact in fp32; p < 1 keeps the threshold below 2^32).
+SDP_DEV uint32_t drop_key(uint64_t seed, uint64_t idx) {
+  return mix32((uint32_t)seed ^ mix32((uint32_t)(idx >> 32) + (uint32_t)(seed >> 32) * 0x9e3779b9U));
+}
+SDP_DEV uint32_t drop_thresh(float p) { return (uint32_t)ceilf(p * 16777216.0f) << 8; }
+SDP_DEV bool drop_keep(uint32_t key, uint32_t idx_lo, uint32_t thr) { return mix32(idx_lo ^ key) >= thr; }
+
+// act'(x) of apply_act (training backward; erf-form GELU).
 SDP_DEV float act_grad(int act, float x) {
   switch (act) {
-    case ACT_GELU: {
-      const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-      return cdf + x * 0.3989422804014327f * expf(-0.5f * x * x);
-    }
+    case ACT_GELU: return gelu_erf_grad(x);
     case ACT_RELU: return x > 0.0f ? 1.0f : 0.0f;
     case ACT_TANH: { const float t = tanhf(x); return 1.0f - t * t; }
     case ACT_SIGMOID: { const float s = 1.0f / (1.0f + expf(-x)); return s * (1.0f - s); }

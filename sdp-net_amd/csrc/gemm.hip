@@ -437,10 +437,11 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
       const int m = mb + j * 16 + 8 * q;
       if constexpr (TRN == 2) {  // dz = dropout(bf16 dh) * act'(z): sdp_act_bwd's arithmetic on the stored dh
         const float inv = epi.p2 > 0.f ? 1.0f / (1.0f - epi.p2) : 1.0f;
+        const uint32_t thr = drop_thresh(epi.p2), key = drop_key(epi.seed2, (uint64_t)m * N + col);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float d = bf2f((bf16_t)o[e]);
-          if (epi.p2 > 0.f) d = uniform01(epi.seed2, (uint64_t)m * N + col + e) >= epi.p2 ? d * inv : 0.f;
+          if (epi.p2 > 0.f) d = drop_keep(key, (uint32_t)((uint64_t)m * N + col) + e, thr) ? d * inv : 0.f;
           const int a2 = ACT >= 0 ? ACT : epi.act2;
           o[e] = (short)f2bf(a2 == ACT_NONE ? d : d * act_grad(a2, bf2f((bf16_t)rr[q][e])));
         }
@@ -460,11 +461,12 @@ SDP_DEV void tile_epilogue_rows(const Epi<bf16_t>& epi, f32x4 (&acc)[4][8], int 
       }
       if constexpr (TRN == 1) {  // h = dropout(act(z)) from the stored z: sdp_act_fwd's arithmetic
         const float inv = epi.p2 > 0.f ? 1.0f / (1.0f - epi.p2) : 1.0f;
+        const uint32_t thr = drop_thresh(epi.p2), key = drop_key(epi.seed2, (uint64_t)m * N + col);
         bf16x8 h;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float v = apply_act(ACT >= 0 ? ACT : epi.act2, bf2f((bf16_t)o[e]));
-          if (epi.p2 > 0.f) v = uniform01(epi.seed2, (uint64_t)m * N + col + e) >= epi.p2 ? v * inv : 0.f;
+          if (epi.p2 > 0.f) v = drop_keep(key, (uint32_t)((uint64_t)m * N + col) + e, thr) ? v * inv : 0.f;
           h[e] = (short)f2bf(v);
         }
         if (m < M && col_ok) *(bf16x8*)(epi.out2 + (uint64_t)m * (uint64_t)epi.ld2 + col) = h;
@@ -1776,7 +1778,7 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
   hipLaunchKernelGGL((fast::gemm_bf16_8ph<A, E, true>), dim3(tm * tn), dim3(fast::NTHREADS), 0, s,                  \
                      (const bf16_t*)X, ldx, xm, (const bf16_t*)W, ldw, e, M, N, K, tm, tn)
 #endif
-      // exact-erf GELU goes through the runtime-activation epilogue (apply_act)
+      // erf-form GELU goes through the runtime-activation epilogue (apply_act)
       const int ak = (act == ACT_GELU && g_exact_gelu) ? -1 : act;
       // the model's epilogue combinations get compile-time flags (tile_epilogue_fl)
       const int fl = (bias ? fast::EF_BIAS : 0) | (ln_stats ? fast::EF_LN : 0) | (R ? fast::EF_RESID : 0) |

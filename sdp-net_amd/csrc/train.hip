@@ -469,7 +469,7 @@ extern "C" int sdp_seg_colsum(int dtype, const void* X, int64_t ldx, int G, int 
 // activation forward / backward with dropout (rows of a [M, N] matrix, row stride ld)
 //   fwd: y = act(z) * (keep ? 1 / (1 - p) : 0)           (p = 0: no mask)
 //   bwd: dz = dy * (keep ? 1 / (1 - p) : 0) * act'(z)
-// keep = uniform01(seed, m * N + n) >= p.  Exact-erf GELU (nn.GELU(), model.py:15).
+// keep = uniform01(seed, m * N + n) >= p.  Erf-form GELU (nn.GELU(), model.py:15; common.h gelu_erf).
 // ---------------------------------------------------------------------------
 
 // 8 consecutive elements of a row per work item (16-B bf16 / 2 x 16-B fp32 accesses); the
@@ -518,47 +518,60 @@ struct Raw8 {
   }
 };
 
-template <typename T>
+// ACT >= 0: the activation fixed at compile time (the model's GELU / ReLU), -1: the run-time code.
+// Work items are indexed in 32 bits (the host takes this form for M * N / 8 < 2^31); the dropout
+// hash keys once per 8-element run (drop_key), one mix32 per element after that.
+template <typename T, int ACT>
 __global__ __launch_bounds__(256) void act_fwd_v8(const T* __restrict__ Z, int64_t ldz, T* __restrict__ Y,
                                                   int64_t ldy, int M, int N, int act, float p, uint64_t seed) {
-  const int n8 = N >> 3;
-  const int64_t total = (int64_t)M * n8;
+  const uint32_t n8 = (uint32_t)N >> 3;
+  const uint32_t total = (uint32_t)M * n8;
   const float inv = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int64_t m = e / n8;
-    const int n = (int)(e - m * n8) * 8;
+  const uint32_t thr = drop_thresh(p);
+  const int a = ACT >= 0 ? ACT : act;
+  for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < total; e += gridDim.x * 256u) {
+    const uint32_t m = e / n8;
+    const uint32_t n = (e - m * n8) * 8u;
     V8<T> x;
-    x.load(Z + m * ldz + n);
+    x.load(Z + (int64_t)m * ldz + n);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      float v = apply_act(act, x.v[q]);
-      if (p > 0.f) v = uniform01(seed, (uint64_t)m * N + n + q) >= p ? v * inv : 0.f;
-      x.v[q] = v;
+    for (int q = 0; q < 8; ++q) x.v[q] = apply_act(a, x.v[q]);
+    if (p > 0.f) {
+      const uint64_t base = (uint64_t)m * (uint32_t)N + n;
+      const uint32_t key = drop_key(seed, base);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x.v[q] = drop_keep(key, (uint32_t)base + q, thr) ? x.v[q] * inv : 0.f;
     }
-    x.store(Y + m * ldy + n);
+    x.store(Y + (int64_t)m * ldy + n);
   }
 }
 
-template <typename T>
+template <typename T, int ACT>
 __global__ __launch_bounds__(256) void act_bwd_v8(const T* __restrict__ Z, int64_t ldz, const T* __restrict__ DY,
                                                   int64_t lddy, T* __restrict__ DZ, int64_t lddz, int M, int N,
                                                   int act, float p, uint64_t seed) {
-  const int n8 = N >> 3;
-  const int64_t total = (int64_t)M * n8;
+  const uint32_t n8 = (uint32_t)N >> 3;
+  const uint32_t total = (uint32_t)M * n8;
   const float inv = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int64_t m = e / n8;
-    const int n = (int)(e - m * n8) * 8;
+  const uint32_t thr = drop_thresh(p);
+  const int a = ACT >= 0 ? ACT : act;
+  for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < total; e += gridDim.x * 256u) {
+    const uint32_t m = e / n8;
+    const uint32_t n = (e - m * n8) * 8u;
     V8<T> z, g;
-    z.load(Z + m * ldz + n);
-    g.load(DY + m * lddy + n);
+    z.load(Z + (int64_t)m * ldz + n);
+    g.load(DY + (int64_t)m * lddy + n);
+    if (p > 0.f) {
+      const uint64_t base = (uint64_t)m * (uint32_t)N + n;
+      const uint32_t key = drop_key(seed, base);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      float d = g.v[q];
-      if (p > 0.f) d = uniform01(seed, (uint64_t)m * N + n + q) >= p ? d * inv : 0.f;
-      g.v[q] = act == ACT_NONE ? d : d * act_grad(act, z.v[q]);
+      for (int q = 0; q < 8; ++q) g.v[q] = drop_keep(key, (uint32_t)base + q, thr) ? g.v[q] * inv : 0.f;
     }
-    g.store(DZ + m * lddz + n);
+    if (a != ACT_NONE) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) g.v[q] *= act_grad(a, z.v[q]);
+    }
+    g.store(DZ + (int64_t)m * lddz + n);
   }
 }
 
@@ -572,6 +585,7 @@ __global__ __launch_bounds__(256) void rowscale_v8(const TX* __restrict__ X, int
   const int n8 = N >> 3;
   const int64_t total = (int64_t)M * n8;
   const float inv = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  const uint32_t thr = drop_thresh(p);
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     const int64_t m = e / n8;
     const int n = (int)(e - m * n8) * 8;
@@ -581,10 +595,12 @@ __global__ __launch_bounds__(256) void rowscale_v8(const TX* __restrict__ X, int
 #pragma unroll
       for (int q = 0; q < 8; ++q) x.v[q] = to_f<TX>(from_f<TX>(apply_act(act, x.v[q])));
     }
+    const uint64_t base = (uint64_t)m * N + n;
+    const uint32_t key = dmode ? drop_key(seed, base) : 0u;
     if (dmode == 1) {  // dropout on the branch (= sdp_act_fwd / sdp_act_bwd with no activation, rounded to TX)
 #pragma unroll
       for (int q = 0; q < 8; ++q)
-        x.v[q] = to_f<TX>(from_f<TX>(uniform01(seed, (uint64_t)m * N + n + q) >= p ? x.v[q] * inv : 0.f));
+        x.v[q] = to_f<TX>(from_f<TX>(drop_keep(key, (uint32_t)base + q, thr) ? x.v[q] * inv : 0.f));
     }
     const float s_ = sc ? sc[m / sgrp] : 1.0f;
     V8<TY> y;
@@ -600,7 +616,7 @@ __global__ __launch_bounds__(256) void rowscale_v8(const TX* __restrict__ X, int
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float r = to_f<TY>(from_f<TY>(y.v[q]));
-        y.v[q] = uniform01(seed, (uint64_t)m * N + n + q) >= p ? r * inv : 0.f;
+        y.v[q] = drop_keep(key, (uint32_t)base + q, thr) ? r * inv : 0.f;
       }
     }
     y.store(Y + ym(m) * ldy + n);
@@ -660,15 +676,21 @@ extern "C" int sdp_act_fwd(int dtype, const void* Z, int64_t ldz, void* Y, int64
   if ((int64_t)M * N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const int es = dtype == 1 ? 2 : 4;
-  if (N % 8 == 0 && ldz % 8 == 0 && ldy % 8 == 0 && (uintptr_t)Z % 16 == 0 && (uintptr_t)Y % 16 == 0 && (es == 2 || es == 4)) {
+  if (N % 8 == 0 && ldz % 8 == 0 && ldy % 8 == 0 && (uintptr_t)Z % 16 == 0 && (uintptr_t)Y % 16 == 0 && (es == 2 || es == 4) &&
+      (int64_t)M * (N / 8) < (1ll << 31)) {
     const int gv = ew_grid((int64_t)M * (N / 8));
-    if (dtype == 1)
-      hipLaunchKernelGGL(act_fwd_v8<bf16_t>, dim3(gv), dim3(256), 0, s, (const bf16_t*)Z, ldz, (bf16_t*)Y, ldy, M, N, act, p, seed);
-    else if (dtype == 0)
-      hipLaunchKernelGGL(act_fwd_v8<float>, dim3(gv), dim3(256), 0, s, (const float*)Z, ldz, (float*)Y, ldy, M, N, act, p, seed);
-    else
-      return (int)hipErrorInvalidValue;
-    return SDP_CHECK_LAUNCH();
+    auto go = [&](auto tag) {
+      using T = typename decltype(tag)::type;
+#define SDP_AF(A) hipLaunchKernelGGL((act_fwd_v8<T, A>), dim3(gv), dim3(256), 0, s, (const T*)Z, ldz, (T*)Y, ldy, M, N, act, p, seed)
+      if (act == ACT_GELU) SDP_AF(ACT_GELU);
+      else if (act == ACT_NONE) SDP_AF(ACT_NONE);
+      else SDP_AF(-1);
+#undef SDP_AF
+      return SDP_CHECK_LAUNCH();
+    };
+    if (dtype == 1) return go(DTag<bf16_t>{});
+    if (dtype == 0) return go(DTag<float>{});
+    return (int)hipErrorInvalidValue;
   }
   const int g = ew_grid((int64_t)M * N);
   if (dtype == 1)
@@ -686,17 +708,22 @@ extern "C" int sdp_act_bwd(int dtype, const void* Z, int64_t ldz, const void* DY
   if ((int64_t)M * N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (N % 8 == 0 && ldz % 8 == 0 && lddy % 8 == 0 && lddz % 8 == 0 && (uintptr_t)Z % 16 == 0 &&
-      (uintptr_t)DY % 16 == 0 && (uintptr_t)DZ % 16 == 0) {
+      (uintptr_t)DY % 16 == 0 && (uintptr_t)DZ % 16 == 0 && (int64_t)M * (N / 8) < (1ll << 31)) {
     const int gv = ew_grid((int64_t)M * (N / 8));
-    if (dtype == 1)
-      hipLaunchKernelGGL(act_bwd_v8<bf16_t>, dim3(gv), dim3(256), 0, s, (const bf16_t*)Z, ldz, (const bf16_t*)DY, lddy,
-                         (bf16_t*)DZ, lddz, M, N, act, p, seed);
-    else if (dtype == 0)
-      hipLaunchKernelGGL(act_bwd_v8<float>, dim3(gv), dim3(256), 0, s, (const float*)Z, ldz, (const float*)DY, lddy,
-                         (float*)DZ, lddz, M, N, act, p, seed);
-    else
-      return (int)hipErrorInvalidValue;
-    return SDP_CHECK_LAUNCH();
+    auto go = [&](auto tag) {
+      using T = typename decltype(tag)::type;
+#define SDP_AB(A)                                                                                                  \
+  hipLaunchKernelGGL((act_bwd_v8<T, A>), dim3(gv), dim3(256), 0, s, (const T*)Z, ldz, (const T*)DY, lddy, (T*)DZ, lddz, \
+                     M, N, act, p, seed)
+      if (act == ACT_GELU) SDP_AB(ACT_GELU);
+      else if (act == ACT_NONE) SDP_AB(ACT_NONE);
+      else SDP_AB(-1);
+#undef SDP_AB
+      return SDP_CHECK_LAUNCH();
+    };
+    if (dtype == 1) return go(DTag<bf16_t>{});
+    if (dtype == 0) return go(DTag<float>{});
+    return (int)hipErrorInvalidValue;
   }
   const int g = ew_grid((int64_t)M * N);
   if (dtype == 1)
@@ -1235,6 +1262,7 @@ __global__ __launch_bounds__(256) void add_ln_fwd_v8(const TX* __restrict__ X, i
   const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
   const float inv = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  const uint32_t thr = drop_thresh(p);
   const float s_ = sc ? sc[m / sgrp] : 1.0f;
   const TX* xp = X + xm(m) * ldx;
   const TY* rp = R + rm(m) * ldr;
@@ -1252,9 +1280,11 @@ __global__ __launch_bounds__(256) void add_ln_fwd_v8(const TX* __restrict__ X, i
         for (int q = 0; q < 8; ++q) x.v[q] = to_f<TX>(from_f<TX>(apply_act(act, x.v[q])));
       }
       if (dmode == 1) {
+        const uint64_t base = (uint64_t)m * C + c;
+        const uint32_t key = drop_key(seed, base);
 #pragma unroll
         for (int q = 0; q < 8; ++q)
-          x.v[q] = to_f<TX>(from_f<TX>(uniform01(seed, (uint64_t)m * C + c + q) >= p ? x.v[q] * inv : 0.f));
+          x.v[q] = to_f<TX>(from_f<TX>(drop_keep(key, (uint32_t)base + q, thr) ? x.v[q] * inv : 0.f));
       }
       y[i].load(rp + c);
 #pragma unroll

@@ -687,10 +687,12 @@ def act_fwd(Z: torch.Tensor, Y: torch.Tensor, M: int, N: int, code: int, p: floa
 
 
 def act_bwd(Z: torch.Tensor, DY: torch.Tensor, DZ: torch.Tensor, M: int, N: int, code: int, p: float = 0.0,
-            seed: int = 0):
+            seed: int = 0, ld: Optional[int] = None):
+    """ld: the row stride of Z, DY and DZ (default N)."""
     _need_cuda(Z, DY, DZ)
     _req(Z.dtype == DY.dtype == DZ.dtype, "act_bwd dtypes")
-    rc = lib().sdp_act_bwd(dcode(Z.dtype), Z.data_ptr(), N, DY.data_ptr(), N, DZ.data_ptr(), N, M, N, code, float(p),
+    ld = ld or N
+    rc = lib().sdp_act_bwd(dcode(Z.dtype), Z.data_ptr(), ld, DY.data_ptr(), ld, DZ.data_ptr(), ld, M, N, code, float(p),
                            int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(DZ))
     _check(rc, "act_bwd")
 

@@ -175,6 +175,26 @@ def test_dropout_mask_consistent():
     assert not torch.equal(y2 != 0, keep)
 
 
+@pytest.mark.parametrize("p", [0.0, 0.3])
+@pytest.mark.parametrize("code", [0, 1, 2])
+def test_act_vector_path_equals_elementwise_path(code, p):
+    """The 8-wide act kernels (compile-time activation, 32-bit items, split dropout hash) against the
+    one-element kernels (uniform01 per element): an odd row stride sends the same rows (same
+    dropout indices m * N + n) down the second path."""
+    M, N = 77, 1024
+    zs = rnd(M, N + 1, seed=41, dtype=BF)
+    dys = rnd(M, N + 1, seed=42, dtype=BF)
+    z, dy = zs[:, :N].contiguous(), dys[:, :N].contiguous()
+    yv, ye = torch.empty(M, N, device=DEV, dtype=BF), torch.zeros(M, N + 1, device=DEV, dtype=BF)
+    sp.act_fwd(z, yv, M, N, code, p=p, seed=99)
+    sp.act_fwd(zs, ye, M, N, code, p=p, seed=99, ldz=N + 1, ldy=N + 1)
+    assert torch.equal(yv, ye[:, :N])
+    dv, de = torch.empty(M, N, device=DEV, dtype=BF), torch.zeros(M, N + 1, device=DEV, dtype=BF)
+    sp.act_bwd(z, dy, dv, M, N, code, p=p, seed=99)
+    sp.act_bwd(zs, dys, de, M, N, code, p=p, seed=99, ld=N + 1)
+    assert torch.equal(dv, de[:, :N])
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, BF])
 @pytest.mark.parametrize("M,C,eps", [(300, 768, 1e-6), (77, 96, 1e-5), (5, 64, 1e-5), (20011, 96, 1e-5),
                                      (333, 128, 1e-5), (70, 32, 1e-5)])

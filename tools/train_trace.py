@@ -2,7 +2,7 @@
 
   rocprofv3 --kernel-trace -d gpurun_out/ttrace -o run --output-format csv -- \\
       python bench.py --config xl_train --steps 3 --warmup 2 --no-cpu-baseline --no-secondary
-  python tools/train_trace.py gpurun_out/ttrace/run_kernel_trace.csv
+  python tools/train_trace.py gpurun_out/ttrace/run_kernel_trace.csv [family [launches.csv]]
 
 Window: between the ends of the last two optimizer launches (adamw_k).  Prints the step's wall
 time, per hardware queue the union of its kernels' intervals (busy) and the kernel families that
@@ -73,6 +73,10 @@ def main(path):
         slow = sorted(((b - a, a, n) for a, b, n in byq[mq] if n == sys.argv[2]), reverse=True)[:12]
         for d, a, n in slow:
             print(f"    {n} {d / 1e3:7.1f} us at +{(a - t0) / 1e6:7.2f} ms, grid {grid.get((a, n), '?')}")
+    if len(sys.argv) > 3:  # every launch of the step window: start (ms from the window), us, queue, kernel, grid
+        with open(sys.argv[3], "w") as f:
+            for a, b, n, q in win:
+                f.write(f"{(a - t0) / 1e6:.4f},{(b - a) / 1e3:.1f},{q},{n},{grid.get((a, n), '?')}\n")
     # concurrency profile
     pts = sorted([(a, 1) for a, b, _, _ in win] + [(b, -1) for a, b, _, _ in win])
     lvl, last, hist = 0, t0, collections.Counter()
