@@ -430,6 +430,27 @@ int sdp_ln_bwd_mixed(int x_dtype, int dy_dtype, const void* X, int64_t ldx, int 
                      int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,
                      int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride, int dx_off, int M, int C,
                      float* part, void* stream);
+/* sdp_ln_bwd_mixed in one launch (training backward), with
+ *  (a) the affine sums finished in the kernel (ticket != NULL): part [sdp_ln_bwd_blocks(M)][2C] and
+ *      gpart [ceil(blocks / 32)][2C] are scratch, aff [2C] receives {dgamma, dbeta}; ticket points
+ *      at ceil(blocks / 32) + 1 zeroed ints, which the kernel leaves zeroed (one buffer per stream).
+ *      Fixed summation order: deterministic, whichever block finishes last.  Opt-in
+ *      (SDPNET_LN_TICKET=1): the device-scope fences it needs across the XCDs' L2s made the XL
+ *      training step ~20 % slower (profiles/r06_ln_bwd_fused_ab.md);
+ *  (b) optionally (O2 != NULL) the gradient of the branch that fed the LayerNorm input, bf16 dense
+ *      rows: O2 = bf16(DX * scale[m / sgrp]); dmode 2: dropout on the rounded value (keep iff
+ *      hash(seed, m * C + c) >= p, kept / (1 - p)); act != 0: O2 = bf16(O2 * act'(Z)), Z bf16 dense
+ *      rows -- bit-identical to sdp_rowscale_add_mixed (+ _dropout mode 2) then sdp_act_bwd on DX.
+ * hipErrorNotSupported where the one-launch form does not apply (C <= 128, C % 8, unaligned rows,
+ * dmode 1): the caller runs sdp_ln_bwd_mixed and the passes.  Replaces, per ConvMixer backward,
+ * LN2 backward + drop_path_2 scale + act' (layers.py:99-103) and, per EncoderLayer backward, norm2
+ * backward + drop_path1 / dropout of the attention branch (:300-306). */
+int sdp_ln_bwd_fused(int x_dtype, int dy_dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
+                     const float* stats, const float* gamma, const void* DY, int64_t lddy, int dy_grp,
+                     int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,
+                     int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride, int dx_off, int M, int C,
+                     float* part, float* gpart, float* aff, int* ticket, const float* scale, int sgrp, const void* Z,
+                     int64_t ldz, int act, float p, uint64_t seed, int dmode, void* O2, int64_t ldo2, void* stream);
 
 /* Attention rows (layers.py:289-298, SDPA dropout_p in training): P = softmax(scale * S[:, :N])
  * (S fp32), Pd = P with dropout p (may be NULL), columns [N, Npad) zeroed; backward

@@ -925,15 +925,90 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ X, int64_t
   }
 }
 
+// What a LayerNorm backward can hand on in the same pass (training, fp32 residual stream): the
+// gradient of the branch that fed the LayerNorm input, in the branch dtype (bf16, dense rows), as the
+// two passes after it computed it from the stored dX:
+//   h = bf16(dX * scale[m / sgrp])                          (sdp_rowscale_add, drop path)
+//   dmode 2: h = bf16(keep(seed, m * C + c) ? h / (1 - p) : 0)  (the branch's dropout, on the rounded h)
+//   act:     h = bf16(h * act'(Z))                          (sdp_act_bwd: the branch activation)
+struct LnBwdEmit {
+  const float* sc;
+  int sgrp;
+  const bf16_t* z;
+  int64_t ldz;
+  int act;
+  float p;
+  uint64_t seed;
+  int dmode;
+  bf16_t* o2;
+  int64_t ldo2;
+};
+
+// Deterministic in-kernel reduction of per-block column partials (part[b][0 .. n)): blocks are
+// grouped GS at a time; the last block of a group to finish (device-scope ticket) sums the group's
+// partials in block order into gpart[g], the last group to finish sums gpart in group order into
+// out.  The sums' order never depends on which block arrives last; tickets are reset by their last
+// user, so a buffer serves any number of launches on one stream.
+template <int NT>
+SDP_DEV void ticket_colsum(const float* part, int nb, int n, int gs, float* gpart, float* out, int* ticket) {
+  __shared__ int s_last;
+  __threadfence();  // this block's partials visible device-wide before its ticket
+  __syncthreads();
+  const int g = blockIdx.x / gs, ng = (nb + gs - 1) / gs;
+  const int b0 = g * gs, nin = min(gs, nb - b0);
+  if (threadIdx.x == 0) s_last = atomicAdd(&ticket[g], 1) == nin - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  for (int c = threadIdx.x * 4; c < n; c += NT * 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int r = 0;
+    for (; r + 8 <= nin; r += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(part + (int64_t)(b0 + r + u) * n + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; r < nin; ++r) acc += *(const f32x4*)(part + (int64_t)(b0 + r) * n + c);
+    *(f32x4*)(gpart + (int64_t)g * n + c) = acc;
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ticket[g] = 0;
+    s_last = atomicAdd(&ticket[ng], 1) == ng - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  for (int c = threadIdx.x * 4; c < n; c += NT * 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int r = 0;
+    for (; r + 8 <= ng; r += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(gpart + (int64_t)(r + u) * n + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; r < ng; ++r) acc += *(const f32x4*)(gpart + (int64_t)r * n + c);
+    *(f32x4*)(out + c) = acc;
+  }
+  if (threadIdx.x == 0) ticket[ng] = 0;
+}
+
 // Same backward, 8 consecutive channels per lane (16-B accesses; C % 8 == 0, aligned rows):
-// lane covers channels 8 * lane + 512 * i, i < V.
-template <typename T, typename TD, int V>
+// lane covers channels 8 * lane + 512 * i, i < V.  EM: also writes the branch gradient (LnBwdEmit);
+// ticket != nullptr: the affine partials are reduced in the same launch (ticket_colsum).
+template <typename T, typename TD, int V, bool EM>
 __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_t ldx, RowMap xm,
                                                  const float* __restrict__ st, const float* __restrict__ g,
                                                  const TD* __restrict__ DY, int64_t lddy, RowMap dym,
                                                  const T* __restrict__ ADD, int64_t ldadd, RowMap am,
                                                  T* __restrict__ DX, int64_t lddx, RowMap dxm, int M, int C,
-                                                 float* __restrict__ part) {
+                                                 float* __restrict__ part, float* gpart, float* aff, int* ticket,
+                                                 LnBwdEmit em) {
   extern __shared__ float red[];  // [2][4][C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float dg[V][8], db[V][8];
@@ -948,6 +1023,7 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
   struct RowIn {
     Raw8<T> x[V], a[V];
     Raw8<TD> dy[V];
+    Raw8<bf16_t> z[V];
     float mean, rstd;
   };
   auto fetch = [&](int64_t m, RowIn& r) {
@@ -963,9 +1039,14 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
         r.dy[i].load(dyp + c);
         r.x[i].load(xp + c);
         if (ap) r.a[i].load(ap + c);
+        if constexpr (EM) {
+          if (em.act != ACT_NONE) r.z[i].load(em.z + m * em.ldz + c);
+        }
       }
     }
   };
+  [[maybe_unused]] const float inv2 = EM && em.p > 0.f ? 1.0f / (1.0f - em.p) : 1.0f;
+  [[maybe_unused]] const uint32_t thr2 = EM ? drop_thresh(em.p) : 0u;
   int64_t m = (int64_t)blockIdx.x * 4 + w;
   RowIn cur, nxt;
   if (m < M) fetch(m, cur);
@@ -995,6 +1076,8 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
     }
     s1 = wave_sum(s1) / (float)C;
     s2 = wave_sum(s2) / (float)C;
+    [[maybe_unused]] float s_ = 1.0f;
+    if constexpr (EM) s_ = em.sc ? em.sc[m / em.sgrp] : 1.0f;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       const int c = 8 * lane + 512 * i;
@@ -1006,6 +1089,23 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
           o.v[q] = ADD ? cur.a[i][q] + v : v;
         }
         o.store(dxp + c);
+        if constexpr (EM) {  // the two passes that followed, on the stored value (rounded to T)
+          const uint64_t base = (uint64_t)m * C + c;
+          const uint32_t key = em.dmode == 2 ? drop_key(em.seed, base) : 0u;
+          bf16x8 hv;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float h = to_f<T>(from_f<T>(o.v[q])) * s_;
+            if (em.dmode == 2) {
+              const float r = bf2f(f2bf(h));
+              h = drop_keep(key, (uint32_t)base + q, thr2) ? r * inv2 : 0.f;
+            }
+            h = bf2f(f2bf(h));
+            if (em.act != ACT_NONE) h = h * act_grad(em.act, cur.z[i][q]);
+            hv[q] = (short)f2bf(h);
+          }
+          *(bf16x8*)(em.o2 + m * em.ldo2 + c) = hv;
+        }
       }
     }
     cur = nxt;
@@ -1028,6 +1128,7 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
     part[(int64_t)blockIdx.x * 2 * C + C + c] =
         red[4 * C + c] + red[5 * C + c] + red[6 * C + c] + red[7 * C + c];
   }
+  if (ticket) ticket_colsum<256>(part, gridDim.x, 2 * C, 32, gpart, aff, ticket);
 }
 
 // LayerNorm forward that also writes its statistics (training forward keeps them for the
@@ -1413,8 +1514,10 @@ static int ln_bwd_impl(int xdt, int dydt, const void* X, int64_t ldx, int x_grp,
                        const float* stats, const float* gamma, const void* DY, int64_t lddy, int dy_grp,
                        int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,
                        int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride, int dx_off, int M, int C,
-                       float* part, void* stream) {
+                       float* part, void* stream, float* gpart = nullptr, float* aff = nullptr, int* ticket = nullptr,
+                       const LnBwdEmit* em = nullptr) {
   if (!X || !stats || !gamma || !DY || !DX || M < 0 || C <= 0 || C > 2048) return (int)hipErrorInvalidValue;
+  if (ticket && (!part || !gpart || !aff)) return (int)hipErrorInvalidValue;
   if (M == 0) return 0;
   const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), dym = mk_tmap(dy_grp, dy_gstride, dy_off),
                am = mk_tmap(a_grp, a_gstride, a_off), dxm = mk_tmap(dx_grp, dx_gstride, dx_off);
@@ -1424,6 +1527,18 @@ static int ln_bwd_impl(int xdt, int dydt, const void* X, int64_t ldx, int x_grp,
   const bool vec = C % 8 == 0 && ldx % 8 == 0 && lddy % 8 == 0 && lddx % 8 == 0 && (!ADD || ldadd % 8 == 0) &&
                    (uintptr_t)X % 16 == 0 && (uintptr_t)DY % 16 == 0 && (uintptr_t)DX % 16 == 0 &&
                    (!ADD || (uintptr_t)ADD % 16 == 0) && (uintptr_t)gamma % 16 == 0;
+  // the one-launch forms (branch-gradient output, in-kernel affine sums) exist for ln_bwd_v8 only
+  const bool fused = ticket || em;
+  if (fused) {
+    auto a16 = [](const void* q) { return (uintptr_t)q % 16 == 0; };
+    if (!vec || C <= 128 || (C * 2) % 4 || (ticket && (!a16(part) || !a16(gpart) || !a16(aff))))
+      return (int)hipErrorNotSupported;
+    if (em && (!em->o2 || em->ldo2 % 8 || !a16(em->o2) || (em->sc && em->sgrp <= 0) || em->dmode < 0 ||
+               em->dmode > 2 || em->dmode == 1 || em->p < 0.f || em->p >= 1.f || em->act < 0 || em->act > ACT_KELU ||
+               (em->act != ACT_NONE && (!em->z || em->ldz % 8 || !a16(em->z)))))
+      return (int)hipErrorNotSupported;
+  }
+  const LnBwdEmit e0{};
   if (vec) {
     return by_dtypes(xdt, dydt, [&](auto tx, auto td) {
       using TX = typename decltype(tx)::type;
@@ -1437,10 +1552,15 @@ static int ln_bwd_impl(int xdt, int dydt, const void* X, int64_t ldx, int x_grp,
         return SDP_CHECK_LAUNCH();
       }
       const int v8 = (C + 511) / 512;
-#define SDP_LNV(VV)                                                                                              \
-  hipLaunchKernelGGL((ln_bwd_v8<TX, TD, VV>), grid, dim3(256), lds, s, (const TX*)X, ldx, xm, stats, gamma,        \
-                     (const TD*)DY, lddy, dym, (const TX*)ADD, ldadd, am, (TX*)DX, lddx, dxm, M, C, part)
-      if (v8 <= 1) SDP_LNV(1); else if (v8 <= 2) SDP_LNV(2); else SDP_LNV(4);
+#define SDP_LNV(VV, EMV)                                                                                          \
+  hipLaunchKernelGGL((ln_bwd_v8<TX, TD, VV, EMV>), grid, dim3(256), lds, s, (const TX*)X, ldx, xm, stats, gamma,   \
+                     (const TD*)DY, lddy, dym, (const TX*)ADD, ldadd, am, (TX*)DX, lddx, dxm, M, C, part, gpart, aff, \
+                     ticket, em ? *em : e0)
+      if (em) {
+        if (v8 <= 1) SDP_LNV(1, true); else if (v8 <= 2) SDP_LNV(2, true); else SDP_LNV(4, true);
+      } else {
+        if (v8 <= 1) SDP_LNV(1, false); else if (v8 <= 2) SDP_LNV(2, false); else SDP_LNV(4, false);
+      }
 #undef SDP_LNV
       return SDP_CHECK_LAUNCH();
     });
@@ -1476,6 +1596,25 @@ extern "C" int sdp_ln_bwd(int dtype, const void* X, int64_t ldx, int x_grp, int6
                           float* part, void* stream) {
   return ln_bwd_impl(dtype, dtype, X, ldx, x_grp, x_gstride, x_off, stats, gamma, DY, lddy, dy_grp, dy_gstride, dy_off,
                      ADD, ldadd, a_grp, a_gstride, a_off, DX, lddx, dx_grp, dx_gstride, dx_off, M, C, part, stream);
+}
+
+// sdp_ln_bwd_mixed in one launch with (a) the affine sums finished in the kernel: part
+// [sdp_ln_bwd_blocks(M)][2C] and gpart [ceil(blocks / 32)][2C] scratch, aff [2C] = {dgamma, dbeta},
+// ticket[ceil(blocks / 32) + 1] zeroed ints (left zeroed), or ticket = nullptr for part only; and
+// (b) optionally (O2 != nullptr) the branch gradient O2 (bf16, LnBwdEmit): bf16(DX * scale[m / sgrp]),
+// dmode 2 dropout (p, seed, index m * C + c), times act'(Z) (act != 0; Z bf16).  hipErrorNotSupported
+// where the one-launch form does not apply (C <= 128, C % 8, misaligned rows, dmode 1).
+extern "C" int sdp_ln_bwd_fused(int x_dtype, int dy_dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride,
+                                int x_off, const float* stats, const float* gamma, const void* DY, int64_t lddy,
+                                int dy_grp, int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp,
+                                int64_t a_gstride, int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride,
+                                int dx_off, int M, int C, float* part, float* gpart, float* aff, int* ticket,
+                                const float* scale, int sgrp, const void* Z, int64_t ldz, int act, float p,
+                                uint64_t seed, int dmode, void* O2, int64_t ldo2, void* stream) {
+  const LnBwdEmit em{scale, sgrp, (const bf16_t*)Z, ldz, act, p, seed, dmode, (bf16_t*)O2, ldo2};
+  return ln_bwd_impl(x_dtype, dy_dtype, X, ldx, x_grp, x_gstride, x_off, stats, gamma, DY, lddy, dy_grp, dy_gstride,
+                     dy_off, ADD, ldadd, a_grp, a_gstride, a_off, DX, lddx, dx_grp, dx_gstride, dx_off, M, C, part,
+                     stream, gpart, aff, ticket, O2 ? &em : nullptr);
 }
 
 // X, ADD and DX in x_dtype (the residual stream and its gradient), DY in dy_dtype (the

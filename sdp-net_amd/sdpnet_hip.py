@@ -103,6 +103,9 @@ _SIGS = {
                         _f32, _u64, _i32, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_ln_bwd_mixed": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _vp,
                           _i64, *_ROWMAP, _i32, _i32, _vp, _vp], _i32),
+    "sdp_ln_bwd_fused": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _vp,
+                          _i64, *_ROWMAP, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _i32, _f32, _u64, _i32,
+                          _vp, _i64, _vp], _i32),
     "sdp_ln_apply": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_ln_bwd_blocks": ([_i32], _i32),
     "sdp_ln_fwd": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
@@ -765,13 +768,66 @@ def ln_apply(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, beta: torch.Tens
     _check(rc, "ln_apply")
 
 
+_TICKETS = {}
+# SDPNET_LN_BWD_FUSED=0: LayerNorm backward as before (partials + two seg_colsum launches, branch passes
+# separate) -- A/B switch
+_LN_BWD_FUSED = os.environ.get("SDPNET_LN_BWD_FUSED", "1") != "0"
+# SDPNET_LN_TICKET=1: the affine sums finished inside the LayerNorm backward (ticketed last-block
+# reduction; its device-scope fences measured far slower on the XL training step), else the two
+# seg_colsum levels after it
+_LN_TICKET = os.environ.get("SDPNET_LN_TICKET", "0") != "0"
+
+
+def _tickets(dev: torch.device) -> torch.Tensor:
+    """Zeroed ints for the in-kernel affine sums of sdp_ln_bwd_fused, one buffer per (device,
+    stream): the kernels leave them zeroed, and launches on one stream never overlap."""
+    st = torch.cuda.current_stream(dev)
+    key = (dev.index, st.cuda_stream)
+    t = _TICKETS.get(key)
+    if t is None:
+        t = _TICKETS[key] = torch.zeros(64, dtype=torch.int32, device=dev)
+    return t
+
+
 def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows, M: int, C: int,
-           add: Optional[Rows] = None, want_affine: bool = True):
-    """dx (= LN backward [+ add]); returns (dgamma, dbeta) fp32 [C] or None."""
+           add: Optional[Rows] = None, want_affine: bool = True, emit: Optional[dict] = None, affine_on=None):
+    """dx (= LN backward [+ add]); returns (dgamma, dbeta) fp32 [C] or None.
+
+    emit = dict(out=bf16 [M, C] dense, scale=None, sgrp=1, z=None, act=0, p=0.0, seed=0, dmode=0): also
+    writes the gradient of the branch that fed the LayerNorm input, as sdp_rowscale_add (scale, and
+    dmode 2 dropout) followed by sdp_act_bwd (act'(z)) would from the stored dx -- in the same launch
+    where sdp_ln_bwd_fused applies, else by those two passes (bit-identical either way).
+    affine_on(fn, *inputs): where the affine sums of the per-block partials run (e.g. a side stream's
+    runner, returning fn()'s result); default: here, on the current stream."""
     _need_cuda(x.t, stats, gamma, dy.t, dx.t)
     _req(dx.t.dtype == x.t.dtype and (add is None or add.t.dtype == x.t.dtype), "ln_bwd x / add / dx dtypes")
     nb = lib().sdp_ln_bwd_blocks(M)
-    part = torch.empty(nb, 2, C, dtype=torch.float32, device=dx.t.device) if want_affine else None
+    dev = dx.t.device
+    part = torch.empty(nb, 2, C, dtype=torch.float32, device=dev) if want_affine else None
+    if emit is not None:
+        o2, z = emit["out"], emit.get("z")
+        _need_cuda(o2, z, emit.get("scale"))
+        _req(o2.dtype == torch.bfloat16 and o2.is_contiguous() and o2.shape[0] >= M and o2.shape[-1] == C and
+             (z is None or (z.dtype == torch.bfloat16 and z.is_contiguous() and z.shape[0] >= M and z.shape[-1] == C)),
+             "ln_bwd emit operands")
+    ticket = want_affine and _LN_TICKET
+    if _LN_BWD_FUSED and M > 0 and (emit is not None or ticket):
+        ng = (nb + 31) // 32
+        gpart = torch.empty(ng, 2 * C, dtype=torch.float32, device=dev) if ticket else None
+        aff = torch.empty(2 * C, dtype=torch.float32, device=dev) if ticket else None
+        e = emit or {}
+        sc = e.get("scale")
+        rc = lib().sdp_ln_bwd_fused(dcode(x.t.dtype), dcode(dy.t.dtype), *x.args(), stats.data_ptr(), gamma.data_ptr(),
+                                    *dy.args(), *_rows_args(add), *dx.args(), M, C, _ptr(part), _ptr(gpart), _ptr(aff),
+                                    _tickets(dev).data_ptr() if ticket else None, _ptr(sc), int(e.get("sgrp", 1)),
+                                    _ptr(e.get("z")), C, int(e.get("act", 0)), float(e.get("p", 0.0)),
+                                    int(e.get("seed", 0)) & 0xFFFFFFFFFFFFFFFF, int(e.get("dmode", 0)),
+                                    _ptr(e.get("out")), C, _stream(dx.t))
+        if rc != _HIP_NOT_SUPPORTED:
+            _check(rc, "ln_bwd_fused")
+            if ticket:
+                return aff[:C], aff[C:]
+            return _affine_sums(part, nb, C, affine_on) if want_affine else None
     if dy.t.dtype != x.t.dtype:  # fp32 stream, bf16 gradient of the LN output
         rc = lib().sdp_ln_bwd_mixed(dcode(x.t.dtype), dcode(dy.t.dtype), *x.args(), stats.data_ptr(), gamma.data_ptr(),
                                     *dy.args(), *_rows_args(add), *dx.args(), M, C, _ptr(part), _stream(dx.t))
@@ -779,12 +835,27 @@ def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows
         rc = lib().sdp_ln_bwd(dcode(x.t.dtype), *x.args(), stats.data_ptr(), gamma.data_ptr(), *dy.args(),
                               *_rows_args(add), *dx.args(), M, C, _ptr(part), _stream(dx.t))
     _check(rc, "ln_bwd")
+    if emit is not None:  # the two passes the one-launch form replaces
+        o2, z = emit["out"], emit.get("z")
+        rowscale_add(dx, dense(o2[:M]) if o2.shape[0] != M else dense(o2), M, C, scale=emit.get("scale"),
+                     sgrp=int(emit.get("sgrp", 1)), p=float(emit.get("p", 0.0)), seed=int(emit.get("seed", 0)),
+                     dmode=int(emit.get("dmode", 0)))
+        if int(emit.get("act", 0)):
+            act_bwd(z[:M], o2[:M], o2[:M], M, C, int(emit["act"]))
     if part is None:
         return None
-    out = torch.empty(2, C, dtype=torch.float32, device=dx.t.device)
+    return _affine_sums(part, nb, C, affine_on)
+
+
+def _affine_sums(part: torch.Tensor, nb: int, C: int, run_on=None):
+    """(dgamma, dbeta) from the LayerNorm backward's per-block partials [nb, 2, C]."""
+    if run_on is not None:
+        return run_on(lambda: _affine_sums(part, nb, C), part)
+    dev = part.device
+    out = torch.empty(2, C, dtype=torch.float32, device=dev)
     if nb >= 128:  # two levels: 32-row chunk sums in parallel, then the chunk sums
         g = nb // 32
-        tmp = torch.empty(g + 1, 2 * C, dtype=torch.float32, device=dx.t.device)
+        tmp = torch.empty(g + 1, 2 * C, dtype=torch.float32, device=dev)
         seg_colsum(part.view(nb, 2 * C), tmp, g, 32, 32, 1, 2 * C)
         rest = nb - 32 * g
         if rest:

@@ -665,3 +665,73 @@ def test_add_ln_fwd_one_pass_is_bit_identical(xdt, ydt, adt, act, p, C):
     # against plain torch: LN of the stored sum
     ys = outs[1][0].reshape(M, C).float()
     close(outs[1][1], F.layer_norm(ys, (C,), g, b, 1e-5), 1e-2 if adt == BF else 1e-5, what="add_ln_fwd LN")
+
+
+def _ln_bwd_case(B, R, P, C, seed, dense_rows):
+    N = R + P
+    M = B * P
+    x = rnd(B, N, C, seed=seed, scale=1.5) + rnd(B, N, 1, seed=seed + 1, scale=2)
+    add = rnd(B, N, C, seed=seed + 2)
+    da = rnd(M, C, seed=seed + 3, dtype=BF)
+    g = rnd(C, seed=seed + 4) * 0.2 + 1
+    st = torch.empty(M, 2, device=DEV)
+    rows = (lambda t: sp.dense(t.view(-1, C))) if dense_rows else (lambda t: sp.Rows(t, C, P, N, R))
+    if dense_rows:
+        M = B * N
+        da = rnd(M, C, seed=seed + 3, dtype=BF)
+        st = torch.empty(M, 2, device=DEV)
+    sp.rowstats(rows(x), 1e-6, st, M, C)
+    return x, add, da, g, st, rows, M
+
+
+@pytest.mark.parametrize("ticket", [False, True])
+@pytest.mark.parametrize("C", [768, 1032])
+@pytest.mark.parametrize("style", ["mixer", "encoder"])
+def test_ln_bwd_fused_matches_separate_passes(style, C, ticket, monkeypatch):
+    """sdp_ln_bwd_fused: DX and the emitted branch gradient bit-identical to sdp_ln_bwd_mixed followed by
+    the rowscale (drop path / dropout mode 2) and act_bwd passes; the in-kernel affine sums (ticketed,
+    fixed order) agree with the two-level seg_colsum sums to fp32 rounding and repeat bit for bit
+    (the tickets reset themselves between launches)."""
+    B, R, P = (3, 4, 49) if style == "mixer" else (5, 1, 63)
+    x, add, da, g, st, rows, M = _ln_bwd_case(B, R, P, C, 50, style == "encoder")
+    N = R + P
+    if style == "mixer":
+        scale, sgrp = torch.tensor([1.25, 0.0, 1.25], device=DEV), P
+        z = rnd(M, C, seed=57, dtype=BF)
+        emit = dict(scale=scale, sgrp=sgrp, z=z, act=1)
+    else:
+        scale, sgrp = torch.tensor([1.25, 0.0, 1.25, 1.25, 1.25], device=DEV), N
+        emit = dict(scale=scale, sgrp=sgrp, p=0.2, seed=321, dmode=2)
+    outs = []
+    monkeypatch.setattr(sp, "_LN_TICKET", ticket)
+    for fused in (False, True, True):
+        monkeypatch.setattr(sp, "_LN_BWD_FUSED", fused)
+        dx = torch.zeros_like(x)
+        o2 = torch.empty(M, C, device=DEV, dtype=BF)
+        aff = sp.ln_bwd(rows(x), st, g, sp.dense(da), rows(dx), M, C, add=rows(add), emit=dict(emit, out=o2))
+        outs.append((dx, o2, aff))
+    (dx0, o0, (g0, b0)), (dx1, o1, (g1, b1)), (dx2, o2_, (g2, b2)) = outs
+    assert torch.equal(dx0, dx1) and torch.equal(o0, o1)
+    assert torch.equal(g1, g2) and torch.equal(b1, b2)
+    close(g1, g0, 1e-5, "dgamma")
+    close(b1, b0, 1e-5, "dbeta")
+    ref_b = da.float().sum(0)
+    close(b1, ref_b, 1e-4, "dbeta vs torch")
+
+
+def test_ln_bwd_fused_affine_full_grid_deterministic(monkeypatch):
+    """1024 blocks (32 ticket groups) at the XL training shape: the affine sums equal the two-level
+    path to fp32 rounding, repeat bit for bit, and the branch-free call (no emit) leaves dx as before."""
+    B, R, P, C = 120, 4, 256, 768
+    x, add, da, g, st, rows, M = _ln_bwd_case(B, R, P, C, 60, False)
+    monkeypatch.setattr(sp, "_LN_TICKET", True)
+    res = []
+    for fused in (False, True, True):
+        monkeypatch.setattr(sp, "_LN_BWD_FUSED", fused)
+        dx = torch.zeros_like(x)
+        res.append((dx, sp.ln_bwd(rows(x), st, g, sp.dense(da), rows(dx), M, C, add=rows(add))))
+    (d0, (g0, b0)), (d1, (g1, b1)), (d2, (g2, b2)) = res
+    assert torch.equal(d0, d1)
+    assert torch.equal(g1, g2) and torch.equal(b1, b2)
+    close(g1, g0, 1e-5, "dgamma")
+    close(b1, b0, 1e-5, "dbeta")
