@@ -790,15 +790,13 @@ def _tickets(dev: torch.device) -> torch.Tensor:
 
 
 def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows, M: int, C: int,
-           add: Optional[Rows] = None, want_affine: bool = True, emit: Optional[dict] = None, affine_on=None):
+           add: Optional[Rows] = None, want_affine: bool = True, emit: Optional[dict] = None):
     """dx (= LN backward [+ add]); returns (dgamma, dbeta) fp32 [C] or None.
 
     emit = dict(out=bf16 [M, C] dense, scale=None, sgrp=1, z=None, act=0, p=0.0, seed=0, dmode=0): also
     writes the gradient of the branch that fed the LayerNorm input, as sdp_rowscale_add (scale, and
     dmode 2 dropout) followed by sdp_act_bwd (act'(z)) would from the stored dx -- in the same launch
-    where sdp_ln_bwd_fused applies, else by those two passes (bit-identical either way).
-    affine_on(fn, *inputs): where the affine sums of the per-block partials run (e.g. a side stream's
-    runner, returning fn()'s result); default: here, on the current stream."""
+    where sdp_ln_bwd_fused applies, else by those two passes (bit-identical either way)."""
     _need_cuda(x.t, stats, gamma, dy.t, dx.t)
     _req(dx.t.dtype == x.t.dtype and (add is None or add.t.dtype == x.t.dtype), "ln_bwd x / add / dx dtypes")
     nb = lib().sdp_ln_bwd_blocks(M)
@@ -827,7 +825,7 @@ def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows
             _check(rc, "ln_bwd_fused")
             if ticket:
                 return aff[:C], aff[C:]
-            return _affine_sums(part, nb, C, affine_on) if want_affine else None
+            return _affine_sums(part, nb, C) if want_affine else None
     if dy.t.dtype != x.t.dtype:  # fp32 stream, bf16 gradient of the LN output
         rc = lib().sdp_ln_bwd_mixed(dcode(x.t.dtype), dcode(dy.t.dtype), *x.args(), stats.data_ptr(), gamma.data_ptr(),
                                     *dy.args(), *_rows_args(add), *dx.args(), M, C, _ptr(part), _stream(dx.t))
@@ -844,13 +842,11 @@ def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows
             act_bwd(z[:M], o2[:M], o2[:M], M, C, int(emit["act"]))
     if part is None:
         return None
-    return _affine_sums(part, nb, C, affine_on)
+    return _affine_sums(part, nb, C)
 
 
-def _affine_sums(part: torch.Tensor, nb: int, C: int, run_on=None):
+def _affine_sums(part: torch.Tensor, nb: int, C: int):
     """(dgamma, dbeta) from the LayerNorm backward's per-block partials [nb, 2, C]."""
-    if run_on is not None:
-        return run_on(lambda: _affine_sums(part, nb, C), part)
     dev = part.device
     out = torch.empty(2, C, dtype=torch.float32, device=dev)
     if nb >= 128:  # two levels: 32-row chunk sums in parallel, then the chunk sums

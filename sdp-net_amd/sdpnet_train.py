@@ -418,8 +418,6 @@ def _add_ln_fwd(x: Rows, y: Rows, M: int, C: int, resid: Rows, g: torch.Tensor, 
 
 # SDPNET_TRAIN_ADD_LN=0: the branch add and the next LayerNorm as two passes (A/B switch)
 _ADD_LN = os.environ.get("SDPNET_TRAIN_ADD_LN", "1") != "0"
-# SDPNET_TRAIN_AFFINE_SIDE=1: the LayerNorm-affine sums of the per-block partials on the side stream
-_AFF_SIDE = os.environ.get("SDPNET_TRAIN_AFFINE_SIDE", "0") != "0"
 # SDPNET_TRAIN_LN_EMIT=0: the branch gradient after a LayerNorm backward as separate passes (A/B switch)
 _LN_EMIT = os.environ.get("SDPNET_TRAIN_LN_EMIT", "1") != "0"
 
@@ -506,7 +504,6 @@ class _MixerFn(torch.autograd.Function):
         dz2 = _dgrad_act(dz3, W_["dnw"], S["z2"], act, wt=W_["dnw_t"])
         has = S["has"]  # [g1, b1, dww, dwb, ccw, ccb, g2, b2, upw, upb, dnw, dnb]: bias grads only if the bias exists
         side = _Side(dev)
-        aff_on = side.run if _AFF_SIDE and side.on else None
         h_, a2_, d_, a1_ = S["h"], S["a2"], S["d"], S["a1"]
         gdn, gdnb = side.run(lambda: (_wgrad(dz3, h_), _colsum(dz3) if has[11] else None), dz3, h_)
         da2 = _dgrad(dz2, W_["upw"], W_["upw_t"])
@@ -516,10 +513,9 @@ class _MixerFn(torch.autograd.Function):
         dz1 = _empty((M, C), dt, dev)
         if _LN_EMIT and dt == torch.bfloat16:  # branch 2's gradient dz1 written by the LN2 backward
             gg2, gb2 = sp.ln_bwd(Rows(S["mid"], C, P, N, R), S["s2"], W_["g2"], _dense(da2), imid, M, C, add=iout,
-                                 emit=dict(out=dz1, scale=S["dp2"], sgrp=P, z=S["z1"], act=act), affine_on=aff_on)
+                                 emit=dict(out=dz1, scale=S["dp2"], sgrp=P, z=S["z1"], act=act))
         else:
-            gg2, gb2 = sp.ln_bwd(Rows(S["mid"], C, P, N, R), S["s2"], W_["g2"], _dense(da2), imid, M, C, add=iout,
-                                 affine_on=aff_on)
+            gg2, gb2 = sp.ln_bwd(Rows(S["mid"], C, P, N, R), S["s2"], W_["g2"], _dense(da2), imid, M, C, add=iout)
             # branch 2
             dh1 = _dense_copy(imid, M, C, dt, S["dp2"], P)
             sp.act_bwd(S["z1"], dh1, dz1, M, C, act)
@@ -532,8 +528,7 @@ class _MixerFn(torch.autograd.Function):
                                       _colsum(dd) if has[3] else None), a1_, dd)
         dx = dmid  # residual; LN1's input gradient is added in place on the image rows
         idx = Rows(dx, C, P, N, R)
-        gg1, gb1 = sp.ln_bwd(Rows(S["tok"], C, P, N, R), S["s1"], W_["g1"], _dense(da1), idx, M, C, add=idx,
-                             affine_on=aff_on)
+        gg1, gb1 = sp.ln_bwd(Rows(S["tok"], C, P, N, R), S["s1"], W_["g1"], _dense(da1), idx, M, C, add=idx)
         grads = [gg1, gb1, gdw, gdwb, gcc, gccb, gg2, gb2, gup, gupb, gdn, gdnb]
         side.join()
         ctx.st = None
@@ -685,7 +680,6 @@ class _EncoderFn(torch.autograd.Function):
         dz2 = _branch_grad(dout, T, C, dt, S["dp2"], N, p_ff, seeds[3])
         dz1 = _dgrad_act(dz2, W_["w2"], S["z1"], act, p_ff, seeds[2], wt=W_["w2_t"])
         side = _Side(dev)
-        aff_on = side.run if _AFF_SIDE and side.on else None
         h_, a2_, o_, a1_ = S["h"], S["a2"], S["o"], S["a1"]
         gw2, gb2 = side.run(lambda: (_wgrad(dz2, h_), _colsum(dz2)), dz2, h_)
         da2 = _dgrad(dz1, W_["w1"], W_["w1_t"])
@@ -694,11 +688,10 @@ class _EncoderFn(torch.autograd.Function):
         if _LN_EMIT and _DMODE and sdt != dt and dt == torch.bfloat16:  # the attention branch's gradient from norm2's backward
             dzo = _empty((T, C), dt, dev)
             gn2g, gn2b = sp.ln_bwd(_dense(S["t2"]), S["s2"], W_["n2g"], _dense(da2), _dense(dt2), T, C, add=_dense(dout),
-                                   emit=dict(out=dzo, scale=S["dp1"], sgrp=N, p=p_ff, seed=seeds[1], dmode=2),
-                                   affine_on=aff_on)
+                                   emit=dict(out=dzo, scale=S["dp1"], sgrp=N, p=p_ff, seed=seeds[1], dmode=2))
         else:
             gn2g, gn2b = sp.ln_bwd(_dense(S["t2"]), S["s2"], W_["n2g"], _dense(da2), _dense(dt2), T, C,
-                                   add=_dense(dout), affine_on=aff_on)
+                                   add=_dense(dout))
             # attention branch
             dzo = _branch_grad(dt2, T, C, dt, S["dp1"], N, p_ff, seeds[1])
         do = _dgrad(dzo, W_["wo"], W_["wo_t"])
@@ -731,8 +724,7 @@ class _EncoderFn(torch.autograd.Function):
         # dzo may BE dt2 (no dropout / drop path): with the side stream still reading it, the LN
         # backward adds into a fresh buffer instead of updating dt2 in place
         dx = _empty((T, C), sdt, dev) if side.on else dt2
-        gn1g, gn1b = sp.ln_bwd(_dense(S["tok"]), S["s1"], W_["n1g"], _dense(da1), _dense(dx), T, C, add=_dense(dt2),
-                               affine_on=aff_on)
+        gn1g, gn1b = sp.ln_bwd(_dense(S["tok"]), S["s1"], W_["n1g"], _dense(da1), _dense(dx), T, C, add=_dense(dt2))
         grads = [gn1g, gn1b, gqkv[:C], gqkv[C:2 * C], gqkv[2 * C:], gqg, gqb, gkg, gkb, gwo, gn2g, gn2b, gw1, gb1,
                  gw2, gb2]
         side.join()
