@@ -416,7 +416,10 @@ int sdp_ln_fwd_mixed(int x_dtype, int y_dtype, const void* X, int64_t ldx, int x
 /* Residual add + LayerNorm forward in one pass (training forward): y = act / dropout(x) * scale[m / sgrp]
  * + r (sdp_rowscale_add_mixed / sdp_rowscale_add_dropout mode 1 arithmetic; x in x_dtype, r and y in
  * y_dtype) and a = LN(y) with its (mean, rstd) statistics (sdp_ln_fwd_mixed; a in a_dtype), bit-identical
- * to the two passes.  hipErrorNotSupported where the one-pass form does not apply (C % 8, C <= 128, C > 2048,
+ * to the two passes.  reg_src != NULL: the register rows b * reg_n + i (i < reg_r, b < reg_b) of reg_src
+ * (y_dtype, row stride ldy) are copied to reg_dst0 (and reg_dst1) by extra workgroups of the same launch
+ * (a ConvMixer leaves them unchanged, layers.py:99-104).
+ * hipErrorNotSupported where the one-pass form does not apply (C % 8, C <= 128, C > 2048,
  * unaligned rows, dropout mode 2).  Replaces the branch add + LayerNorm pairs of layers.py:99-103
  * (ConvMixer, x + drop_path(act(PW(.))) then layer_norm_2) and :300-306 (EncoderLayer, x +
  * drop_path(dropout(o_proj(.))) then norm2) in the training step. */
@@ -424,7 +427,8 @@ int sdp_add_ln_fwd(int x_dtype, int y_dtype, int a_dtype, int act, const void* X
                    int64_t x_gstride, int x_off, const float* scale, int sgrp, const void* R, int64_t ldr, int r_grp,
                    int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp, int64_t y_gstride, int y_off,
                    float p, uint64_t seed, int dmode, float eps, const float* gamma, const float* beta, float* stats,
-                   void* A, int64_t lda, int a_grp, int64_t a_gstride, int a_off, int M, int C, void* stream);
+                   void* A, int64_t lda, int a_grp, int64_t a_gstride, int a_off, int M, int C,
+                   const void* reg_src, void* reg_dst0, void* reg_dst1, int reg_b, int reg_r, int reg_n, void* stream);
 int sdp_ln_bwd_mixed(int x_dtype, int dy_dtype, const void* X, int64_t ldx, int x_grp, int64_t x_gstride, int x_off,
                      const float* stats, const float* gamma, const void* DY, int64_t lddy, int dy_grp,
                      int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,
@@ -441,6 +445,8 @@ int sdp_ln_bwd_mixed(int x_dtype, int dy_dtype, const void* X, int64_t ldx, int 
  *      rows: O2 = bf16(DX * scale[m / sgrp]); dmode 2: dropout on the rounded value (keep iff
  *      hash(seed, m * C + c) >= p, kept / (1 - p)); act != 0: O2 = bf16(O2 * act'(Z)), Z bf16 dense
  *      rows -- bit-identical to sdp_rowscale_add_mixed (+ _dropout mode 2) then sdp_act_bwd on DX.
+ * (c) reg_src != NULL: register rows b * reg_n + i (i < reg_r, b < reg_b) of reg_src copied to reg_dst
+ *     (x_dtype, row stride lddx) -- the rows a ConvMixer passes through unchanged.
  * hipErrorNotSupported where the one-launch form does not apply (C <= 128, C % 8, unaligned rows,
  * dmode 1): the caller runs sdp_ln_bwd_mixed and the passes.  Replaces, per ConvMixer backward,
  * LN2 backward + drop_path_2 scale + act' (layers.py:99-103) and, per EncoderLayer backward, norm2
@@ -450,7 +456,8 @@ int sdp_ln_bwd_fused(int x_dtype, int dy_dtype, const void* X, int64_t ldx, int 
                      int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,
                      int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride, int dx_off, int M, int C,
                      float* part, float* gpart, float* aff, int* ticket, const float* scale, int sgrp, const void* Z,
-                     int64_t ldz, int act, float p, uint64_t seed, int dmode, void* O2, int64_t ldo2, void* stream);
+                     int64_t ldz, int act, float p, uint64_t seed, int dmode, void* O2, int64_t ldo2,
+                     const void* reg_src, void* reg_dst, int reg_b, int reg_r, int reg_n, void* stream);
 
 /* Attention rows (layers.py:289-298, SDPA dropout_p in training): P = softmax(scale * S[:, :N])
  * (S fp32), Pd = P with dropout p (may be NULL), columns [N, Npad) zeroed; backward

@@ -925,6 +925,33 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ X, int64_t
   }
 }
 
+// Register rows carried past a ConvMixer (layers.py:99-104 transforms the image rows only): rows
+// b * N + i (i < R, b < B) of src copied to dst0 (and dst1), row pitch ld bytes, `bytes` per row
+// (a multiple of 16, 16-B aligned).  One wave per row, folded into a row kernel the layer runs anyway
+// instead of a copy launch per buffer.
+struct RegCopy {
+  const char* src;
+  char* dst0;
+  char* dst1;
+  int64_t ld;
+  int B, R, N, bytes;
+};
+SDP_DEV void reg_copy_row(const RegCopy& rc, int w, int lane) {
+  if (!rc.src || w >= rc.B * rc.R) return;
+  const int b = w / rc.R, i = w - b * rc.R;
+  const int64_t off = ((int64_t)b * rc.N + i) * rc.ld;
+  for (int o = lane * 16; o < rc.bytes; o += 64 * 16) {
+    const int4 v = *(const int4*)(rc.src + off + o);
+    *(int4*)(rc.dst0 + off + o) = v;
+    if (rc.dst1) *(int4*)(rc.dst1 + off + o) = v;
+  }
+}
+static bool reg_copy_ok(const RegCopy& rc) {
+  auto a16 = [](const void* q) { return (uintptr_t)q % 16 == 0; };
+  return !rc.src || (rc.dst0 && a16(rc.src) && a16(rc.dst0) && (!rc.dst1 || a16(rc.dst1)) && rc.ld % 16 == 0 &&
+                     rc.bytes % 16 == 0 && rc.bytes <= rc.ld && rc.B >= 0 && rc.R >= 0 && rc.N >= rc.R);
+}
+
 // What a LayerNorm backward can hand on in the same pass (training, fp32 residual stream): the
 // gradient of the branch that fed the LayerNorm input, in the branch dtype (bf16, dense rows), as the
 // two passes after it computed it from the stored dX:
@@ -1008,9 +1035,11 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
                                                  const T* __restrict__ ADD, int64_t ldadd, RowMap am,
                                                  T* __restrict__ DX, int64_t lddx, RowMap dxm, int M, int C,
                                                  float* __restrict__ part, float* gpart, float* aff, int* ticket,
-                                                 LnBwdEmit em) {
+                                                 LnBwdEmit em, RegCopy rc) {
   extern __shared__ float red[];  // [2][4][C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (rc.src)
+    for (int gw = blockIdx.x * 4 + w; gw < rc.B * rc.R; gw += gridDim.x * 4) reg_copy_row(rc, gw, lane);
   float dg[V][8], db[V][8];
 #pragma unroll
   for (int i = 0; i < V; ++i)
@@ -1358,8 +1387,13 @@ __global__ __launch_bounds__(256) void add_ln_fwd_v8(const TX* __restrict__ X, i
                                                      RowMap ym, int act, float p, uint64_t seed, int dmode, float eps,
                                                      const float* __restrict__ g, const float* __restrict__ b,
                                                      float* __restrict__ st, TA* __restrict__ A, int64_t lda,
-                                                     RowMap am, int M, int C) {
+                                                     RowMap am, int M, int C, RegCopy rc) {
   const int lane = threadIdx.x & 63;
+  const int nbm = (M + 3) >> 2;
+  if ((int)blockIdx.x >= nbm) {  // register-row copy blocks after the row blocks
+    reg_copy_row(rc, ((int)blockIdx.x - nbm) * 4 + (threadIdx.x >> 6), lane);
+    return;
+  }
   const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
   const float inv = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
@@ -1435,10 +1469,16 @@ extern "C" int sdp_add_ln_fwd(int x_dtype, int y_dtype, int a_dtype, int act, co
                               int r_grp, int64_t r_gstride, int r_off, void* Y, int64_t ldy, int y_grp,
                               int64_t y_gstride, int y_off, float p, uint64_t seed, int dmode, float eps,
                               const float* gamma, const float* beta, float* stats, void* A, int64_t lda, int a_grp,
-                              int64_t a_gstride, int a_off, int M, int C, void* stream) {
+                              int64_t a_gstride, int a_off, int M, int C, const void* reg_src, void* reg_dst0,
+                              void* reg_dst1, int reg_b, int reg_r, int reg_n, void* stream) {
   if (!X || !R || !Y || !A || !stats || !gamma || !beta || M < 0 || C <= 0 || (scale && sgrp <= 0) || act < 0 ||
-      act > ACT_KELU || p < 0.f || p >= 1.f || dmode < 0 || dmode > 2)
+      act > ACT_KELU || p < 0.f || p >= 1.f || dmode < 0 || dmode > 2 ||
+      (reg_src && (!reg_dst0 || reg_b < 0 || reg_r < 0)))
     return (int)hipErrorInvalidValue;
+  const int yes = y_dtype == 1 ? 2 : 4;
+  const RegCopy rc{reg_b * reg_r > 0 ? (const char*)reg_src : nullptr, (char*)reg_dst0, (char*)reg_dst1, ldy * yes,
+                   reg_b, reg_r, reg_n, C * yes};
+  if (!reg_copy_ok(rc)) return (int)hipErrorNotSupported;
   if (p == 0.f) dmode = 0;
   // (C <= 128: sdp_ln_fwd takes the several-rows-per-wave kernel, whose sums run in another order)
   if (dmode == 2 || C % 8 || C <= 128 || C > 2048 || ldx % 8 || ldr % 8 || ldy % 8 || lda % 8 || (uintptr_t)X % 16 ||
@@ -1451,7 +1491,7 @@ extern "C" int sdp_add_ln_fwd(int x_dtype, int y_dtype, int a_dtype, int act, co
   const RowMap xm = mk_tmap(x_grp, x_gstride, x_off), rm = mk_tmap(r_grp, r_gstride, r_off),
                ym = mk_tmap(y_grp, y_gstride, y_off), am = mk_tmap(a_grp, a_gstride, a_off);
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((M + 3) / 4);
+  const dim3 grid((M + 3) / 4 + (rc.src ? (rc.B * rc.R + 3) / 4 : 0));
   const int v8 = (C + 511) / 512;
   auto launch = [&](auto tx, auto ty, auto ta) {
     using TX = typename decltype(tx)::type;
@@ -1460,7 +1500,7 @@ extern "C" int sdp_add_ln_fwd(int x_dtype, int y_dtype, int a_dtype, int act, co
 #define SDP_ALN(VV)                                                                                               \
   hipLaunchKernelGGL((add_ln_fwd_v8<TX, TY, TA, VV>), grid, dim3(256), 0, s, (const TX*)X, ldx, xm, scale, sgrp, \
                      (const TY*)R, ldr, rm, (TY*)Y, ldy, ym, act, p, seed, dmode, eps, gamma, beta, stats, (TA*)A,  \
-                     lda, am, M, C)
+                     lda, am, M, C, rc)
     if (v8 <= 1) SDP_ALN(1); else if (v8 <= 2) SDP_ALN(2); else SDP_ALN(4);
 #undef SDP_ALN
     return SDP_CHECK_LAUNCH();
@@ -1515,7 +1555,7 @@ static int ln_bwd_impl(int xdt, int dydt, const void* X, int64_t ldx, int x_grp,
                        int64_t dy_gstride, int dy_off, const void* ADD, int64_t ldadd, int a_grp, int64_t a_gstride,
                        int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride, int dx_off, int M, int C,
                        float* part, void* stream, float* gpart = nullptr, float* aff = nullptr, int* ticket = nullptr,
-                       const LnBwdEmit* em = nullptr) {
+                       const LnBwdEmit* em = nullptr, const RegCopy* rcp = nullptr) {
   if (!X || !stats || !gamma || !DY || !DX || M < 0 || C <= 0 || C > 2048) return (int)hipErrorInvalidValue;
   if (ticket && (!part || !gpart || !aff)) return (int)hipErrorInvalidValue;
   if (M == 0) return 0;
@@ -1528,8 +1568,9 @@ static int ln_bwd_impl(int xdt, int dydt, const void* X, int64_t ldx, int x_grp,
                    (uintptr_t)X % 16 == 0 && (uintptr_t)DY % 16 == 0 && (uintptr_t)DX % 16 == 0 &&
                    (!ADD || (uintptr_t)ADD % 16 == 0) && (uintptr_t)gamma % 16 == 0;
   // the one-launch forms (branch-gradient output, in-kernel affine sums) exist for ln_bwd_v8 only
-  const bool fused = ticket || em;
+  const bool fused = ticket || em || (rcp && rcp->src);
   if (fused) {
+    if (rcp && !reg_copy_ok(*rcp)) return (int)hipErrorNotSupported;
     auto a16 = [](const void* q) { return (uintptr_t)q % 16 == 0; };
     if (!vec || C <= 128 || (C * 2) % 4 || (ticket && (!a16(part) || !a16(gpart) || !a16(aff))))
       return (int)hipErrorNotSupported;
@@ -1539,6 +1580,7 @@ static int ln_bwd_impl(int xdt, int dydt, const void* X, int64_t ldx, int x_grp,
       return (int)hipErrorNotSupported;
   }
   const LnBwdEmit e0{};
+  const RegCopy r0{};
   if (vec) {
     return by_dtypes(xdt, dydt, [&](auto tx, auto td) {
       using TX = typename decltype(tx)::type;
@@ -1555,7 +1597,7 @@ static int ln_bwd_impl(int xdt, int dydt, const void* X, int64_t ldx, int x_grp,
 #define SDP_LNV(VV, EMV)                                                                                          \
   hipLaunchKernelGGL((ln_bwd_v8<TX, TD, VV, EMV>), grid, dim3(256), lds, s, (const TX*)X, ldx, xm, stats, gamma,   \
                      (const TD*)DY, lddy, dym, (const TX*)ADD, ldadd, am, (TX*)DX, lddx, dxm, M, C, part, gpart, aff, \
-                     ticket, em ? *em : e0)
+                     ticket, em ? *em : e0, rcp ? *rcp : r0)
       if (em) {
         if (v8 <= 1) SDP_LNV(1, true); else if (v8 <= 2) SDP_LNV(2, true); else SDP_LNV(4, true);
       } else {
@@ -1610,11 +1652,15 @@ extern "C" int sdp_ln_bwd_fused(int x_dtype, int dy_dtype, const void* X, int64_
                                 int64_t a_gstride, int a_off, void* DX, int64_t lddx, int dx_grp, int64_t dx_gstride,
                                 int dx_off, int M, int C, float* part, float* gpart, float* aff, int* ticket,
                                 const float* scale, int sgrp, const void* Z, int64_t ldz, int act, float p,
-                                uint64_t seed, int dmode, void* O2, int64_t ldo2, void* stream) {
+                                uint64_t seed, int dmode, void* O2, int64_t ldo2, const void* reg_src, void* reg_dst,
+                                int reg_b, int reg_r, int reg_n, void* stream) {
   const LnBwdEmit em{scale, sgrp, (const bf16_t*)Z, ldz, act, p, seed, dmode, (bf16_t*)O2, ldo2};
+  const int es = x_dtype == 1 ? 2 : 4;
+  const RegCopy rc{(const char*)reg_src, (char*)reg_dst, nullptr, lddx * es, reg_b, reg_r, reg_n, C * es};
+  if (reg_src && (!reg_dst || reg_b < 0 || reg_r < 0)) return (int)hipErrorInvalidValue;
   return ln_bwd_impl(x_dtype, dy_dtype, X, ldx, x_grp, x_gstride, x_off, stats, gamma, DY, lddy, dy_grp, dy_gstride,
                      dy_off, ADD, ldadd, a_grp, a_gstride, a_off, DX, lddx, dx_grp, dx_gstride, dx_off, M, C, part,
-                     stream, gpart, aff, ticket, O2 ? &em : nullptr);
+                     stream, gpart, aff, ticket, O2 ? &em : nullptr, reg_src && reg_b * reg_r > 0 ? &rc : nullptr);
 }
 
 // X, ADD and DX in x_dtype (the residual stream and its gradient), DY in dy_dtype (the

@@ -100,12 +100,13 @@ _SIGS = {
     "sdp_ln_fwd_mixed": ([_i32, _i32, _vp, _i64, *_ROWMAP, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp],
                          _i32),
     "sdp_add_ln_fwd": ([_i32, _i32, _i32, _i32, _vp, _i64, *_ROWMAP, _vp, _i32, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP,
-                        _f32, _u64, _i32, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
+                        _f32, _u64, _i32, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp, _vp, _vp, _i32,
+                        _i32, _i32, _vp], _i32),
     "sdp_ln_bwd_mixed": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _vp,
                           _i64, *_ROWMAP, _i32, _i32, _vp, _vp], _i32),
     "sdp_ln_bwd_fused": ([_i32, _i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _i64, *_ROWMAP, _vp, _i64, *_ROWMAP, _vp,
                           _i64, *_ROWMAP, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _i32, _f32, _u64, _i32,
-                          _vp, _i64, _vp], _i32),
+                          _vp, _i64, _vp, _vp, _i32, _i32, _i32, _vp], _i32),
     "sdp_ln_apply": ([_i32, _vp, _i64, *_ROWMAP, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
     "sdp_ln_bwd_blocks": ([_i32], _i32),
     "sdp_ln_fwd": ([_i32, _vp, _i64, *_ROWMAP, _f32, _vp, _vp, _vp, _vp, _i64, *_ROWMAP, _i32, _i32, _vp], _i32),
@@ -742,22 +743,49 @@ def rowscale_add(x: Rows, y: Rows, M: int, N: int, scale: Optional[torch.Tensor]
 
 def add_ln_fwd(x: Rows, y: Rows, a: Rows, M: int, C: int, resid: Rows, eps: float, gamma: torch.Tensor,
                beta: torch.Tensor, stats: torch.Tensor, scale: Optional[torch.Tensor] = None, sgrp: int = 1,
-               act: int = 0, p: float = 0.0, seed: int = 0, dmode: int = 0) -> bool:
+               act: int = 0, p: float = 0.0, seed: int = 0, dmode: int = 0, regs=None) -> bool:
     """y = act / dropout(x) * scale[m / sgrp] + resid and a = LN(y) (+ its statistics) in one pass
-    (sdp_add_ln_fwd; bit-identical to rowscale_add followed by ln_fwd).  False where the one-pass form
-    does not apply (the caller runs the two passes)."""
+    (sdp_add_ln_fwd; bit-identical to rowscale_add followed by ln_fwd).  regs = (src, [dst0, dst1], B, R,
+    N): also copy the register rows (token buffers [B, N, C] in y's dtype) in the same launch.  False
+    where the one-pass form does not apply (the caller runs the two passes and the copies)."""
     _need_cuda(x.t, y.t, a.t, resid.t, gamma, beta, stats, scale)
     _req(resid.t.dtype == y.t.dtype, "add_ln_fwd: resid dtype = y dtype")
     _req(stats.dtype == gamma.dtype == beta.dtype == torch.float32, "add_ln_fwd fp32 params")
     _req(scale is None or scale.dtype == torch.float32, "add_ln_fwd scale fp32")
+    rsrc, rd0, rd1, rb, rr, rn = _reg_args(regs, y.t.dtype, C, 2)
     rc = lib().sdp_add_ln_fwd(dcode(x.t.dtype), dcode(y.t.dtype), dcode(a.t.dtype), int(act), *x.args(), _ptr(scale),
                               sgrp, *resid.args(), *y.args(), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(dmode),
                               float(eps), gamma.data_ptr(), beta.data_ptr(), stats.data_ptr(), *a.args(), M, C,
-                              _stream(y.t))
+                              rsrc, rd0, rd1, rb, rr, rn, _stream(y.t))
     if rc == _HIP_NOT_SUPPORTED:
         return False
     _check(rc, "add_ln_fwd")
     return True
+
+
+def _reg_args(regs, dt, C: int, ndst: int):
+    """(src ptr, dst0, dst1, B, R, N) of a register-row copy job regs = (src, [dsts], B, R, N), or Nones."""
+    if regs is None:
+        return None, None, None, 0, 0, 0
+    src, dsts, B, R, N = regs
+    _req(1 <= len(dsts) <= ndst, "register copy: destinations")
+    for t in (src, *dsts):
+        _need_cuda(t)
+        _req(t.dtype == dt and t.is_contiguous() and t.numel() >= B * N * C and t.shape[-1] == C and R <= N,
+             "register copy operands")
+    return (src.data_ptr(), dsts[0].data_ptr(), dsts[1].data_ptr() if len(dsts) > 1 else None, int(B), int(R),
+            int(N))
+
+
+def copy_regs(regs):
+    """The register-row copy job of regs = (src, [dsts], B, R, N) as separate copy_rows launches."""
+    if regs is None:
+        return
+    src, dsts, B, R, N = regs
+    C = src.shape[-1]
+    if R:
+        for d in dsts:
+            copy_rows(src, C, N * C, d, C, N * C, B, R, C)
 
 
 def ln_apply(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, y: Rows, M: int, C: int):
@@ -790,13 +818,15 @@ def _tickets(dev: torch.device) -> torch.Tensor:
 
 
 def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows, M: int, C: int,
-           add: Optional[Rows] = None, want_affine: bool = True, emit: Optional[dict] = None):
+           add: Optional[Rows] = None, want_affine: bool = True, emit: Optional[dict] = None, regs=None):
     """dx (= LN backward [+ add]); returns (dgamma, dbeta) fp32 [C] or None.
 
     emit = dict(out=bf16 [M, C] dense, scale=None, sgrp=1, z=None, act=0, p=0.0, seed=0, dmode=0): also
     writes the gradient of the branch that fed the LayerNorm input, as sdp_rowscale_add (scale, and
     dmode 2 dropout) followed by sdp_act_bwd (act'(z)) would from the stored dx -- in the same launch
-    where sdp_ln_bwd_fused applies, else by those two passes (bit-identical either way)."""
+    where sdp_ln_bwd_fused applies, else by those two passes (bit-identical either way).
+    regs = (src, [dst], B, R, N): register rows of src (dx's dtype) copied to dst, in the same launch
+    where it applies."""
     _need_cuda(x.t, stats, gamma, dy.t, dx.t)
     _req(dx.t.dtype == x.t.dtype and (add is None or add.t.dtype == x.t.dtype), "ln_bwd x / add / dx dtypes")
     nb = lib().sdp_ln_bwd_blocks(M)
@@ -809,7 +839,8 @@ def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows
              (z is None or (z.dtype == torch.bfloat16 and z.is_contiguous() and z.shape[0] >= M and z.shape[-1] == C)),
              "ln_bwd emit operands")
     ticket = want_affine and _LN_TICKET
-    if _LN_BWD_FUSED and M > 0 and (emit is not None or ticket):
+    rsrc, rd0, _, rb, rr, rn = _reg_args(regs, dx.t.dtype, C, 1)
+    if _LN_BWD_FUSED and M > 0 and (emit is not None or ticket or regs is not None):
         ng = (nb + 31) // 32
         gpart = torch.empty(ng, 2 * C, dtype=torch.float32, device=dev) if ticket else None
         aff = torch.empty(2 * C, dtype=torch.float32, device=dev) if ticket else None
@@ -820,12 +851,13 @@ def ln_bwd(x: Rows, stats: torch.Tensor, gamma: torch.Tensor, dy: Rows, dx: Rows
                                     _tickets(dev).data_ptr() if ticket else None, _ptr(sc), int(e.get("sgrp", 1)),
                                     _ptr(e.get("z")), C, int(e.get("act", 0)), float(e.get("p", 0.0)),
                                     int(e.get("seed", 0)) & 0xFFFFFFFFFFFFFFFF, int(e.get("dmode", 0)),
-                                    _ptr(e.get("out")), C, _stream(dx.t))
+                                    _ptr(e.get("out")), C, rsrc, rd0, rb, rr, rn, _stream(dx.t))
         if rc != _HIP_NOT_SUPPORTED:
             _check(rc, "ln_bwd_fused")
             if ticket:
                 return aff[:C], aff[C:]
             return _affine_sums(part, nb, C) if want_affine else None
+    copy_regs(regs)
     if dy.t.dtype != x.t.dtype:  # fp32 stream, bf16 gradient of the LN output
         rc = lib().sdp_ln_bwd_mixed(dcode(x.t.dtype), dcode(dy.t.dtype), *x.args(), stats.data_ptr(), gamma.data_ptr(),
                                     *dy.args(), *_rows_args(add), *dx.args(), M, C, _ptr(part), _stream(dx.t))

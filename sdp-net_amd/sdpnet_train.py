@@ -394,24 +394,31 @@ def _branch_grad(d: torch.Tensor, T: int, C: int, dt, dp: Optional[torch.Tensor]
     return out
 
 
-def _with_regs(src: torch.Tensor, B: int, R: int, N: int, C: int) -> torch.Tensor:
-    """A new token buffer whose register rows are copied from ``src`` (the image rows are
-    about to be written in full by the caller)."""
-    out = torch.empty_like(src)
-    if R:
-        sp.copy_rows(src, C, N * C, out, C, N * C, B, R, C)
-    return out
+# SDPNET_TRAIN_REG_FOLD=0: the ConvMixer's register-row copies as separate launches (A/B switch)
+_REG_FOLD = os.environ.get("SDPNET_TRAIN_REG_FOLD", "1") != "0"
+
+
+def _regs(src: torch.Tensor, dsts, B: int, R: int, N: int):
+    """The register-row copy job src -> dsts for a row kernel to fold in (None: nothing left to copy)."""
+    if not R:
+        return None
+    if not _REG_FOLD:
+        sp.copy_regs((src, dsts, B, R, N))
+        return None
+    return (src, dsts, B, R, N)
 
 
 def _add_ln_fwd(x: Rows, y: Rows, M: int, C: int, resid: Rows, g: torch.Tensor, b: torch.Tensor, eps: float, dt,
-                scale=None, sgrp: int = 1, act: int = 0, p: float = 0.0, seed: int = 0, dmode: int = 0):
+                scale=None, sgrp: int = 1, act: int = 0, p: float = 0.0, seed: int = 0, dmode: int = 0, regs=None):
     """y = act / dropout(x) * scale + resid (the branch add), then (a, stats) = LN(y): one pass
-    (sp.add_ln_fwd) where it applies, else rowscale_add + _ln_fwd (bit-identical either way)."""
+    (sp.add_ln_fwd) where it applies, else rowscale_add + _ln_fwd (bit-identical either way); regs: a
+    register-row copy job (sp.add_ln_fwd) done in the same launch."""
     st = _empty((M, 2), torch.float32, x.t.device)
     a = _empty((M, C), dt, x.t.device)
     if _ADD_LN and sp.add_ln_fwd(x, y, _dense(a), M, C, resid, eps, g, b, st, scale=scale, sgrp=sgrp, act=act, p=p,
-                                 seed=seed, dmode=dmode):
+                                 seed=seed, dmode=dmode, regs=regs):
         return a, st
+    sp.copy_regs(regs)
     sp.rowscale_add(x, y, M, C, scale=scale, sgrp=sgrp, resid=resid, act=act, p=p, seed=seed, dmode=dmode)
     return _ln_fwd(y, M, C, g, b, eps, dt)
 
@@ -471,14 +478,15 @@ class _MixerFn(torch.autograd.Function):
         d = _empty((M, C), dt, dev)
         sp.dwconv(_dense(a1), W_["dww"], W_["dwb"], _dense(d), B, H, W, C, k)
         z1 = _linear(d, W_["ccw"], W_["ccb"], dt)
-        mid = _with_regs(tok, B, R, N, C)
+        mid = torch.empty_like(tok)
+        out = torch.empty_like(tok)
         imid = Rows(mid, C, P, N, R)
-        # act + drop path + residual, then LN2 of the sum (one pass)
+        # act + drop path + residual, then LN2 of the sum (one pass; the register rows of mid and out
+        # copied from tok by the same launch)
         # x = drop_path_1(PW_down(act(PW_up(LN2 x_)))) + x_
         a2, s2 = _add_ln_fwd(_dense(z1), imid, M, C, img, W_["g2"], W_["b2"], m.layer_norm_2.eps, dt, scale=dp2, sgrp=P,
-                             act=act)
+                             act=act, regs=_regs(tok, [mid, out], B, R, N))
         z2, h = _linear_act(a2, W_["upw"], W_["upb"], dt, act)
-        out = _with_regs(mid, B, R, N, C)
         if dp1 is None and tok.dtype == dt:  # residual add in the GEMM epilogue, straight into the token rows
             sp.gemm(_dense(h), W_["dnw"], Rows(out, C, P, N, R), M, C, 4 * C, bias=W_["dnb"], resid=imid)
         else:
@@ -508,14 +516,16 @@ class _MixerFn(torch.autograd.Function):
         gdn, gdnb = side.run(lambda: (_wgrad(dz3, h_), _colsum(dz3) if has[11] else None), dz3, h_)
         da2 = _dgrad(dz2, W_["upw"], W_["upw_t"])
         gup, gupb = side.run(lambda: (_wgrad(dz2, a2_), _colsum(dz2) if has[9] else None), dz2, a2_)
-        dmid = _with_regs(dout, B, R, N, C)
+        dmid = torch.empty_like(dout)  # register rows copied from dout by the LN2 backward's launch
+        regs = _regs(dout, [dmid], B, R, N)
         imid = Rows(dmid, C, P, N, R)
         dz1 = _empty((M, C), dt, dev)
         if _LN_EMIT and dt == torch.bfloat16:  # branch 2's gradient dz1 written by the LN2 backward
             gg2, gb2 = sp.ln_bwd(Rows(S["mid"], C, P, N, R), S["s2"], W_["g2"], _dense(da2), imid, M, C, add=iout,
-                                 emit=dict(out=dz1, scale=S["dp2"], sgrp=P, z=S["z1"], act=act))
+                                 emit=dict(out=dz1, scale=S["dp2"], sgrp=P, z=S["z1"], act=act), regs=regs)
         else:
-            gg2, gb2 = sp.ln_bwd(Rows(S["mid"], C, P, N, R), S["s2"], W_["g2"], _dense(da2), imid, M, C, add=iout)
+            gg2, gb2 = sp.ln_bwd(Rows(S["mid"], C, P, N, R), S["s2"], W_["g2"], _dense(da2), imid, M, C, add=iout,
+                                 regs=regs)
             # branch 2
             dh1 = _dense_copy(imid, M, C, dt, S["dp2"], P)
             sp.act_bwd(S["z1"], dh1, dz1, M, C, act)
