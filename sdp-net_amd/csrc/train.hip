@@ -577,7 +577,7 @@ __global__ __launch_bounds__(256) void act_bwd_v8(const T* __restrict__ Z, int64
 
 // X in TX; the residual R and the output Y in TY (TX = bf16 branch, TY = fp32 residual stream
 // in the fp32-stream training mode; the reverse for a stream gradient cast into a branch).
-template <typename TX, typename TY>
+template <typename TX, typename TY, int ACT>
 __global__ __launch_bounds__(256) void rowscale_v8(const TX* __restrict__ X, int64_t ldx, RowMap xm,
                                                    const float* __restrict__ sc, int sgrp, const TY* __restrict__ R,
                                                    int64_t ldr, RowMap rm, TY* __restrict__ Y, int64_t ldy, RowMap ym,
@@ -591,9 +591,10 @@ __global__ __launch_bounds__(256) void rowscale_v8(const TX* __restrict__ X, int
     const int n = (int)(e - m * n8) * 8;
     V8<TX> x;
     x.load(X + xm(m) * ldx + n);
-    if (act != ACT_NONE) {  // = sdp_act_fwd's stored output (rounded to TX) without the round trip
+    const int a = ACT >= 0 ? ACT : act;
+    if (a != ACT_NONE) {  // = sdp_act_fwd's stored output (rounded to TX) without the round trip
 #pragma unroll
-      for (int q = 0; q < 8; ++q) x.v[q] = to_f<TX>(from_f<TX>(apply_act(act, x.v[q])));
+      for (int q = 0; q < 8; ++q) x.v[q] = to_f<TX>(from_f<TX>(apply_act(a, x.v[q])));
     }
     const uint64_t base = (uint64_t)m * N + n;
     const uint32_t key = dmode ? drop_key(seed, base) : 0u;
@@ -774,8 +775,12 @@ static int rowscale_impl(int xdt, int ydt, int act, const void* X, int64_t ldx, 
     return by_dtypes(xdt, ydt, [&](auto tx, auto ty) {
       using TX = typename decltype(tx)::type;
       using TY = typename decltype(ty)::type;
-      hipLaunchKernelGGL((rowscale_v8<TX, TY>), dim3(gv), dim3(256), 0, s, (const TX*)X, ldx, xm, scale, sgrp,
-                         (const TY*)R, ldr, rm, (TY*)Y, ldy, ym, M, N, act, p, seed, dmode);
+      if (act == ACT_GELU)
+        hipLaunchKernelGGL((rowscale_v8<TX, TY, ACT_GELU>), dim3(gv), dim3(256), 0, s, (const TX*)X, ldx, xm, scale,
+                           sgrp, (const TY*)R, ldr, rm, (TY*)Y, ldy, ym, M, N, act, p, seed, dmode);
+      else
+        hipLaunchKernelGGL((rowscale_v8<TX, TY, -1>), dim3(gv), dim3(256), 0, s, (const TX*)X, ldx, xm, scale, sgrp,
+                           (const TY*)R, ldr, rm, (TY*)Y, ldy, ym, M, N, act, p, seed, dmode);
       return SDP_CHECK_LAUNCH();
     });
   }
@@ -1026,9 +1031,12 @@ SDP_DEV void ticket_colsum(const float* part, int nb, int n, int gs, float* gpar
 }
 
 // Same backward, 8 consecutive channels per lane (16-B accesses; C % 8 == 0, aligned rows):
-// lane covers channels 8 * lane + 512 * i, i < V.  EM: also writes the branch gradient (LnBwdEmit);
+// lane covers channels 8 * lane + 512 * i, i < V.  EA != LNB_NOEMIT: also writes the branch gradient
+// (LnBwdEmit) with activation EA (the model's GELU / none at compile time, -1: em.act at run time);
 // ticket != nullptr: the affine partials are reduced in the same launch (ticket_colsum).
-template <typename T, typename TD, int V, bool EM>
+constexpr int LNB_NOEMIT = -100;  // EA of a LayerNorm backward without the branch-gradient output
+
+template <typename T, typename TD, int V, int EA>
 __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_t ldx, RowMap xm,
                                                  const float* __restrict__ st, const float* __restrict__ g,
                                                  const TD* __restrict__ DY, int64_t lddy, RowMap dym,
@@ -1036,6 +1044,8 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
                                                  T* __restrict__ DX, int64_t lddx, RowMap dxm, int M, int C,
                                                  float* __restrict__ part, float* gpart, float* aff, int* ticket,
                                                  LnBwdEmit em, RegCopy rc) {
+  constexpr bool EM = EA != LNB_NOEMIT;
+  [[maybe_unused]] const int ea = EA >= 0 ? EA : em.act;  // the emitted gradient's activation
   extern __shared__ float red[];  // [2][4][C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (rc.src)
@@ -1069,7 +1079,7 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
         r.x[i].load(xp + c);
         if (ap) r.a[i].load(ap + c);
         if constexpr (EM) {
-          if (em.act != ACT_NONE) r.z[i].load(em.z + m * em.ldz + c);
+          if (ea != ACT_NONE) r.z[i].load(em.z + m * em.ldz + c);
         }
       }
     }
@@ -1130,7 +1140,7 @@ __global__ __launch_bounds__(256) void ln_bwd_v8(const T* __restrict__ X, int64_
               h = drop_keep(key, (uint32_t)base + q, thr2) ? r * inv2 : 0.f;
             }
             h = bf2f(f2bf(h));
-            if (em.act != ACT_NONE) h = h * act_grad(em.act, cur.z[i][q]);
+            if (ea != ACT_NONE) h = h * act_grad(ea, cur.z[i][q]);
             hv[q] = (short)f2bf(h);
           }
           *(bf16x8*)(em.o2 + m * em.ldo2 + c) = hv;
@@ -1380,7 +1390,7 @@ static int ln_fwd_impl(int xdt, int ydt, const void* X, int64_t ldx, int x_grp, 
 // One wave per row; y is rounded to its dtype before the statistics, so both outputs and the
 // statistics are bit-identical to the two separate passes (which stored y and re-read it).  Saves
 // the re-read of y and one launch per sub-layer.
-template <typename TX, typename TY, typename TA, int V>
+template <typename TX, typename TY, typename TA, int V, int ACT>
 __global__ __launch_bounds__(256) void add_ln_fwd_v8(const TX* __restrict__ X, int64_t ldx, RowMap xm,
                                                      const float* __restrict__ sc, int sgrp, const TY* __restrict__ R,
                                                      int64_t ldr, RowMap rm, TY* __restrict__ Y, int64_t ldy,
@@ -1410,9 +1420,10 @@ __global__ __launch_bounds__(256) void add_ln_fwd_v8(const TX* __restrict__ X, i
     if (c < C) {
       V8<TX> x;
       x.load(xp + c);
-      if (act != ACT_NONE) {  // rowscale_v8's arithmetic, step by step
+      const int a = ACT >= 0 ? ACT : act;
+      if (a != ACT_NONE) {  // rowscale_v8's arithmetic, step by step
 #pragma unroll
-        for (int q = 0; q < 8; ++q) x.v[q] = to_f<TX>(from_f<TX>(apply_act(act, x.v[q])));
+        for (int q = 0; q < 8; ++q) x.v[q] = to_f<TX>(from_f<TX>(apply_act(a, x.v[q])));
       }
       if (dmode == 1) {
         const uint64_t base = (uint64_t)m * C + c;
@@ -1497,11 +1508,15 @@ extern "C" int sdp_add_ln_fwd(int x_dtype, int y_dtype, int a_dtype, int act, co
     using TX = typename decltype(tx)::type;
     using TY = typename decltype(ty)::type;
     using TA = typename decltype(ta)::type;
-#define SDP_ALN(VV)                                                                                               \
-  hipLaunchKernelGGL((add_ln_fwd_v8<TX, TY, TA, VV>), grid, dim3(256), 0, s, (const TX*)X, ldx, xm, scale, sgrp, \
+#define SDP_ALN(VV, AA)                                                                                           \
+  hipLaunchKernelGGL((add_ln_fwd_v8<TX, TY, TA, VV, AA>), grid, dim3(256), 0, s, (const TX*)X, ldx, xm, scale, sgrp, \
                      (const TY*)R, ldr, rm, (TY*)Y, ldy, ym, act, p, seed, dmode, eps, gamma, beta, stats, (TA*)A,  \
                      lda, am, M, C, rc)
-    if (v8 <= 1) SDP_ALN(1); else if (v8 <= 2) SDP_ALN(2); else SDP_ALN(4);
+    if (act == ACT_GELU) {
+      if (v8 <= 1) SDP_ALN(1, ACT_GELU); else if (v8 <= 2) SDP_ALN(2, ACT_GELU); else SDP_ALN(4, ACT_GELU);
+    } else {
+      if (v8 <= 1) SDP_ALN(1, -1); else if (v8 <= 2) SDP_ALN(2, -1); else SDP_ALN(4, -1);
+    }
 #undef SDP_ALN
     return SDP_CHECK_LAUNCH();
   };
@@ -1598,11 +1613,13 @@ static int ln_bwd_impl(int xdt, int dydt, const void* X, int64_t ldx, int x_grp,
   hipLaunchKernelGGL((ln_bwd_v8<TX, TD, VV, EMV>), grid, dim3(256), lds, s, (const TX*)X, ldx, xm, stats, gamma,   \
                      (const TD*)DY, lddy, dym, (const TX*)ADD, ldadd, am, (TX*)DX, lddx, dxm, M, C, part, gpart, aff, \
                      ticket, em ? *em : e0, rcp ? *rcp : r0)
-      if (em) {
-        if (v8 <= 1) SDP_LNV(1, true); else if (v8 <= 2) SDP_LNV(2, true); else SDP_LNV(4, true);
-      } else {
-        if (v8 <= 1) SDP_LNV(1, false); else if (v8 <= 2) SDP_LNV(2, false); else SDP_LNV(4, false);
-      }
+#define SDP_LNVA(EA_)                                                                              \
+  if (v8 <= 1) SDP_LNV(1, EA_); else if (v8 <= 2) SDP_LNV(2, EA_); else SDP_LNV(4, EA_);
+      if (!em) { SDP_LNVA(LNB_NOEMIT) }
+      else if (em->act == ACT_GELU) { SDP_LNVA(ACT_GELU) }
+      else if (em->act == ACT_NONE) { SDP_LNVA(ACT_NONE) }
+      else { SDP_LNVA(-1) }
+#undef SDP_LNVA
 #undef SDP_LNV
       return SDP_CHECK_LAUNCH();
     });

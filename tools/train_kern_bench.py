@@ -53,11 +53,16 @@ def main():
     img = lambda t: Rows(t, C, P, N, R)  # noqa: E731
     if "ln_bwd" in only:
         dmid = torch.empty_like(tok)
+        z1 = torch.randn(M, C, device=dev).to(bf)
+        dz1 = torch.empty(M, C, device=dev, dtype=bf)
         us = timeit(lambda: sp.ln_bwd(img(mid), st, g, sp.dense(da), img(dmid), M, C, add=img(tok)), args.reps)
         report("ln_bwd (fp32 x/add/dx, bf16 dy) + affine", us, M * C * 14)
         us = timeit(lambda: sp.ln_bwd(img(mid), st, g, sp.dense(da), img(dmid), M, C, add=img(tok), want_affine=False),
                     args.reps)
         report("ln_bwd, no affine partials", us, M * C * 14)
+        us = timeit(lambda: sp.ln_bwd(img(mid), st, g, sp.dense(da), img(dmid), M, C, add=img(tok),
+                                      emit=dict(out=dz1, z=z1, act=1)), args.reps)
+        report("ln_bwd + affine + emit gelu' (mixer LN2)", us, M * C * 18)
     if "act" in only:
         z = torch.randn(M, 4 * C, device=dev).to(bf)
         h = torch.empty_like(z)
