@@ -57,7 +57,9 @@ Rows = sp.Rows
 _FP32_STREAM = os.environ.get("SDPNET_TRAIN_FP32_STREAM", "1") != "0"
 # GEMM + activation fusion (sdp_gemm_train_epi): bit-identical but measured slower on the XL step
 # (856 vs 890 img/s: the exact-erf GELU runs in the tile epilogue while the MFMAs idle), so off
-_FUSED_EPI = os.environ.get("SDPNET_TRAIN_FUSED_EPI", "0") != "0"
+_FUSED_EPI_MODE = os.environ.get("SDPNET_TRAIN_FUSED_EPI", "0")  # 0 off, 1 both, fwd, bwd (A/B)
+_FUSED_EPI_FWD = _FUSED_EPI_MODE in ("1", "fwd")
+_FUSED_EPI_BWD = _FUSED_EPI_MODE in ("1", "bwd")
 
 
 def set_fp32_stream(on: bool) -> None:
@@ -141,7 +143,7 @@ def _linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], dt,
     N = w.shape[0]
     z = _empty((M, N), dt, x.device)
     h = _empty((M, N), dt, x.device)
-    if _FUSED_EPI and dt == torch.bfloat16 and sp.gemm_train_epi(1, x, w, z, M, N, K, bias=b, y2=h, act=act, p=p,
+    if _FUSED_EPI_FWD and dt == torch.bfloat16 and sp.gemm_train_epi(1, x, w, z, M, N, K, bias=b, y2=h, act=act, p=p,
                                                                 seed=seed):
         return z, h
     sp.gemm(_dense(x), w, _dense(z), M, N, K, bias=b)
@@ -156,7 +158,7 @@ def _dgrad_act(dy: torch.Tensor, w: torch.Tensor, z: torch.Tensor, act: int, p: 
     takes the shape (bit-identical to _dgrad + act_bwd)."""
     M, N = dy.shape
     K = w.shape[1]
-    if _FUSED_EPI and sp.gemm_variant(dy.dtype, M, K, N) == 1:
+    if _FUSED_EPI_BWD and sp.gemm_variant(dy.dtype, M, K, N) == 1:
         dz = _empty((M, K), dy.dtype, dy.device)
         if sp.gemm_train_epi(2, dy, wt if wt is not None else sp.transpose(w), dz, M, K, N, z=z, act=act, p=p,
                              seed=seed):
