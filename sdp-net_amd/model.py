@@ -36,6 +36,9 @@ from training_utilities import KeLu
 # torch.compile of a training model: "layer" (default) = one custom op per sub-layer (DDP's
 # bucket all-reduce overlaps the compiled backward), "model" = one op pair for the whole model
 _COMPILE_TRAIN_OPS = os.environ.get("SDPNET_COMPILE_TRAIN_OPS", "layer")
+# bf16 eval forward with autocast's fp32 residual stream (training_tools.py:85): model.eval_fp32_stream
+# = True, or this default for every model
+_EVAL_FP32_STREAM = os.environ.get("SDPNET_EVAL_FP32_STREAM", "0") != "0"
 
 torch.set_float32_matmul_precision('high')  # model.py:9 (import side effect kept)
 
@@ -183,7 +186,22 @@ class MainModel(SdPModel):
             return torch.ops.sdpnet.main_forward(x, self._sdp_handle, num_registers, code)
         if _hooked(self):
             return self._forward_modules(x, num_registers, return_raw_outputs)
+        if self._fp32_stream_eval(x):
+            import sdpnet_train
+            return sdpnet_train.eval_forward(self, x, num_registers, return_raw_outputs)
         return self._fused_forward(x, num_registers, compute_dtype(x, self), return_raw_outputs)
+
+    def _fp32_stream_eval(self, x: torch.Tensor) -> bool:
+        """bf16 eval forward along the training forward's kernels with the residual stream (the token
+        rows between sub-layers) in fp32, as torch.autocast keeps it (training_tools.py:85; residual adds
+        layers.py:102-103, :303, :309), bf16 GEMM operands, no dropout / drop path
+        (sdpnet_train.eval_forward).  Opt-in (model.eval_fp32_stream = True or
+        SDPNET_EVAL_FP32_STREAM=1): the fused forward keeps the stream in bf16, ~2.3x the reference's own
+        autocast logit error at M and faster."""
+        on = getattr(self, "eval_fp32_stream", None)
+        if on is None:
+            on = _EVAL_FP32_STREAM
+        return bool(on) and x.is_cuda and compute_dtype(x, self) == torch.bfloat16
 
     def _fused_forward(self, x: torch.Tensor, num_registers: int, dt, return_raw_outputs: bool):
         with torch.no_grad():

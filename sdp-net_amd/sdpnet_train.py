@@ -451,7 +451,13 @@ def _mixer_params(m) -> List[Optional[nn.Parameter]]:
             m.layer_norm_2.gamma, m.layer_norm_2.beta, up.weight, up.bias, dn.weight, dn.bias]
 
 
+# set by eval_forward: the training forward's kernels without dropout / drop path (eval semantics)
+_NO_DROP = False
+
+
 def _drop_p(module) -> float:
+    if _NO_DROP:
+        return 0.0
     return float(module.p) if hasattr(module, "p") else 0.0
 
 
@@ -609,8 +615,8 @@ class _EncoderFn(torch.autograd.Function):
         T = B * N
         dev = tok.device
         act = act_code(e.activation)
-        p_ff = float(e.dropout.p)
-        p_att = float(e.att_dropout) if e.fast_att else p_ff  # manual path drops with self.dropout (:297)
+        p_ff = 0.0 if _NO_DROP else float(e.dropout.p)
+        p_att = float(e.att_dropout) if e.fast_att and not _NO_DROP else p_ff  # manual path drops with self.dropout (:297)
         qn = qg is not None
         pq, po, p1, p2 = _wprep(("qkv", id(wq)), dt), _wprep(id(wo), dt), _wprep(id(w1), dt), _wprep(id(w2), dt)
         wqkv = pq[0] if pq else as_dtype(torch.cat([f32(wq), f32(wk), f32(wv)], 0), dt)
@@ -863,7 +869,7 @@ class _HeadFn(torch.autograd.Function):
             ctx.st, ctx.has = st, [p is not None for p in params]
             return z1
         drop = [mm for mm in head.output_head if isinstance(mm, nn.Dropout)]
-        pd = float(drop[0].p) if drop else 0.0
+        pd = float(drop[0].p) if drop and not _NO_DROP else 0.0
         seed = rng.next()
         hh = _empty(z1.shape, dt, dev)
         sp.act_fwd(z1, hh, B, z1.shape[1], sp.ACT_CODES["tanh"], pd, seed)
@@ -1209,6 +1215,20 @@ def train_pos_embedding(emb, x: torch.Tensor, num_registers: int):
     ew = None if conv_emb else emb.vertical_embedding_layer.weight
     bone = emb.bone if conv_emb and isinstance(emb.bone, nn.Parameter) else None
     return _PosEmbFn.apply(x, emb, num_registers, eh, ew, bone, emb.register_embedding_layer.weight)
+
+
+def eval_forward(model, x: torch.Tensor, num_registers: int = 3, return_raw_outputs: bool = False):
+    """MainModel.forward in eval mode along the training forward's kernels (model._fp32_stream_eval):
+    the residual stream in fp32 as torch.autocast keeps it (training_tools.py:85), bf16 GEMM operands,
+    dropout and drop path off (eval semantics, utility_layers.py:16-27), no autograd state kept."""
+    global _NO_DROP
+    prev = _NO_DROP
+    _NO_DROP = True
+    try:
+        with torch.no_grad():
+            return train_forward(model, x, num_registers, return_raw_outputs)
+    finally:
+        _NO_DROP = prev
 
 
 def train_forward(model, x: torch.Tensor, num_registers: int = 3, return_raw_outputs: bool = False):

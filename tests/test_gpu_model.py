@@ -141,6 +141,35 @@ def test_canonical_error_budget(name):
     assert e16[0] <= 4 * eref[0], "bf16 error more than 4x the reference's own autocast error"
 
 
+@pytest.mark.parametrize("name", ["xxs_cf_b4", "m_cf_b2", "xl_cf_b2"])
+def test_fp32_stream_eval_matches_reference_autocast(name):
+    """The opt-in autocast-exact eval (model.eval_fp32_stream: the training forward's kernels with the
+    residual stream in fp32, bf16 GEMM operands, dropout / drop path off) against the reference's
+    fp32 logits, next to the reference's own CPU-autocast bf16 error; raw outputs too."""
+    m, meta, arr, x = get_model(name)
+    nr = meta["num_registers"]
+    ref = arr["logits"]
+    m.eval_fp32_stream = True
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(x.to(DEV), num_registers=nr)
+        yb, xo, regs = m(x.to(DEV).to(torch.bfloat16), num_registers=nr, return_raw_outputs=True)
+    finally:
+        del m.eval_fp32_stream
+    fused = _err(m(x.to(DEV).to(torch.bfloat16), num_registers=nr).float().cpu().numpy(), ref)
+    e = _err(y.float().cpu().numpy(), ref)
+    eb = _err(yb.float().cpu().numpy(), ref)
+    eref = _err(arr["logits_autocast_bf16"], ref)
+    print(f"{name}: fp32-stream eval abs {e[0]:.2e} (bf16 input {eb[0]:.2e}), fused bf16 eval {fused[0]:.2e}, "
+          f"reference autocast {eref[0]:.2e}: ratios {e[0] / eref[0]:.2f} / {fused[0] / eref[0]:.2f}")
+    assert y.dtype == torch.bfloat16 and yb.dtype == torch.bfloat16
+    assert e[0] <= BF16_TOL and eb[0] <= BF16_TOL
+    assert e[0] <= 2 * eref[0] + 1e-4, "fp32-stream eval error above twice the reference's own autocast error"
+    assert xo.shape[0] == x.shape[0] and regs.shape[0] == x.shape[0]
+    if "raw_x" in arr:
+        assert np.abs(xo.float().cpu().numpy() - arr["raw_x"]).max() <= 2e-2 * max(1, np.abs(arr["raw_x"]).max())
+
+
 def test_tanh_gelu_share_of_bf16_error():
     """The bf16 fast-GEMM epilogue uses the tanh-form GELU (declared deviation from the exact
     erf nn.GELU(), model.py:15).  Its share of the M bf16 logits error: the same forward with
