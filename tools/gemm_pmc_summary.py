@@ -7,6 +7,7 @@ gfx950 correction) against the algorithmic bytes.
   python tools/gemm_pmc_summary.py gpurun_out/gpmc [--json out.json]
 """
 import csv
+import os
 import json
 import sys
 from collections import defaultdict
@@ -20,7 +21,8 @@ NCU, PEAK = 256, 2516.6e12
 
 
 def gemm_rows(path):
-    return [r for r in csv.DictReader(open(path)) if "gemm_bf16_8ph" in r["Kernel_Name"]]
+    kname = os.environ.get("PMC_KERNEL", "gemm_bf16_8ph")
+    return [r for r in csv.DictReader(open(path)) if kname in r["Kernel_Name"]]
 
 
 def blocks(rows):
