@@ -737,21 +737,22 @@ def test_ln_bwd_fused_affine_full_grid_deterministic(monkeypatch):
     close(b1, b0, 1e-5, "dbeta")
 
 
+@pytest.mark.parametrize("C", [768, 96])
 @pytest.mark.parametrize("R", [0, 4])
-def test_register_rows_copied_in_the_row_kernels(R):
+def test_register_rows_copied_in_the_row_kernels(R, C):
     """The register-row copy jobs folded into sdp_add_ln_fwd (two destinations) and sdp_ln_bwd_fused
-    (one): register rows equal the source's, image rows are the kernels' own results."""
-    B, P, C = 3, 49, 768
+    (one): register rows equal the source's, image rows are the kernels' own results.  C = 96: the
+    one-launch forms do not apply and the wrappers' separate copies run instead."""
+    import sdpnet_train as st_
+    B, P = 3, 49
     N, M = R + P, B * P
     tok = rnd(B, N, C, seed=70)
     z = rnd(M, C, seed=71, dtype=BF)
     g, b = rnd(C, seed=72) * 0.2 + 1, rnd(C, seed=73) * 0.2
     mid, out = torch.full_like(tok, float("nan")), torch.full_like(tok, float("nan"))
-    a = torch.empty(M, C, device=DEV, dtype=BF)
-    st = torch.empty(M, 2, device=DEV)
     img = lambda t: sp.Rows(t, C, P, N, R)  # noqa: E731
-    assert sp.add_ln_fwd(sp.dense(z), img(mid), sp.dense(a), M, C, img(tok), 1e-6, g, b, st, act=1,
-                         regs=(tok, [mid, out], B, R, N) if R else None)
+    a, st = st_._add_ln_fwd(sp.dense(z), img(mid), M, C, img(tok), g, b, 1e-6, BF, act=1,
+                            regs=(tok, [mid, out], B, R, N) if R else None)
     assert torch.equal(mid[:, :R], tok[:, :R]) and torch.equal(out[:, :R], tok[:, :R])
     assert not torch.isnan(mid[:, R:]).any() and torch.isnan(out[:, R:]).all()
     da = rnd(M, C, seed=74, dtype=BF)
