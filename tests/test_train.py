@@ -211,6 +211,35 @@ def test_adamw_kernel_matches_torch_adamw_with_scaler_and_clip():
     assert float(opt_o.scaler[0]) == 65536.0 * 0.5
 
 
+@pytest.mark.gpu
+def test_adamw_gradient_address_table_reuse():
+    """AdamW.step keeps the device table of gradient addresses while they stay put: gradients updated
+    in place (same addresses, new values) and then replaced by new tensors (new addresses) both give
+    torch.optim.AdamW's parameters."""
+    import sdpnet_train
+    torch.manual_seed(4)
+    shapes = [(257, 33), (4097,), (2, 3)]
+    ps = [torch.randn(*s, device=DEV) for s in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    ours = [p.clone().requires_grad_(True) for p in ps]
+    opt_r = torch.optim.AdamW(ref, lr=2e-3, weight_decay=0.05)
+    opt_o = sdpnet_train.AdamW(ours, lr=2e-3, weight_decay=0.05)
+    for o, s in zip(ours, shapes):
+        o.grad = torch.zeros(*s, device=DEV)
+    for it in range(5):
+        gs = [torch.randn(*s, device=DEV) * 0.1 for s in shapes]
+        for r, o, g in zip(ref, ours, gs):
+            r.grad = g.clone()
+            if it < 3:
+                o.grad.copy_(g)      # same addresses: the cached table
+            else:
+                o.grad = g.clone()   # new addresses: a new table
+        opt_r.step()
+        opt_o.step(grad_scale=1.0)
+        for r, o in zip(ref, ours):
+            assert torch.allclose(r, o, atol=2e-6, rtol=1e-5), (it, (r - o).abs().max().item())
+
+
 def _torch_adamw_reference(shapes, lr=3e-3, wd=0.05, init_scale=1024.0, growth_interval=2):
     ps = [torch.randn(*sh, device=DEV) for sh in shapes]
     ref = [p.clone().requires_grad_(True) for p in ps]
