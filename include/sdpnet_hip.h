@@ -144,8 +144,8 @@ int sdp_debug_skip(int mask);
 int sdp_build_info(void);
 
 /* Tile raster of the 8-phase GEMM: M-blocks per group (consecutive blocks walk a group of
- * gm M-blocks before the next N-tile).  1 = row-major, -1 = auto (8 when N spans >= 12
- * tiles, else 1).  Results do not depend on it.  Returns the previous value. */
+ * gm M-blocks before the next N-tile).  1 = row-major, -1 = auto (4 for every shape since round 6).
+ * Results do not depend on it.  Returns the previous value. */
 int sdp_gemm_set_group_m(int gm);
 
 /* GELU form of the bf16 fast-GEMM epilogue: 0 = tanh form (default, one v_exp + one

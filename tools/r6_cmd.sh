@@ -1,5 +1,12 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-secondary --no-graph > gpurun_out/evb_0.log 2>&1 && echo "fused, no graph: $(grep -o '"value": [0-9.]*' gpurun_out/evb_0.log | head -1)"
-SDPNET_EVAL_FP32_STREAM=1 timeout -k 10 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-secondary --no-graph > gpurun_out/evb_1.log 2>&1 && echo "fp32 stream, no graph: $(grep -o '"value": [0-9.]*' gpurun_out/evb_1.log | head -1)"
-tail -3 gpurun_out/evb_1.log | cut -c1-300
+for i in 1 2; do
+  for v in -1 4; do
+    log=gpurun_out/gmx_${i}_$v.log
+    SDPNET_GEMM_GROUP_M=$v timeout -k 10 400 python bench.py --config xl --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > $log 2>&1 || { tail -5 $log; exit 1; }
+    echo "xl GROUP_M=$v: $(grep -o '"value": [0-9.]*' $log | head -1)"
+    log=gpurun_out/gmt_${i}_$v.log
+    SDPNET_GEMM_GROUP_M=$v timeout -k 10 400 python bench.py --config xl_train --steps 15 --warmup 3 --no-cpu-baseline --no-secondary > $log 2>&1 || { tail -5 $log; exit 1; }
+    echo "xlt GROUP_M=$v: $(grep -o '"value": [0-9.]*' $log | head -1)"
+  done
+done
