@@ -144,7 +144,7 @@ int sdp_debug_skip(int mask);
 int sdp_build_info(void);
 
 /* Tile raster of the 8-phase GEMM: M-blocks per group (consecutive blocks walk a group of
- * gm M-blocks before the next N-tile).  1 = row-major, -1 = auto (4 for every shape since round 6).
+ * gm M-blocks before the next N-tile).  1 = row-major, -1 = auto (since round 6: 2 below 9 N-tiles, else 4).
  * Results do not depend on it.  Returns the previous value. */
 int sdp_gemm_set_group_m(int gm);
 

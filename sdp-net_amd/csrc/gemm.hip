@@ -1521,10 +1521,11 @@ extern "C" int sdp_gemm_set_fast_kernel(int k) {  // 0 queries; an unknown id re
   return old;
 }
 
-// -1 = auto: 4 M-blocks per group for every shape (round 6: against 8 for >= 12 N-tiles and
-// row-major below, the M forward +0.4 % over five interleaved pairs, the XL forward +1.4 %, the XL
-// training step neutral; 2 / 3 / 6 / 16 measured no better, profiles/r06_gemm_raster_ab.md)
+// -1 = auto: groups of 2 M-blocks below 9 N-tiles (N = 768), 4 from 9 (round 6: against 8 from 12
+// N-tiles and row-major below, 4 everywhere gave the M forward +0.4 % and the XL forward +1.4 %, then
+// 2 for the narrow shapes another +0.4 % over five interleaved pairs; profiles/r06_gemm_raster_ab.md)
 static int g_group_m = -1;
+static inline int auto_group_m(int tiles_n) { return tiles_n < 9 ? 2 : 4; }
 extern "C" int sdp_gemm_set_group_m(int gm) {
   int old = g_group_m;
   g_group_m = gm;
@@ -1690,7 +1691,7 @@ extern "C" int sdp_gemm_train_epi(int mode, const void* X, int64_t ldx, const vo
   Epi<bf16_t> e{bias, (const bf16_t*)Z, ldz, dm, (bf16_t*)Y, ldy, dm, ACT_NONE, 0, nullptr, nullptr, nullptr};
   e.nt_store = g_nt_store;
   const int tm = (M + fast::BM - 1) / fast::BM, tn = (N + fast::BN - 1) / fast::BN;
-  e.group_m = g_group_m >= 1 ? g_group_m : 4;
+  e.group_m = g_group_m >= 1 ? g_group_m : auto_group_m(tn);
   e.out2 = (bf16_t*)Y2;
   e.ld2 = ldy2;
   e.act2 = act;
@@ -1746,10 +1747,10 @@ static int gemm_impl(int dtype, const void* X, int64_t ldx, int x_grp, int64_t x
     Epi<bf16_t> e{bias, (const bf16_t*)R, ldr, rm, (bf16_t*)Y, ldy, ym, act, resid_pre, ln_stats, ln_colsum, nullptr};
     e.nt_store = g_nt_store;
     {
-      // auto raster: groups of 4 M-blocks for every shape (round 6, g_group_m above; round 2 chose
+      // auto raster: groups of 2 / 4 M-blocks (round 6, auto_group_m above; round 2 chose
       // row-major up to 9 N-tiles and groups of 8 from 12 on the solo L2-miss count,
       // tools/raster_traffic.py, profiles/r02_gemm_probes.md -- the two-stream model prefers 4)
-      e.group_m = g_group_m >= 1 ? g_group_m : 4;
+      e.group_m = g_group_m >= 1 ? g_group_m : auto_group_m((N + fast::BN - 1) / fast::BN);
     }
     const bool aligned = (ldy % 4 == 0) && ((uintptr_t)Y % 8 == 0) && (!R || ((ldr % 4 == 0) && ((uintptr_t)R % 8 == 0))) &&
                          (!bias || ((uintptr_t)bias % 16 == 0)) && (ldx % 8 == 0) && ((uintptr_t)X % 16 == 0) &&

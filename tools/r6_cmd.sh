@@ -1,12 +1,9 @@
 set -o pipefail
 mkdir -p gpurun_out
-for i in 1 2; do
-  for v in -1 4; do
-    log=gpurun_out/gmx_${i}_$v.log
-    SDPNET_GEMM_GROUP_M=$v timeout -k 10 400 python bench.py --config xl --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > $log 2>&1 || { tail -5 $log; exit 1; }
-    echo "xl GROUP_M=$v: $(grep -o '"value": [0-9.]*' $log | head -1)"
-    log=gpurun_out/gmt_${i}_$v.log
-    SDPNET_GEMM_GROUP_M=$v timeout -k 10 400 python bench.py --config xl_train --steps 15 --warmup 3 --no-cpu-baseline --no-secondary > $log 2>&1 || { tail -5 $log; exit 1; }
-    echo "xlt GROUP_M=$v: $(grep -o '"value": [0-9.]*' $log | head -1)"
+for i in 1 2 3; do
+  for v in 4,4 2,4 2,8; do
+    log=gpurun_out/gm2_${i}_${v/,/_}.log
+    SDPNET_TMP_GM=$v timeout -k 10 400 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary > $log 2>&1 || { tail -5 $log; exit 1; }
+    echo "m GM(small,big)=$v: $(grep -o '"value": [0-9.]*' $log | head -1)"
   done
 done
